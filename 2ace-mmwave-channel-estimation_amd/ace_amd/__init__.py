@@ -1,0 +1,12 @@
+"""ace_amd -- MI355X-native 2ACE ADMM channel recovery (HIP kernels behind a C-ABI).
+
+Importing this package loads ``libace.so``; it raises if the HIP library has
+not been built (there is no CPU fallback on the product path).
+"""
+from ._lib import LIB, AceError, AdmmCfg, default_cfg  # noqa: F401
+from ._lib import (ACE_VARIANT_A2ONLY, ACE_VARIANT_NUCLEAR, ACE_ST_CONVERGED, ACE_ST_NO_OPT,  # noqa: F401
+                   ACE_ST_EIG_NOCONV)
+from .solver import InferADMM, infer_admm_batch, infer_admm_host, synth_problem, BatchResult  # noqa: F401
+from . import synth  # noqa: F401
+
+__version__ = LIB.ace_version().decode()

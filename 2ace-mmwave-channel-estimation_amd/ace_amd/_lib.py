@@ -1,0 +1,100 @@
+"""ctypes binding of libace.so (the C-ABI declared in include/ace.h).
+
+The product path has no CPU fallback: if the HIP library is missing this
+module raises at import time, and every solver entry point goes through it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = pathlib.Path(os.environ.get("ACE_LIB", _HERE / "libace.so"))
+
+ACE_OK = 0
+ACE_ERR_ARG = -1
+ACE_ERR_UNSUPPORTED = -2
+ACE_ERR_HIP = -3
+ACE_ERR_WORKSPACE = -4
+
+ACE_VARIANT_A2ONLY = 0
+ACE_VARIANT_NUCLEAR = 1
+
+ACE_ST_CONVERGED = 1
+ACE_ST_NO_OPT = 2
+ACE_ST_EIG_NOCONV = 4
+
+
+class AceError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"ace error {code}: {msg}")
+        self.code = code
+
+
+class AdmmCfg(C.Structure):
+    """Mirror of ``ace_admm_cfg`` (include/ace.h)."""
+    _fields_ = [
+        ("variant", C.c_int),
+        ("scale_by_row", C.c_int),
+        ("use_rank_one", C.c_int),
+        ("maxiter", C.c_int),
+        ("fixed_iters", C.c_int),
+        ("a_shared", C.c_int),
+        ("eig_warm", C.c_int),
+        ("reserved", C.c_int),
+        ("mu0", C.c_double),
+        ("rho", C.c_double),
+        ("tol_rel", C.c_double),
+        ("tol_abs", C.c_double),
+    ]
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"ace_amd: HIP library {LIB_PATH} not found -- build it with "
+            f"`make -C 2ace-mmwave-channel-estimation_amd/csrc` (or __graft_entry__.build()). "
+            f"There is no CPU fallback on the product path.")
+    lib = C.CDLL(str(LIB_PATH))
+    vp, dp, ip, up = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_uint32)
+    cfgp = C.POINTER(AdmmCfg)
+    lib.ace_admm_cfg_default.argtypes = [cfgp]
+    lib.ace_admm_cfg_default.restype = None
+    lib.ace_admm_workspace_size.argtypes = [cfgp, C.c_int, C.c_int, C.c_int]
+    lib.ace_admm_workspace_size.restype = C.c_size_t
+    lib.ace_admm_solve_batch.argtypes = [cfgp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_size_t, vp]
+    lib.ace_admm_solve_batch.restype = C.c_int
+    lib.ace_admm_solve_host.argtypes = [cfgp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        dp, dp, dp, dp, dp, ip, up, dp]
+    lib.ace_admm_solve_host.restype = C.c_int
+    lib.ace_synth_codebook.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, vp, vp]
+    lib.ace_synth_codebook.restype = C.c_int
+    lib.ace_synth_channels.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_double, C.c_double, vp, C.c_int, vp, vp, vp, vp]
+    lib.ace_synth_channels.restype = C.c_int
+    lib.ace_last_error.argtypes = []
+    lib.ace_last_error.restype = C.c_char_p
+    lib.ace_version.argtypes = []
+    lib.ace_version.restype = C.c_char_p
+    return lib
+
+
+LIB = _load()
+
+
+def check(rc):
+    if rc != ACE_OK:
+        raise AceError(rc, LIB.ace_last_error().decode())
+    return rc
+
+
+def default_cfg(**kw) -> AdmmCfg:
+    cfg = AdmmCfg()
+    LIB.ace_admm_cfg_default(C.byref(cfg))
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise TypeError(f"unknown ace_admm_cfg field {k!r}")
+        setattr(cfg, k, v)
+    return cfg

@@ -1,0 +1,128 @@
+/*
+ * ace.h -- C-ABI of the MI355X-native 2ACE ADMM channel-recovery hot path.
+ *
+ * Reference interfaces replaced (reference root: gavinsyw/2ACE-mmWave-Channel-Estimation):
+ *
+ *  ace_admm_solve_batch   <- [X,Y,converged] = InferADMM(A,B,X0,scale_by_row,use_rank_one,
+ *                            tx,rx,lambda,mu0,rho,tol_rel,tol_abs,maxiter,U,D)
+ *                            main/src/my_recovery_algorithms/ADMM_v2/inferLowRankV4_multi.m:281
+ *                            (A2only Z-prox :423-485) and inferLowRank_Nuclear.m:269
+ *                            (nuclear Z-prox :411-439).  One call solves a batch of
+ *                            independent realisations; the refinement stage called at
+ *                            inferLowRankV4_multi.m:92 / :100 is r = 1, scale_by_row = 1.
+ *  ace_admm_solve_host    <- the same, on host arrays (drop-in for MATLAB Engine calls
+ *                            that pass matlab.double buffers; main/main.py:427-437).
+ *  ace_synth_*            <- synthetic trace generation with the semantics of
+ *                            main/src/generate_channel/Generate_Channel.m:64-164,
+ *                            generate_sensing_matrix/Generate_Sensing_Matrix.m:85-122
+ *                            ('Random_Phase_State') and
+ *                            generate_measurement/Generate_Measurement.m:67-136.
+ *
+ * Conventions
+ *  - Complex values are complex128, interleaved (re, im) doubles.
+ *  - A is row-major [a_shared ? 1 : batch][m][n]; n = tx*rx with the
+ *    column-major vec(H) ordering of the reference (element k = i + tx*j).
+ *  - Per-realisation vectors are realisation-major: B[batch][m] (f64),
+ *    X0/X[batch][n] (c128), Y[batch][m] (c128).
+ *  - All pointers passed to ace_admm_solve_batch / ace_synth_* are DEVICE
+ *    pointers; the caller owns every buffer (no allocation crosses the ABI).
+ *    The workspace must be ace_admm_workspace_size() bytes, 256-B aligned.
+ *  - `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *    asynchronous on that stream except where noted; they are re-entrant per
+ *    stream (no global mutable state besides the thread-local error text).
+ *  - Return value 0 = success, negative = error; ace_last_error() returns a
+ *    thread-local description of the last error on this thread.
+ */
+#ifndef ACE_H_
+#define ACE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACE_OK 0
+#define ACE_ERR_ARG -1        /* invalid argument / shape */
+#define ACE_ERR_UNSUPPORTED -2 /* configuration outside the implemented scope */
+#define ACE_ERR_HIP -3        /* HIP runtime error */
+#define ACE_ERR_WORKSPACE -4  /* workspace too small */
+
+#define ACE_VARIANT_A2ONLY 0  /* inferLowRankV4_multi.m ArgMinZ (rank-profile tail rescale) */
+#define ACE_VARIANT_NUCLEAR 1 /* inferLowRank_Nuclear.m ArgMinZ (singular-value soft threshold) */
+
+/* status bits per realisation */
+#define ACE_ST_CONVERGED 1u   /* convergence test (inferLowRankV4_multi.m:372) passed */
+#define ACE_ST_NO_OPT 2u      /* objective never finite: returned last iterate (reference would raise) */
+#define ACE_ST_EIG_NOCONV 4u  /* Z-prox Jacobi hit its sweep cap at least once */
+
+typedef struct ace_admm_cfg {
+    int variant;       /* ACE_VARIANT_* */
+    int scale_by_row;  /* 1: row-wise magnitude step (refinement); at r = 1 both modes coincide */
+    int use_rank_one;  /* ArgMinZ rank profile [1] / [0.95] (inferLowRankV4_multi.m:448-450) */
+    int maxiter;       /* 500 in the reference (:13) */
+    int fixed_iters;   /* 1: throughput mode -- run exactly maxiter iterations (no early exit) */
+    int a_shared;      /* 1: one A for the whole batch (shared codebook); 0: private A per realisation */
+    int eig_warm;      /* 1: warm-start the Z-prox Jacobi from the previous iteration's eigenvectors */
+    int reserved;
+    double mu0;        /* 1e-3   (:7) */
+    double rho;        /* 1.03   (:8) */
+    double tol_rel;    /* 1e-4   (:10) */
+    double tol_abs;    /* 1e-8   (:11) */
+} ace_admm_cfg;
+
+/* Fill cfg with the reference defaults (inferLowRankV4_multi.m:6-14), variant A2only,
+ * refinement stage (scale_by_row = 1), shared A, convergence enabled. */
+void ace_admm_cfg_default(ace_admm_cfg* cfg);
+
+/* Workspace bytes needed by ace_admm_solve_batch for this problem. */
+size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n);
+
+/* Batched InferADMM at r = 1 on device buffers.
+ *   A      [a_shared?1:batch][m][n] c128      sensing matrix (codebook rows)
+ *   B      [batch][m] f64                     RSS magnitudes
+ *   X0     [batch][n] c128                    initial iterate
+ *   X, Y   [batch][n] / [batch][m] c128 out   best-objective iterate (opt_X, opt_Y)
+ *   iters  [batch] int32 out (may be NULL)    iterations run
+ *   status [batch] uint32 out (may be NULL)   ACE_ST_* bits
+ *   mu     [batch] f64 out (may be NULL)      final penalty mu
+ * Constraints: n == tx*rx, tx <= 32, rx <= 32 (tx, rx in {4,8,16,32} in the reference),
+ * m >= 1.  Returns once all kernels are enqueued; in convergence mode
+ * (fixed_iters == 0) the host polls a device flag every few iterations and so
+ * synchronises `stream` periodically. */
+int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx,
+                         const double* A, const double* B, const double* X0,
+                         double* X, double* Y, int32_t* iters, uint32_t* status, double* mu,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* Host-pointer convenience wrapper: allocates device memory, copies in, solves,
+ * copies out, frees.  Synchronous. */
+int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx,
+                        const double* A, const double* B, const double* X0,
+                        double* X, double* Y, int32_t* iters, uint32_t* status, double* mu);
+
+/* Synthetic traces (device).  Counter-based RNG (splitmix64 of seed/stream/counter),
+ * identical integer streams to ace_amd.synth on the host.
+ *   ace_synth_codebook: A[count][m][n] c128 with entries exp(j*pi/2*k)/sqrt(n),
+ *     k ~ U{0..3}; realisation index base `first` (private A) -- for a shared codebook
+ *     pass count = 1, first = -1.
+ *   ace_synth_channels: for realisations first..first+count-1: vecH [count][n] c128
+ *     (L paths, AoD/AoA ~ U(-47.5deg, 47.5deg), CN gains normalised), B = |A vecH + w|
+ *     with w ~ CN(0, 10^(-snr_db/10)), and X0 = vecH + x0_noise * ||vecH||/sqrt(n) * CN(0,1).
+ *     A is [a_shared?1:count][m][n]. */
+int ace_synth_codebook(uint64_t seed, int64_t first, int count, int m, int n, double* A, void* stream);
+int ace_synth_channels(uint64_t seed, int64_t first, int count, int m, int tx, int rx, int L,
+                       double snr_db, double x0_noise, const double* A, int a_shared,
+                       double* vecH, double* B, double* X0, void* stream);
+
+/* Last error text for this thread ("" if none). */
+const char* ace_last_error(void);
+
+/* Library version string. */
+const char* ace_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACE_H_ */

@@ -25,6 +25,8 @@ ACE_ST_CONVERGED = 1
 ACE_ST_NO_OPT = 2
 ACE_ST_EIG_NOCONV = 4
 
+KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final"]
+
 
 class AceError(RuntimeError):
     def __init__(self, code, msg):
@@ -74,6 +76,10 @@ def _load():
     lib.ace_synth_channels.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.c_double, C.c_double, vp, C.c_int, vp, vp, vp, vp]
     lib.ace_synth_channels.restype = C.c_int
+    lib.ace_prof_start.argtypes = [C.c_int]
+    lib.ace_prof_start.restype = C.c_int
+    lib.ace_prof_stop.argtypes = [dp, ip]
+    lib.ace_prof_stop.restype = C.c_int
     lib.ace_last_error.argtypes = []
     lib.ace_last_error.restype = C.c_char_p
     lib.ace_version.argtypes = []

@@ -108,6 +108,29 @@ size_t carve(const ace_admm_cfg* c, int batch, int m, int n, int tx, char* base,
     return off;
 }
 
+// ---- event-pair kernel timing (ace_prof_start / ace_prof_stop)
+struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> ev;   // 2 per record
+    std::vector<int> cls;
+    size_t used = 0;
+} g_prof;
+
+struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
+    hipStream_t st;
+    int idx = -1;
+    ProfScope(int c, hipStream_t s) : st(s) {
+        if (g_prof.on && g_prof.used < g_prof.cls.size()) {
+            idx = (int)g_prof.used++;
+            g_prof.cls[idx] = c;
+            (void)hipEventRecord(g_prof.ev[2 * idx], st);
+        }
+    }
+    ~ProfScope() {
+        if (idx >= 0) (void)hipEventRecord(g_prof.ev[2 * idx + 1], st);
+    }
+};
+
 int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
     if (!c) return fail(ACE_ERR_ARG, "cfg is NULL");
     if (batch < 1 || m < 1 || n < 1) return fail(ACE_ERR_ARG, "batch/m/n must be >= 1 (got %d/%d/%d)", batch, m, n);
@@ -127,6 +150,40 @@ extern "C" {
 
 const char* ace_last_error(void) { return g_err.c_str(); }
 const char* ace_version(void) { return "ace-mi355x 0.1.0 (gfx950)"; }
+
+int ace_prof_start(int max_launches) {
+    g_err.clear();
+    if (max_launches < 1) return fail(ACE_ERR_ARG, "max_launches must be >= 1");
+    for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
+    g_prof.ev.assign(2 * (size_t)max_launches, nullptr);
+    for (auto& e : g_prof.ev) ACE_HIP(hipEventCreate(&e));
+    g_prof.cls.assign(max_launches, 0);
+    g_prof.used = 0;
+    g_prof.on = true;
+    return ACE_OK;
+}
+
+int ace_prof_stop(double* total_ms, int32_t* launches) {
+    g_err.clear();
+    g_prof.on = false;
+    for (int c = 0; c < ACE_NKCLASS; ++c) {
+        if (total_ms) total_ms[c] = 0.0;
+        if (launches) launches[c] = 0;
+    }
+    for (size_t i = 0; i < g_prof.used; ++i) {
+        ACE_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+        float ms = 0.f;
+        ACE_HIP(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+        const int c = g_prof.cls[i];
+        if (total_ms) total_ms[c] += ms;
+        if (launches) launches[c] += 1;
+    }
+    for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
+    g_prof.ev.clear();
+    g_prof.cls.clear();
+    g_prof.used = 0;
+    return ACE_OK;
+}
 
 void ace_admm_cfg_default(ace_admm_cfg* c) {
     std::memset(c, 0, sizeof *c);
@@ -168,11 +225,14 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
 
     // ---- setup: K = A A^H, G = (I + K)^{-1}, A^H (shared regime)
     const int mats = shared ? 1 : batch;
+    {
+    ProfScope ps(ACE_K_SETUP, st);
     // K[j][i] = sum_k conj(A[i][k]) A[j][k]  : GEMM with L = conj(A), V = rows of A
     launch_zgemm(0, true, m, n, m, A, n, mn, A, n, mn, w.K, nullptr, m, mm, mats, st);
     ACE_HIP(hipMemcpyAsync(w.G, w.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
     launch_inv_ipk(m, mats, w.G, mm, st);
     if (shared) launch_conj_transpose(m, n, A, w.AH, st);
+    }
     ACE_HIP(hipGetLastError());
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
@@ -210,28 +270,31 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
 
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
-    applyA(0, X0, w.T, nullptr);                                 // AX = A*X0
-    launch_init(n, m, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, cfg->mu0, st);
-    za.it = 0;
-    launch_zstep(cfg->variant, true, za, batch, st);             // Z = ArgMinZ(X, N=0, mu=1)
-    applyMM(w.K, w.Y[0], w.KY[0]);                               // K*Y (for A'*Y terms)
+    {
+        ProfScope ps(ACE_K_INIT, st);
+        applyA(0, X0, w.T, nullptr);                             // AX = A*X0
+        launch_init(n, m, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, cfg->mu0, st);
+        za.it = 0;
+        launch_zstep(cfg->variant, true, za, batch, st);         // Z = ArgMinZ(X, N=0, mu=1)
+        applyMM(w.K, w.Y[0], w.KY[0]);                           // K*Y (for A'*Y terms)
+    }
     ACE_HIP(hipGetLastError());
 
     int p = 0;
     const int poll = 8;
     for (int it = 1; it <= cfg->maxiter; ++it) {
-        launch_pre(n, m, batch, w.Z, w.N, w.Y[p], w.M, w.V, w.S, w.st, st);
-        applyA(1, w.V, w.T, w.S);                                // T = S - A V
-        applyMM(w.G, w.T, w.g);                                  // g = G T
-        launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[p], w.Y[1 - p], w.st, st);
-        applyMM(w.K, w.Y[1 - p], w.KY[1 - p]);                   // K Y
-        applyAH(w.g, w.X, w.V);                                  // X = V + A^H g
+        { ProfScope ps(ACE_K_PRE, st); launch_pre(n, m, batch, w.Z, w.N, w.Y[p], w.M, w.V, w.S, w.st, st); }
+        { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }          // T = S - A V
+        { ProfScope ps(ACE_K_APPLY_G, st); applyMM(w.G, w.T, w.g); }            // g = G T
+        { ProfScope ps(ACE_K_YSTEP, st); launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[p], w.Y[1 - p], w.st, st); }
+        { ProfScope ps(ACE_K_APPLY_K, st); applyMM(w.K, w.Y[1 - p], w.KY[1 - p]); }  // K Y
+        { ProfScope ps(ACE_K_APPLY_AH, st); applyAH(w.g, w.X, w.V); }           // X = V + A^H g
         za.it = it;
         za.Ynew = w.Y[1 - p];
         za.Yold = w.Y[p];
         za.KYnew = w.KY[1 - p];
         za.KYold = w.KY[p];
-        launch_zstep(cfg->variant, false, za, batch, st);
+        { ProfScope ps(ACE_K_ZSTEP, st); launch_zstep(cfg->variant, false, za, batch, st); }
         p = 1 - p;
         if (!cfg->fixed_iters && (it % poll == 0) && it < cfg->maxiter) {
             int h_done = 0;
@@ -241,7 +304,10 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
         }
     }
     ACE_HIP(hipGetLastError());
-    launch_finalize(n, m, batch, w.optX, w.optY, w.X, w.Y[p], Xo, Yo, iters, status, mu_out, w.st, st);
+    {
+        ProfScope ps(ACE_K_FINAL, st);
+        launch_finalize(n, m, batch, w.optX, w.optY, w.X, w.Y[p], Xo, Yo, iters, status, mu_out, w.st, st);
+    }
     ACE_HIP(hipGetLastError());
     return ACE_OK;
 }

@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: channel recoveries/s of the 2ACE ADMM hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): 32-antenna (tx = rx = 32,
+n = 1024) channels, m = 256 random-codebook RSS measurements, A2only ADMM.
+One recovery = one InferADMM refinement solve (inferLowRankV4_multi.m:281-386
+called at :92 -- r = 1, scale_by_row, mu0 = 1e-3, rho = 1.03) with exactly 200
+iterations (the convergence test is evaluated every iteration; early exit off).
+A step = one batch of 4096 recoveries per GPU sharing one codebook (regime S),
+including the per-batch setup (K = A A^H, (I+K)^-1); inputs are synthetic
+(Generate_Channel / Random_Phase_State / Generate_Measurement semantics) and
+already resident in HBM when the timed region starts.  With N GPUs each rank
+solves its own 4096 realisations (weak scaling) and the recovered channels are
+gathered to rank 0 over RCCL inside the timed region.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "2ace-mmwave-channel-estimation_amd"))
+
+METRIC = "channel recoveries/sec (32-ant, 256 RSS meas, 200 ADMM iters) @1/2/4/8 GPU"
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= FP64 vector) dense peak, spec
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=4096, help="recoveries per GPU per step")
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--variant", default="A2only", choices=["A2only", "A2nuclear"])
+    ap.add_argument("--private", action="store_true", help="private codebook per realisation (regime P)")
+    ap.add_argument("--tx", type=int, default=32)
+    ap.add_argument("--m", type=int, default=256)
+    ap.add_argument("--seed", type=int, default=58659179)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
+    ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
+    return ap.parse_args()
+
+
+def unit_flops(m, n, tx, rx):
+    """Algorithmic flops per kernel launch class per realisation per iteration (complex MAC = 8)."""
+    return {
+        "apply_A": 8.0 * m * n,
+        "apply_G": 8.0 * m * m,
+        "apply_K": 8.0 * m * m,
+        "apply_AH": 8.0 * n * m,
+        "zstep": 8.0 * 3 * tx * tx * rx,   # E E^H + U diag U^H E (3 s^3), eig excluded
+    }
+
+
+def cpu_baseline(args, n_samples):
+    """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
+    timed on the host cores on a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ace_oracle_c as OC
+    from ace_amd import synth
+    tx = args.tx
+    n = tx * tx
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not args.private)
+    t0 = time.perf_counter()
+    U = OC.make_U(A[0], nthreads=cores)
+    t_setup = time.perf_counter() - t0
+    var = 0 if args.variant == "A2only" else 1
+    t0 = time.perf_counter()
+    OC.infer_admm_r1_batch(A[:1], U[None], B, X0, tx, tx, variant=var, fixed_iters=True, maxiter=args.iters,
+                           nthreads=cores)
+    t_solve = time.perf_counter() - t0
+    # setup amortised over a full GPU-sized batch, as on the GPU
+    t_total = t_solve + t_setup * n_samples / args.batch
+    return {"value": n_samples / t_total, "unit": "recoveries/s", "cores": cores, "kind": "port",
+            "sample": (f"{n_samples} recoveries of the same workload ({args.iters} fixed iters, m={args.m}, "
+                       f"n={n}, shared codebook) on {cores} threads of "
+                       f"{_cpu_model()}; U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}; "
+                       f"solve {t_solve:.2f}s")}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    import ace_amd
+    from ace_amd import infer_admm_batch, synth_problem
+    from ace_amd._lib import LIB, KERNEL_CLASSES, check
+    import ctypes as C
+
+    tx = args.tx
+    n, m, bsz = tx * tx, args.m, args.batch
+    A, B, X0, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, a_shared=not args.private, device=dev)
+    ws = ace_amd.solver.Workspace()
+    out = None
+    gather_buf = None
+    if world > 1 and rank == 0:
+        gather_buf = [torch.empty((bsz, n), dtype=torch.complex128, device=dev) for _ in range(world)]
+
+    def step():
+        nonlocal out
+        out = infer_admm_batch(A, B, X0, tx, tx, variant=args.variant, maxiter=args.iters, fixed_iters=True,
+                               out=out, workspace=ws)
+        if world > 1:   # the single result gather over RCCL/xGMI (north_star)
+            dist.gather(out.X, gather_list=gather_buf if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = not args.no_prof
+    if prof:
+        check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = (C.c_double * 10)()
+    kn = (C.c_int32 * 10)()
+    if prof:
+        check(LIB.ace_prof_stop(kt, kn))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    it_ok = bool((out.iters == args.iters).all().item())
+    finite = bool(torch.isfinite(torch.view_as_real(out.X)).all().item())
+
+    if rank == 0:
+        total = world * bsz * args.steps
+        value = total / elapsed
+        kernels = {}
+        roof = None
+        if prof:
+            uf = unit_flops(m, n, tx, tx)
+            for i, name in enumerate(KERNEL_CLASSES):
+                if kn[i]:
+                    kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
+            dom = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["total_ms"])
+            per_launch_flops = uf[dom] * bsz
+            achieved = per_launch_flops / (kernels[dom]["avg_ms"] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None, "kernel": dom,
+                    "flops_per_launch": per_launch_flops,
+                    "note": "FP64 dense peak (matrix = vector on MI355X); traffic: see profiles/ PMC summary"}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            ns = args.cpu_recoveries or 256
+            cpu = cpu_baseline(args, ns)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "recoveries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Generate_Channel/Random_Phase_State/Generate_Measurement semantics, 30 dB SNR)",
+            "config": {
+                "workload": ("config 2: 32-ant URA (n=1024), 256 random-codebook RSS meas, A2only ADMM "
+                             "refinement solve (r=1), 200 fixed iterations" if args.variant == "A2only" and tx == 32
+                             else f"{args.variant}, tx=rx={tx}, m={m}, {args.iters} fixed iterations"),
+                "variant": args.variant,
+                "codebook": "private per realisation (regime P)" if args.private else "shared (regime S)",
+                "batch_per_gpu": bsz,
+                "global_batch": world * bsz,
+                "m": m, "n": n, "iters": args.iters,
+                "parallelism": f"dp{world} (realisation sharding, RCCL gather of X to rank 0)",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+            "checks": {"all_iters_ran": it_ok, "finite": finite},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

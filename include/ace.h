@@ -116,6 +116,25 @@ int ace_synth_channels(uint64_t seed, int64_t first, int count, int m, int tx, i
                        double snr_db, double x0_noise, const double* A, int a_shared,
                        double* vecH, double* B, double* X0, void* stream);
 
+/* ---- kernel timing (measurement only; no reference counterpart) ----------------
+ * Between ace_prof_start and ace_prof_stop every kernel ace_admm_solve_batch
+ * enqueues is bracketed by a pair of hipEvents recorded on the launch stream.
+ * ace_prof_stop waits for the events and returns, per kernel class, the summed
+ * device time (ms) and the number of launches.  Process-global; not thread-safe. */
+#define ACE_K_SETUP 0    /* K = A A^H, (I+K)^{-1}, A^H */
+#define ACE_K_INIT 1     /* A X0, init, initial Z-prox, K Y */
+#define ACE_K_PRE 2      /* V = Z - N/mu, S = Y - M/mu */
+#define ACE_K_APPLY_A 3  /* T = S - A V */
+#define ACE_K_APPLY_G 4  /* g = G T */
+#define ACE_K_YSTEP 5    /* ArgMinY, M update, reductions */
+#define ACE_K_APPLY_K 6  /* K Y */
+#define ACE_K_APPLY_AH 7 /* X = V + A^H g */
+#define ACE_K_ZSTEP 8    /* ArgMinZ, N update, residuals, stop test */
+#define ACE_K_FINAL 9
+#define ACE_NKCLASS 10
+int ace_prof_start(int max_launches);
+int ace_prof_stop(double* total_ms, int32_t* launches);
+
 /* Last error text for this thread ("" if none). */
 const char* ace_last_error(void);
 

@@ -21,18 +21,98 @@ constexpr int TXMAX = 32;
 constexpr int HS = TXMAX + 1;  // LDS row stride (complex) for 32x32 tiles
 constexpr int MAX_SWEEPS = 40;
 
-// Circle-method pairing: step s of n-1, pair k of n/2 -> (p, q) with p < q.
-__device__ __forceinline__ void rr_pair(int n, int s, int k, int& p, int& q) {
-    int a, b;
-    if (k == 0) {
-        a = n - 1;
-        b = s;
-    } else {
-        a = (s + k) % (n - 1);
-        b = (s - k + (n - 1)) % (n - 1);
+// upper-triangular enumeration of the 16x16 slot-pair blocks (ka <= kb)
+__constant__ unsigned char c_tri_a[136] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,2,2,2,2,2,2,2,2,2,2,2,2,2,2,3,3,3,3,3,3,3,3,3,3,3,3,3,4,4,4,4,4,4,4,4,4,4,4,4,5,5,5,5,5,5,5,5,5,5,5,6,6,6,6,6,6,6,6,6,6,7,7,7,7,7,7,7,7,7,8,8,8,8,8,8,8,8,9,9,9,9,9,9,9,10,10,10,10,10,10,11,11,11,11,11,12,12,12,12,13,13,13,14,14,15};
+__constant__ unsigned char c_tri_b[136] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,2,3,4,5,6,7,8,9,10,11,12,13,14,15,3,4,5,6,7,8,9,10,11,12,13,14,15,4,5,6,7,8,9,10,11,12,13,14,15,5,6,7,8,9,10,11,12,13,14,15,6,7,8,9,10,11,12,13,14,15,7,8,9,10,11,12,13,14,15,8,9,10,11,12,13,14,15,9,10,11,12,13,14,15,10,11,12,13,14,15,11,12,13,14,15,12,13,14,15,13,14,15,14,15,15};
+
+// Jacobi rotation J = [[cs, sn], [-sn e*, cs e*]] annihilating h_pq of the Hermitian
+// 2x2 block [[ap, c], [c*, aq]] (c = |c| e): tan(theta) = t with
+// t = sign(aq - ap) 2|c| / (|aq - ap| + sqrt((aq - ap)^2 + 4|c|^2)).
+struct Rot {
+    double cs, sn;
+    d2 e;
+    bool on;
+};
+// v_rsq_f64 / v_rcp_f64 seeds refined by two Newton steps (~1 ulp); operands are
+// positive and finite here (guarded by the rotation threshold).
+__device__ __forceinline__ double frsq(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
+    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
+    return y;
+}
+__device__ __forceinline__ double frcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return y;
+}
+// rotate pair (p,q) unless |h_pq| is negligible: |h_pq| <= 1e-18 tr(H) (absolute, below
+// LAPACK's normwise eps) or |h_pq|^2 <= 1e-32 |h_pp h_qq| (relative, the classical
+// Jacobi test)
+__device__ __forceinline__ bool needs_rot(double ap, double aq, d2 c, double abs_tol) {
+    const double ac2 = cabs2(c);
+    return ac2 > abs_tol * abs_tol && ac2 > 1e-32 * fabs(ap * aq) && ac2 > 1e-300;
+}
+__device__ __forceinline__ Rot make_rot(double ap, double aq, d2 c, double abs_tol) {
+    Rot r{1.0, 0.0, make_double2(1.0, 0.0), false};
+    const double ac2 = cabs2(c);
+    if (needs_rot(ap, aq, c, abs_tol)) {
+        const double ir = frsq(ac2), ac = ac2 * ir;
+        r.e = make_double2(c.x * ir, c.y * ir);
+        const double d = aq - ap;
+        const double q = fma(d, d, 4.0 * ac2);
+        const double D = q * frsq(q);
+        double tt = 2.0 * ac * frcp(fabs(d) + D);
+        if (d < 0.0) tt = -tt;
+        r.cs = frsq(fma(tt, tt, 1.0));
+        r.sn = tt * r.cs;
+        r.on = true;
     }
-    p = a < b ? a : b;
-    q = a < b ? b : a;
+    return r;
+}
+
+// Packed upper-triangular index of (i, j), i <= j < 32 (528 entries).
+__device__ __forceinline__ int up_idx(int i, int j) { return i * 32 - ((i * (i - 1)) >> 1) + (j - i); }
+
+// Circle-method position map for n (even) positions with pairs (2k, 2k+1): position
+// 0 is fixed, the "top" elements 2k move right, the "bottom" elements 2k+1 move left.
+__device__ __forceinline__ int circ_next(int n, int p) {
+    if (n == 2) return p;
+    const int P = n >> 1;
+    if (p == 0) return 0;
+    if (p == 1) return 2;
+    if ((p & 1) == 0) return (p == 2 * P - 2) ? 2 * P - 1 : p + 2;
+    return p - 2;
+}
+
+// 32x32 complex product from LDS tiles (row stride HS) on the f64 matrix cores:
+// C = opA(A) * opB(B), op = identity or conjugate transpose.  Wave w computes the
+// 16x16 block rows [16*(w>>1), +16) x cols [16*(w&1), +16); real and imaginary
+// parts accumulate in separate 16x16 f64 tiles (4 real MFMAs per complex k-step).
+template <bool CTA, bool CTB>
+__device__ __forceinline__ void mm32(const d2* A, const d2* B, d4v& cr, d4v& ci, int lane, int w) {
+    const int i0 = 16 * (w >> 1), j0 = 16 * (w & 1);
+    cr = d4v{0.0, 0.0, 0.0, 0.0};
+    ci = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 4) {
+        const int kk = k0 + (lane >> 4);
+        d2 av = CTA ? A[kk * HS + i0 + (lane & 15)] : A[(i0 + (lane & 15)) * HS + kk];
+        d2 bv = CTB ? B[(j0 + (lane & 15)) * HS + kk] : B[kk * HS + j0 + (lane & 15)];
+        if (CTA) av.y = -av.y;
+        if (CTB) bv.y = -bv.y;
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, cr, 0, 0, 0);
+        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, cr, 0, 0, 0);
+        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, ci, 0, 0, 0);
+        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, ci, 0, 0, 0);
+    }
+}
+// store an mm32 result: lane l, reg r -> row i0 + (l>>4) + 4r, col j0 + (l&15)
+__device__ __forceinline__ void store32(d2* C, const d4v& cr, const d4v& ci, int lane, int w) {
+    const int i0 = 16 * (w >> 1), j0 = 16 * (w & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(i0 + (lane >> 4) + 4 * r) * HS + j0 + (lane & 15)] = make_double2(cr[r], ci[r]);
 }
 
 template <int VARIANT, bool INIT>
@@ -42,7 +122,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
     const int n = a.n, m = a.m, tx = a.tx, rx = a.rx;
     RealState* st = a.st + b;
     __shared__ double red[16 * 8];
-    __shared__ int flag_rot, flag_improved, flag_any;
+    __shared__ int flag_improved, flag_any;
     if (!INIT && st->done) return;
     const double mu = INIT ? 1.0 : st->mu;
     const double imu = 1.0 / mu;
@@ -77,145 +157,196 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         const double f = nz > 0.0 ? fmax(0.0, nz - imu) / nz : 0.0;
         for (int k = t; k < n; k += nt) emit(k, cscale(evalE(k), f));
     } else {
-        __shared__ d2 Hs[TXMAX * HS];
-        __shared__ d2 Qs[TXMAX * HS];
-        __shared__ d2 Ts[TXMAX * HS];
-        __shared__ double rc[TXMAX / 2], rs[TXMAX / 2];
-        __shared__ d2 re[TXMAX / 2];
-        __shared__ int rp[TXMAX / 2], rq[TXMAX / 2];
+        // ---- A2only ArgMinZ (inferLowRankV4_multi.m:423-485) ------------------------
+        // Two 32x32 complex LDS tiles (E/H/T in L0, eigenvectors Q in L1), zero-padded
+        // to 32 for tx, rx < 32.  The five 32x32 complex products run on the f64
+        // matrix cores (mm32).  The Hermitian eigensolver is a parallel cyclic Jacobi
+        // with one barrier per step: every thread derives the two rotations it needs
+        // from a double-buffered "rotation input" array (diagonal + the next step's
+        // pair entries), written by the threads that produce those entries.
+        __shared__ d2 L0[TXMAX * HS];
+#ifdef ACE_DEBUG_SWEEPS
+        const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long dbg_t1 = 0, dbg_t2 = 0;
+#endif
+        __shared__ d2 L1[TXMAX * HS];
+        __shared__ int flags[MAX_SWEEPS + 1];
         __shared__ double wv[TXMAX], scl[TXMAX], rs2[TXMAX];
         __shared__ int ord[TXMAX], ascp[TXMAX];
-        // E into Ts
-        for (int e = t; e < tx * rx; e += nt) {
-            const int i = e % tx, j = e / tx;
-            Ts[i * HS + j] = evalE(e);
+        const int lane = t & 63, w = t >> 6;
+        if (t <= MAX_SWEEPS) flags[t] = 0;
+        // E = reshape(X + N/mu, tx, []) into L0 (zero padded)
+        for (int e = t; e < TXMAX * TXMAX; e += nt) {
+            const int i = e & 31, j = e >> 5;
+            L0[i * HS + j] = (i < tx && j < rx) ? evalE(i + tx * j) : make_double2(0.0, 0.0);
         }
         __syncthreads();
-        // H = E E^H  (:428)
-        for (int e = t; e < tx * tx; e += nt) {
-            const int i = e / tx, i2 = e % tx;
-            d2 s = make_double2(0.0, 0.0);
-            for (int j = 0; j < rx; ++j) {
-                const d2 u = Ts[i * HS + j], v = Ts[i2 * HS + j];
-                s.x += u.x * v.x + u.y * v.y;  // u * conj(v)
-                s.y += u.y * v.x - u.x * v.y;
-            }
-            if (i == i2) s.y = 0.0;
-            Hs[i * HS + i2] = s;
-        }
+        d4v cr, ci;
+        mm32<false, true>(L0, L0, cr, ci, lane, w);      // H = E E^H  (:428)
+        __syncthreads();
+        store32(L0, cr, ci, lane, w);
         const bool warm = (!INIT) && a.warm && a.Q;
         d2* Qg = a.Q ? reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx : nullptr;
-        if (warm) {
-            for (int e = t; e < tx * tx; e += nt) Qs[(e / tx) * HS + (e % tx)] = Qg[e];
-            __syncthreads();
-            // Ts = H Q ; H = Q^H Ts
-            for (int e = t; e < tx * tx; e += nt) {
-                const int i = e / tx, c = e % tx;
-                d2 s = make_double2(0.0, 0.0);
-                for (int k = 0; k < tx; ++k) s = cadd(s, cmul(Hs[i * HS + k], Qs[k * HS + c]));
-                Ts[i * HS + c] = s;
-            }
-            __syncthreads();
-            for (int e = t; e < tx * tx; e += nt) {
-                const int r = e / tx, c = e % tx;
-                d2 s = make_double2(0.0, 0.0);
-                for (int k = 0; k < tx; ++k) s = cadd(s, cmulc(Qs[k * HS + r], Ts[k * HS + c]));
-                Hs[r * HS + c] = s;
-            }
-            __syncthreads();
-            // re-Hermitise: H = (H + H^H)/2 (upper from lower)
-            for (int e = t; e < tx * tx; e += nt) {
-                const int r = e / tx, c = e % tx;
-                if (r < c) {
-                    const d2 u = Hs[r * HS + c], l = Hs[c * HS + r];
-                    const d2 h = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
-                    Hs[r * HS + c] = h;
-                    Hs[c * HS + r] = make_double2(h.x, -h.y);
-                } else if (r == c) {
-                    Hs[r * HS + c].y = 0.0;
-                }
-            }
-        } else {
-            for (int e = t; e < tx * tx; e += nt) {
-                const int i = e / tx, c = e % tx;
-                Qs[i * HS + c] = make_double2(i == c ? 1.0 : 0.0, 0.0);
-            }
+        for (int e = t; e < TXMAX * TXMAX; e += nt) {
+            const int i = e >> 5, c = e & 31;
+            d2 q = make_double2(i == c ? 1.0 : 0.0, 0.0);
+            if (warm && i < tx && c < tx) q = Qg[i * tx + c];
+            L1[i * HS + c] = q;
         }
         __syncthreads();
-        double tr = 0.0;
-        for (int k = 0; k < tx; ++k) tr += fabs(Hs[k * HS + k].x);
-        const double abs_tol = 1e-18 * tr;
-        const int P = tx / 2;
-        int sweeps = 0;
-        // Parallel cyclic Jacobi: every step applies P disjoint rotations as one
-        // block-diagonal unitary J: H <- J^H H J, Q <- Q J.
-        for (; sweeps < MAX_SWEEPS; ++sweeps) {
-            if (t == 0) flag_rot = 0;
+        if (warm) {  // H <- Q^H H Q: nearly diagonal when Q is last iteration's eigenbasis
+            mm32<false, false>(L0, L1, cr, ci, lane, w);  // T = H Q
             __syncthreads();
-            for (int s = 0; s < tx - 1; ++s) {
-                if (t < P) {
-                    int p, q;
-                    rr_pair(tx, s, t, p, q);
-                    const double ap = Hs[p * HS + p].x, aq = Hs[q * HS + q].x;
-                    const d2 c = Hs[p * HS + q];
-                    const double ac = sqrt(cabs2(c));
-                    double cs = 1.0, sn = 0.0;
-                    d2 ep = make_double2(1.0, 0.0);
-                    if (ac > abs_tol && ac * ac > 1e-32 * fabs(ap * aq) && ac > 1e-300) {
-                        ep = make_double2(c.x / ac, c.y / ac);
-                        const double zeta = (aq - ap) / (2.0 * ac);
-                        const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                        cs = 1.0 / sqrt(1.0 + tt * tt);
-                        sn = tt * cs;
-                        flag_rot = 1;
-                    }
-                    rc[t] = cs;
-                    rs[t] = sn;
-                    re[t] = ep;
-                    rp[t] = p;
-                    rq[t] = q;
+            store32(L0, cr, ci, lane, w);
+            __syncthreads();
+            mm32<true, false>(L1, L0, cr, ci, lane, w);   // Q^H T
+            __syncthreads();
+            store32(L0, cr, ci, lane, w);
+            __syncthreads();
+            for (int e = t; e < TXMAX * TXMAX; e += nt) {  // exact Hermitian symmetry
+                const int r = e >> 5, c = e & 31;
+                if (r < c) {
+                    const d2 u = L0[r * HS + c], l = L0[c * HS + r];
+                    const d2 h = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                    L0[r * HS + c] = h;
+                    L0[c * HS + r] = make_double2(h.x, -h.y);
+                } else if (r == c) {
+                    L0[r * HS + c].y = 0.0;
                 }
-                __syncthreads();
-                // H blocks (ka, kb): H'[a,b] = Ja^H H[a,b] Jb, J = [[cs, sn], [-sn e*, cs e*]]
-                for (int e = t; e < P * P; e += nt) {
-                    const int ka = e / P, kb = e % P;
-                    const int pa = rp[ka], qa = rq[ka], pb = rp[kb], qb = rq[kb];
-                    const double ca = rc[ka], sa = rs[ka], cb = rc[kb], sb = rs[kb];
-                    const d2 ea = re[ka], eb = re[kb];
-                    const d2 h00 = Hs[pa * HS + pb], h01 = Hs[pa * HS + qb];
-                    const d2 h10 = Hs[qa * HS + pb], h11 = Hs[qa * HS + qb];
-                    const d2 ebc = make_double2(eb.x, -eb.y);
-                    // T = H Jb
-                    const d2 t01 = cmul(h01, ebc), t11 = cmul(h11, ebc);
-                    const d2 T00 = csub(cscale(h00, cb), cscale(t01, sb));
-                    const d2 T01 = cadd(cscale(h00, sb), cscale(t01, cb));
-                    const d2 T10 = csub(cscale(h10, cb), cscale(t11, sb));
-                    const d2 T11 = cadd(cscale(h10, sb), cscale(t11, cb));
-                    // H' = Ja^H T : row0 = ca*T0 - sa*ea*T1, row1 = sa*T0 + ca*ea*T1
-                    const d2 u10 = cmul(ea, T10), u11 = cmul(ea, T11);
-                    Hs[pa * HS + pb] = csub(cscale(T00, ca), cscale(u10, sa));
-                    Hs[pa * HS + qb] = csub(cscale(T01, ca), cscale(u11, sa));
-                    Hs[qa * HS + pb] = cadd(cscale(T00, sa), cscale(u10, ca));
-                    Hs[qa * HS + qb] = cadd(cscale(T01, sa), cscale(u11, ca));
-                }
-                for (int e = t; e < tx * P; e += nt) {
-                    const int i = e / P, kb = e % P;
-                    const int pb = rp[kb], qb = rq[kb];
-                    const double cb = rc[kb], sb = rs[kb];
-                    const d2 eb = re[kb];
-                    const d2 qp = Qs[i * HS + pb];
-                    const d2 qq = cmul(Qs[i * HS + qb], make_double2(eb.x, -eb.y));
-                    Qs[i * HS + pb] = csub(cscale(qp, cb), cscale(qq, sb));
-                    Qs[i * HS + qb] = cadd(cscale(qp, sb), cscale(qq, cb));
-                }
-                __syncthreads();
             }
-            if (!flag_rot) break;
             __syncthreads();
         }
+        double tr = 0.0;
+        for (int k = 0; k < tx; ++k) tr += fabs(L0[k * HS + k].x);
+        const double abs_tol = 1e-18 * tr;
+        const int P = tx >> 1;
+        // ---- Jacobi in the position frame -------------------------------------------
+        // Pair k always sits at positions (2k, 2k+1); after every step the positions
+        // are permuted by the circle-method map (circ_next), so each sweep of tx-1
+        // steps meets every index pair once.  H lives in packed upper-triangular form,
+        // double buffered (read cur, write the permuted result to nxt), aliased onto
+        // L0 (2 x 528 complex = one 32x33 tile).  Q stays in the original (label)
+        // order; Lab[.][p] is the label at position p.  All addressing is static per
+        // thread, so a step is branch-free with one barrier.
+        __shared__ int Lab[2][TXMAX];
+        {
+            const int j = t & 31, i0 = t >> 5;  // rows i0, i0+8, i0+16, i0+24 of column j
+            const d2 h0 = L0[i0 * HS + j], h1 = L0[(i0 + 8) * HS + j];
+            const d2 h2 = L0[(i0 + 16) * HS + j], h3 = L0[(i0 + 24) * HS + j];
+            __syncthreads();
+            if (i0 <= j) L0[up_idx(i0, j)] = h0;
+            if (i0 + 8 <= j) L0[up_idx(i0 + 8, j)] = h1;
+            if (i0 + 16 <= j) L0[up_idx(i0 + 16, j)] = h2;
+            if (i0 + 24 <= j) L0[up_idx(i0 + 24, j)] = h3;
+            if (t < TXMAX) Lab[0][t] = t;
+            __syncthreads();
+        }
+        d2* Hp = L0;                              // Hp[buf * 528 + up_idx(i, j)]
+        // static per-thread block (ta <= tb): read / write slots, conj flags
+        int ta = -1, tb = -1;
+        if (t < 136) {
+            ta = c_tri_a[t];
+            tb = c_tri_b[t];
+            if (tb >= P) ta = -1;
+        }
+        const int sa = ta < 0 ? 0 : ta, sb = tb < 0 ? 0 : tb;
+        int rd[4], wr[4], dg[4], dgj[4];
+        double wsg[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 2 * sa + (r >> 1), j = 2 * sb + (r & 1);
+            rd[r] = i <= j ? up_idx(i, j) : up_idx(j, i);
+            dg[r] = up_idx(i, i);   // diagonals of row i and column j (convergence test)
+            dgj[r] = up_idx(j, j);
+            const int ii = circ_next(tx, i), jj = circ_next(tx, j);
+            wr[r] = ii <= jj ? up_idx(ii, jj) : up_idx(jj, ii);
+            wsg[r] = ii <= jj ? 1.0 : -1.0;
+        }
+        const bool diagblk = (ta == tb);                // (2k+1, 2k) mirrors (2k, 2k+1): not stored
+        const double rsg10 = diagblk ? -1.0 : 1.0;      // diagonal block reads (2k+1,2k) as conj
+        const int kl = lane & 15;                       // rotation evaluated by this lane
+        const int rp = up_idx(2 * kl, 2 * kl), rq = up_idx(2 * kl + 1, 2 * kl + 1), rc = up_idx(2 * kl, 2 * kl + 1);
+        const int pn = t < tx ? circ_next(tx, t) : 0;
+        int cur = 0, sweeps = 0;
+#ifdef ACE_DEBUG_SWEEPS
+        dbg_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
+        for (; sweeps < MAX_SWEEPS; ++sweeps) {
+            // convergence pre-check over this thread's block entries (off-diagonal ones)
+            if (ta >= 0) {
+                const d2* H = Hp + cur * 528;
+                bool need = false;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool offd = !diagblk || r == 1;   // off-diagonal entries of the block
+                    if (offd) need |= needs_rot(H[dg[r]].x, H[dgj[r]].x, H[rd[r]], abs_tol);
+                }
+                if (need) flags[sweeps] = 1;
+            }
+            __syncthreads();
+            if (!flags[sweeps]) break;
+            for (int s = 0; s < tx - 1; ++s) {
+                const int nx = cur ^ 1;
+                const d2* H = Hp + cur * 528;
+                d2* Hn = Hp + nx * 528;
+                Rot Jl{1.0, 0.0, make_double2(1.0, 0.0), false};
+                if (kl < P) Jl = make_rot(H[rp].x, H[rq].x, H[rc], abs_tol);
+                Rot Ja, Jb;
+                Ja.cs = __shfl(Jl.cs, sa, 64);
+                Ja.sn = __shfl(Jl.sn, sa, 64);
+                Ja.e.x = __shfl(Jl.e.x, sa, 64);
+                Ja.e.y = __shfl(Jl.e.y, sa, 64);
+                Jb.cs = __shfl(Jl.cs, sb, 64);
+                Jb.sn = __shfl(Jl.sn, sb, 64);
+                Jb.e.x = __shfl(Jl.e.x, sb, 64);
+                Jb.e.y = __shfl(Jl.e.y, sb, 64);
+                if (ta >= 0) {
+                    // H'[a,b] = Ja^H H[a,b] Jb,  J = [[cs, sn], [-sn e*, cs e*]]
+                    const d2 h00 = H[rd[0]], h01 = H[rd[1]], h11 = H[rd[3]];
+                    d2 h10 = H[rd[2]];
+                    h10.y *= rsg10;
+                    const d2 ebc = make_double2(Jb.e.x, -Jb.e.y);
+                    const d2 t01 = cmul(h01, ebc), t11 = cmul(h11, ebc);
+                    const d2 T00 = csub(cscale(h00, Jb.cs), cscale(t01, Jb.sn));
+                    const d2 T01 = cadd(cscale(h00, Jb.sn), cscale(t01, Jb.cs));
+                    const d2 T10 = csub(cscale(h10, Jb.cs), cscale(t11, Jb.sn));
+                    const d2 T11 = cadd(cscale(h10, Jb.sn), cscale(t11, Jb.cs));
+                    const d2 u10 = cmul(Ja.e, T10), u11 = cmul(Ja.e, T11);
+                    const d2 nv[4] = {csub(cscale(T00, Ja.cs), cscale(u10, Ja.sn)),
+                                      csub(cscale(T01, Ja.cs), cscale(u11, Ja.sn)),
+                                      cadd(cscale(T00, Ja.sn), cscale(u10, Ja.cs)),
+                                      cadd(cscale(T01, Ja.sn), cscale(u11, Ja.cs))};
+                    Hn[wr[0]] = make_double2(nv[0].x, nv[0].y * wsg[0]);
+                    Hn[wr[1]] = make_double2(nv[1].x, nv[1].y * wsg[1]);
+                    Hn[wr[3]] = make_double2(nv[3].x, nv[3].y * wsg[3]);
+                    if (!diagblk) Hn[wr[2]] = make_double2(nv[2].x, nv[2].y * wsg[2]);
+                }
+                // Q <- Q J on label columns (Lab[2k], Lab[2k+1]) for (row i, pair k = lane & 15)
+                if (kl < P) {
+                    const int lp = Lab[cur][2 * kl], lq = Lab[cur][2 * kl + 1];
+                    const d2 ebc = make_double2(Jl.e.x, -Jl.e.y);
+#pragma unroll
+                    for (int e = t; e < TXMAX * 16; e += 256) {
+                        const int i = e >> 4;
+                        if (i < tx) {
+                            const d2 qp = L1[i * HS + lp];
+                            const d2 qq = cmul(L1[i * HS + lq], ebc);
+                            L1[i * HS + lp] = csub(cscale(qp, Jl.cs), cscale(qq, Jl.sn));
+                            L1[i * HS + lq] = cadd(cscale(qp, Jl.sn), cscale(qq, Jl.cs));
+                        }
+                    }
+                }
+                if (t < tx) Lab[nx][pn] = Lab[cur][t];
+                cur = nx;
+                __syncthreads();
+            }
+        }
         if (sweeps >= MAX_SWEEPS && t == 0) atomicOr(&st->status, (int)ACE_ST_EIG_NOCONV);
-        // eigenvalues; MATLAB order emulation: ascending (LAPACK) then stable descending (:429-430)
-        if (t < tx) wv[t] = Hs[t * HS + t].x;
+#ifdef ACE_DEBUG_SWEEPS
+        dbg_t2 = __builtin_amdgcn_s_memrealtime();
+#endif
+        // eigenvalue at position p belongs to eigenvector (Q column) Lab[p]
+        if (t < tx) wv[Lab[cur][t]] = Hp[cur * 528 + up_idx(t, t)].x;
         __syncthreads();
         if (t < tx) {  // position in LAPACK's ascending order
             const double wk = wv[t];
@@ -233,8 +364,8 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
                 rank += (sj > sk) || (sj == sk && ascp[j] < asc);
             }
             ord[rank] = t;  // ord[sorted position] = eigen index
-            scl[t] = 1.0;
         }
+        if (t < TXMAX) scl[t] = 1.0;
         __syncthreads();
         if (t == 0) {  // rank-profile tail rescaling (:469-480), sequential sums
             double* s2 = rs2;
@@ -258,32 +389,41 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             flag_any = any;
         }
         __syncthreads();
+        if (a.Q) {
+            for (int e = t; e < tx * tx; e += nt) Qg[e] = L1[(e / tx) * HS + (e % tx)];
+        }
         if (flag_any) {
-            // Z = U diag(sqrt(scl)) U^H E  (:482-484); E restaged into Hs
-            for (int e = t; e < tx * rx; e += nt) {
-                const int i = e % tx, j = e / tx;
-                Hs[i * HS + j] = evalE(e);
+            // Z = U diag(sqrt(scl)) U^H E  (:482-484); E restaged into L0
+            for (int e = t; e < TXMAX * TXMAX; e += nt) {
+                const int i = e & 31, j = e >> 5;
+                L0[i * HS + j] = (i < tx && j < rx) ? evalE(i + tx * j) : make_double2(0.0, 0.0);
             }
             __syncthreads();
-            for (int e = t; e < tx * rx; e += nt) {
-                const int c = e / rx, j = e % rx;
-                d2 s = make_double2(0.0, 0.0);
-                for (int i = 0; i < tx; ++i) s = cadd(s, cmulc(Qs[i * HS + c], Hs[i * HS + j]));
-                Ts[c * HS + j] = cscale(s, sqrt(scl[c]));
+            mm32<true, false>(L1, L0, cr, ci, lane, w);   // U^H E
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {                 // row c of the product is eigen index c
+                const double sw = sqrt(scl[16 * (w >> 1) + (lane >> 4) + 4 * r]);
+                cr[r] *= sw;
+                ci[r] *= sw;
             }
             __syncthreads();
-            for (int e = t; e < tx * rx; e += nt) {
-                const int i = e % tx, j = e / tx;
-                d2 s = make_double2(0.0, 0.0);
-                for (int c = 0; c < tx; ++c) s = cadd(s, cmul(Qs[i * HS + c], Ts[c * HS + j]));
-                emit(e, s);
-            }
+            store32(L0, cr, ci, lane, w);
+            __syncthreads();
+            mm32<false, false>(L1, L0, cr, ci, lane, w);  // U (diag(sqrt(scl)) U^H E)
+            __syncthreads();
+            store32(L0, cr, ci, lane, w);
+            __syncthreads();
+            for (int k = t; k < n; k += nt) emit(k, L0[(k % tx) * HS + k / tx]);
         } else {
             for (int k = t; k < n; k += nt) emit(k, evalE(k));
         }
-        if (a.Q) {
-            for (int e = t; e < tx * tx; e += nt) Qg[e] = Qs[(e / tx) * HS + (e % tx)];
-        }
+#ifdef ACE_DEBUG_SWEEPS
+        __syncthreads();
+        const unsigned long long dbg_t3 = __builtin_amdgcn_s_memrealtime();
+        if (t == 0 && (b == 0 || b == 2000) && (a.it < 4 || a.it % 20 == 0))
+            printf("b %d it %d sweeps %d pre %llu jac %llu post %llu (x10ns)\n", b, a.it, sweeps, dbg_t1 - dbg_t0,
+                   dbg_t2 - dbg_t1, dbg_t3 - dbg_t2);
+#endif
     }
     if (INIT) return;
 

@@ -1,0 +1,53 @@
+"""Realisation sharding across GPUs (one process per GPU, torch.distributed).
+
+Independent Monte-Carlo realisations are the only parallel axis of the
+reference (it ``parfor``s over them: Numerical_Simulation/main_programs/
+Vs_M_par.m:145); nothing is exchanged while solving.  Each rank takes a
+contiguous block of the global batch and the recovered channels are collected
+on rank 0 with a single gather (RCCL over xGMI with the "nccl" backend, or gloo
+on CPU).
+"""
+from __future__ import annotations
+
+
+def shard_range(global_batch: int, world: int, rank: int):
+    """Contiguous block [first, first+count) of realisation indices owned by ``rank``.
+    Blocks differ in size by at most one (the first ``global_batch % world`` ranks get +1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank {rank} / world {world}")
+    base, extra = divmod(global_batch, world)
+    count = base + (1 if rank < extra else 0)
+    first = rank * base + min(rank, extra)
+    return first, count
+
+
+def gather_to_root(local, counts, group=None):
+    """Gather per-rank tensors (first dimension = realisations, sizes ``counts``)
+    to rank 0 and return the concatenation there (None on other ranks).
+
+    Ragged shards are padded to the largest count for the collective and
+    trimmed afterwards, so one ``gather`` call suffices."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(counts) != world:
+        raise ValueError("counts must have one entry per rank")
+    cmax = max(counts)
+    if local.shape[0] != counts[rank]:
+        raise ValueError(f"rank {rank}: local batch {local.shape[0]} != counts[{rank}] {counts[rank]}")
+    if local.is_complex():  # collectives move the (re, im) pairs as real data (gloo has no complex)
+        out = gather_to_root(torch.view_as_real(local.contiguous()), counts, group)
+        return None if out is None else torch.view_as_complex(out.contiguous())
+    if local.shape[0] < cmax:
+        pad = torch.zeros((cmax - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        send = torch.cat([local, pad])
+    else:
+        send = local.contiguous()
+    if rank == 0:
+        bufs = [torch.empty_like(send) for _ in range(world)]
+        dist.gather(send, gather_list=bufs, dst=0, group=group)
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+    dist.gather(send, gather_list=None, dst=0, group=group)
+    return None

@@ -125,16 +125,15 @@ def main():
     A, B, X0, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, a_shared=not args.private, device=dev)
     ws = ace_amd.solver.Workspace()
     out = None
-    gather_buf = None
-    if world > 1 and rank == 0:
-        gather_buf = [torch.empty((bsz, n), dtype=torch.complex128, device=dev) for _ in range(world)]
+    from ace_amd.dist import gather_to_root
+    counts = [bsz] * world
 
     def step():
         nonlocal out
         out = infer_admm_batch(A, B, X0, tx, tx, variant=args.variant, maxiter=args.iters, fixed_iters=True,
                                out=out, workspace=ws)
-        if world > 1:   # the single result gather over RCCL/xGMI (north_star)
-            dist.gather(out.X, gather_list=gather_buf if rank == 0 else None, dst=0)
+        if world > 1:   # the single result gather of recovered channels over RCCL/xGMI (north_star)
+            gather_to_root(out.X, counts)
 
     for _ in range(args.warmup):
         step()

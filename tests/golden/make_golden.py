@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors (tests/golden/*.npz).
+
+Source of truth: the numpy restatement oracle (oracle/ace_oracle.py) of the
+reference MATLAB solvers.  MATLAB is not available in this image and the
+reference ships no ADMM outputs, so these vectors pin the restatement against
+drift and give the GPU path fixed targets; they are not MATLAB outputs
+("parity unpinned").
+
+Inputs are synthetic (ace_amd.synth, counter-based RNG; the integer codebook
+stream is stored explicitly as phase codes so the fixture does not depend on
+the generator) and the train/test partitions are explicit, standing in for
+MATLAB's randsample (inferLowRankV4_multi.m:48).
+
+Also records a slice of the reference's own codebook fixture
+(codebook/codebook_mat/random_probe_cb_16x16.mat) as phase codes, when the
+reference tree is present (this script runs in the build container only).
+
+Run: python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import math
+import pathlib
+import sys
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "2ace-mmwave-channel-estimation_amd"))
+
+import ace_oracle as O  # noqa: E402
+from ace_amd import synth  # noqa: E402
+
+
+def codes_of(A):
+    """Phase code k with A = j^k / sqrt(n)."""
+    n = A.shape[-1]
+    z = A * math.sqrt(n)
+    k = np.rint(np.angle(z) / (np.pi / 2)).astype(np.int64) % 4
+    assert np.allclose((1j ** k) / math.sqrt(n), A, atol=1e-15)
+    return k.astype(np.uint8)
+
+
+def partitions(rng, m, restarts, cc_frac=0.95):
+    mt = math.floor(m * cc_frac)
+    return np.stack([rng.permutation(m)[:mt] for _ in range(restarts)])
+
+
+def pipeline_case(name, seed, tx, m, restarts, variant, count=2):
+    A, B, X0, H = synth.problem(seed, 0, count, m, tx, tx)
+    A0 = A[0]
+    rng = np.random.default_rng(seed)
+    out = dict(codes=codes_of(A0), B=B, H=H, tx=tx, m=m, variant=variant, restarts=restarts)
+    Xs, Ys, qs, its, rb, trs = [], [], [], [], [], []
+    for b in range(count):
+        tr = partitions(rng, m, restarts)
+        res = O.infer_low_rank_pipeline(A0, B[b], tx, tx, list(tr), variant=variant)
+        Xs.append(res.X)
+        Ys.append(res.Y)
+        qs.append(res.quality)
+        its.append(res.stage_iters)
+        rb.append(res.rolled_back)
+        trs.append(tr)
+    out.update(train_idx=np.stack(trs), X=np.stack(Xs), Y=np.stack(Ys), quality=np.array(qs),
+               stage_iters=np.array(its), rolled_back=np.array(rb))
+    np.savez_compressed(HERE / f"{name}.npz", **out)
+    print(name, "quality", np.round(out["quality"], 4), "iters", out["stage_iters"].tolist(),
+          "nmse", [round(O.phase_aligned_rel_err(out["X"][b], H[b]), 4) for b in range(count)])
+
+
+def refine_case(name, seed, tx, m, variant, maxiter, fixed, count=3):
+    A, B, X0, H = synth.problem(seed, 0, count, m, tx, tx)
+    A0 = A[0]
+    U = O.make_U(A0)
+    Xs, Ys, its, cv = [], [], [], []
+    for b in range(count):
+        r = O.infer_admm(A0, B[b], X0[b][:, None], True, False, tx, tx, U=U, variant=variant,
+                         maxiter=maxiter, fixed_iters=fixed)
+        Xs.append(r.X.ravel())
+        Ys.append(r.Y.ravel())
+        its.append(r.iters)
+        cv.append(r.converged)
+    np.savez_compressed(HERE / f"{name}.npz", codes=codes_of(A0), B=B, X0=X0, H=H, tx=tx, m=m, variant=variant,
+                        maxiter=maxiter, fixed=fixed, X=np.stack(Xs), Y=np.stack(Ys), iters=np.array(its),
+                        converged=np.array(cv))
+    print(name, "iters", its, "converged", cv)
+
+
+def reference_codebook_slice():
+    mat = pathlib.Path("/root/reference/codebook/codebook_mat/random_probe_cb_16x16.mat")
+    if not mat.exists():
+        print("reference codebook not present; keeping existing fixture")
+        return
+    import scipy.io as sio
+    cb = sio.loadmat(str(mat))["cb"]       # plain MATLAB v5 numeric array, no pickle
+    k = np.rint(np.angle(cb) / (np.pi / 2)).astype(np.int64) % 4
+    assert np.allclose(1j ** k, cb, atol=1e-12), "reference codebook entries are not unit QPSK"
+    digest = hashlib.sha256(np.ascontiguousarray(k.astype(np.uint8)).tobytes()).hexdigest()
+    np.savez_compressed(HERE / "ref_codebook_16x16_slice.npz", codes_head=k[:64].astype(np.uint8),
+                        shape=np.array(cb.shape), codes_sha256=np.array(digest))
+    (HERE / "ref_codebook_16x16.json").write_text(json.dumps(
+        {"source": "codebook/codebook_mat/random_probe_cb_16x16.mat", "shape": list(cb.shape),
+         "dtype": str(cb.dtype), "entries": "unit-modulus QPSK {1, j, -1, -j}",
+         "codes_sha256": digest}, indent=1) + "\n")
+    print("reference codebook", cb.shape, digest[:16])
+
+
+def main():
+    # config 1: 16-ant, 64 RSS meas -- single-restart inferLowRankV4 and the
+    # 3-restart inferLowRankV4_multi / 1-restart inferLowRank_Nuclear
+    pipeline_case("pipeline_v4_16ant_m64", 101, 16, 64, 1, O.VARIANT_A2ONLY)
+    pipeline_case("pipeline_v4multi_16ant_m64", 102, 16, 64, 3, O.VARIANT_A2ONLY)
+    pipeline_case("pipeline_nuclear_16ant_m64", 103, 16, 64, 1, O.VARIANT_NUCLEAR)
+    # the benchmark unit (refinement InferADMM, r = 1) at 16-ant and 32-ant
+    refine_case("refine_a2only_16ant_m64", 201, 16, 64, O.VARIANT_A2ONLY, 500, False)
+    refine_case("refine_a2only_32ant_m256", 202, 32, 256, O.VARIANT_A2ONLY, 500, False)
+    refine_case("refine_a2only_32ant_m256_fixed200", 203, 32, 256, O.VARIANT_A2ONLY, 200, True)
+    refine_case("refine_nuclear_16ant_m64_fixed60", 204, 16, 64, O.VARIANT_NUCLEAR, 60, True)
+    # generator pin: first codes and a normal draw for a fixed seed
+    np.savez_compressed(HERE / "synth_pin.npz", codes=synth.codebook_codes(58659179, 8, 16),
+                        normals=synth.normal_pairs(58659179, 3, 4), vecH=synth.channel(58659179, 0, 4, 4))
+    reference_codebook_slice()
+
+
+if __name__ == "__main__":
+    main()

@@ -229,6 +229,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         // order; Lab[.][p] is the label at position p.  All addressing is static per
         // thread, so a step is branch-free with one barrier.
         __shared__ int Lab[2][TXMAX];
+        __shared__ double4 RotS[TXMAX / 2];
         {
             const int j = t & 31, i0 = t >> 5;  // rows i0, i0+8, i0+16, i0+24 of column j
             const d2 h0 = L0[i0 * HS + j], h1 = L0[(i0 + 8) * HS + j];
@@ -289,17 +290,17 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
                 const int nx = cur ^ 1;
                 const d2* H = Hp + cur * 528;
                 d2* Hn = Hp + nx * 528;
-                Rot Jl{1.0, 0.0, make_double2(1.0, 0.0), false};
-                if (kl < P) Jl = make_rot(H[rp].x, H[rq].x, H[rc], abs_tol);
-                Rot Ja, Jb;
-                Ja.cs = __shfl(Jl.cs, sa, 64);
-                Ja.sn = __shfl(Jl.sn, sa, 64);
-                Ja.e.x = __shfl(Jl.e.x, sa, 64);
-                Ja.e.y = __shfl(Jl.e.y, sa, 64);
-                Jb.cs = __shfl(Jl.cs, sb, 64);
-                Jb.sn = __shfl(Jl.sn, sb, 64);
-                Jb.e.x = __shfl(Jl.e.x, sb, 64);
-                Jb.e.y = __shfl(Jl.e.y, sb, 64);
+                // rotations of the step, once per work-group (wave 0, lanes 0..P-1)
+                if (t < P) {
+                    const Rot J = make_rot(H[rp].x, H[rq].x, H[rc], abs_tol);
+                    RotS[t] = make_double4(J.cs, J.sn, J.e.x, J.e.y);
+                }
+                __syncthreads();
+                const double4 ra = RotS[sa], rb = RotS[sb], rl = RotS[kl];
+                Rot Ja, Jb, Jl;
+                Ja.cs = ra.x; Ja.sn = ra.y; Ja.e = make_double2(ra.z, ra.w);
+                Jb.cs = rb.x; Jb.sn = rb.y; Jb.e = make_double2(rb.z, rb.w);
+                Jl.cs = rl.x; Jl.sn = rl.y; Jl.e = make_double2(rl.z, rl.w);
                 if (ta >= 0) {
                     // H'[a,b] = Ja^H H[a,b] Jb,  J = [[cs, sn], [-sn e*, cs e*]]
                     const d2 h00 = H[rd[0]], h01 = H[rd[1]], h11 = H[rd[3]];

@@ -96,6 +96,7 @@ struct ZArgs {
 };
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st);
+void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st);  // A2only, one wave per realisation
 void launch_pre(int n, int m, int batch, const double* Z, const double* N, const double* Y, const double* M, double* V,
                 double* S, const RealState* rs, hipStream_t st);
 void launch_ystep(int m, int batch, const double* S, const double* g, double* M, const double* B, const double* Yold,

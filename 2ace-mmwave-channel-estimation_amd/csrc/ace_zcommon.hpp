@@ -1,0 +1,121 @@
+// Helpers shared by the Z-prox kernels (ace_zprox.hip, ace_zprox1w.hip): Jacobi
+// rotations, packed-triangular indexing, the circle-method position map.
+#pragma once
+#include "ace_common.hpp"
+
+namespace ace {
+namespace {
+constexpr int ZT = 32;            // padded tile size (tx, rx <= 32)
+constexpr int ZHS = ZT + 1;       // LDS row stride (complex) of a 32x32 tile
+constexpr int ZPACK = 528;        // packed upper triangle of a 32x32 matrix
+
+// upper-triangular enumeration of the 16x16 slot-pair blocks (ka <= kb)
+static __constant__ unsigned char c_tri_a[136] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,2,2,2,2,2,2,2,2,2,2,2,2,2,2,3,3,3,3,3,3,3,3,3,3,3,3,3,4,4,4,4,4,4,4,4,4,4,4,4,5,5,5,5,5,5,5,5,5,5,5,6,6,6,6,6,6,6,6,6,6,7,7,7,7,7,7,7,7,7,8,8,8,8,8,8,8,8,9,9,9,9,9,9,9,10,10,10,10,10,10,11,11,11,11,11,12,12,12,12,13,13,13,14,14,15};
+static __constant__ unsigned char c_tri_b[136] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,2,3,4,5,6,7,8,9,10,11,12,13,14,15,3,4,5,6,7,8,9,10,11,12,13,14,15,4,5,6,7,8,9,10,11,12,13,14,15,5,6,7,8,9,10,11,12,13,14,15,6,7,8,9,10,11,12,13,14,15,7,8,9,10,11,12,13,14,15,8,9,10,11,12,13,14,15,9,10,11,12,13,14,15,10,11,12,13,14,15,11,12,13,14,15,12,13,14,15,13,14,15,14,15,15};
+
+// Jacobi rotation J = [[cs, sn], [-sn e*, cs e*]] annihilating h_pq of the Hermitian
+// 2x2 block [[ap, c], [c*, aq]] (c = |c| e): tan(theta) = t with
+// t = sign(aq - ap) 2|c| / (|aq - ap| + sqrt((aq - ap)^2 + 4|c|^2)).
+struct Rot {
+    double cs, sn;
+    d2 e;
+    bool on;
+};
+// v_rsq_f64 / v_rcp_f64 seeds refined by two Newton steps (~1 ulp); operands are
+// positive and finite here (guarded by the rotation threshold).
+__device__ __forceinline__ double frsq(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
+    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
+    return y;
+}
+__device__ __forceinline__ double frcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return y;
+}
+// rotate pair (p,q) unless |h_pq| is negligible: |h_pq| <= 1e-18 tr(H) (absolute, below
+// LAPACK's normwise eps) or |h_pq|^2 <= 1e-32 |h_pp h_qq| (relative, the classical
+// Jacobi test)
+__device__ __forceinline__ bool needs_rot(double ap, double aq, d2 c, double abs_tol) {
+    const double ac2 = cabs2(c);
+    return ac2 > abs_tol * abs_tol && ac2 > 1e-32 * fabs(ap * aq) && ac2 > 1e-300;
+}
+__device__ __forceinline__ Rot make_rot(double ap, double aq, d2 c, double abs_tol) {
+    Rot r{1.0, 0.0, make_double2(1.0, 0.0), false};
+    const double ac2 = cabs2(c);
+    if (needs_rot(ap, aq, c, abs_tol)) {
+        const double ir = frsq(ac2), ac = ac2 * ir;
+        r.e = make_double2(c.x * ir, c.y * ir);
+        const double d = aq - ap;
+        const double q = fma(d, d, 4.0 * ac2);
+        const double D = q * frsq(q);
+        double tt = 2.0 * ac * frcp(fabs(d) + D);
+        if (d < 0.0) tt = -tt;
+        r.cs = frsq(fma(tt, tt, 1.0));
+        r.sn = tt * r.cs;
+        r.on = true;
+    }
+    return r;
+}
+
+// Packed upper-triangular index of (i, j), i <= j < 32 (528 entries).
+__device__ __forceinline__ int up_idx(int i, int j) { return i * 32 - ((i * (i - 1)) >> 1) + (j - i); }
+
+// Circle-method position map for n (even) positions with pairs (2k, 2k+1): position
+// 0 is fixed, the "top" elements 2k move right, the "bottom" elements 2k+1 move left.
+__device__ __forceinline__ int circ_next(int n, int p) {
+    if (n == 2) return p;
+    const int P = n >> 1;
+    if (p == 0) return 0;
+    if (p == 1) return 2;
+    if ((p & 1) == 0) return (p == 2 * P - 2) ? 2 * P - 1 : p + 2;
+    return p - 2;
+}
+
+// Per-iteration control of one realisation, executed by a single thread after the
+// Z-step reductions: best-objective bookkeeping (inferLowRankV4_multi.m:344-351),
+// residuals (:364-366), thresholds (:368-370), stop test (:372), mu update (:379-381).
+// Sums: nX2 = ||X||^2, nZ2 = ||Z||^2, jn2 = ||X - Z||^2, dZ2 = ||Z - Z0||^2,
+// dAtY = ||A^H (Y - Y0)||^2, nAtY = ||A^H Y||^2.  Returns 1 when the objective improved.
+__device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, double mu, double nX2, double nZ2,
+                                            double jn2, double dZ2, double dAtY, double nAtY) {
+    const int m = a.m, n = a.n;
+    const double nX = sqrt(nX2), nZ = sqrt(nZ2);
+    const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
+    const double obj = sqrt(st->obj2);
+    const double nAX = sqrt(st->nAX2), nY = sqrt(st->nY2);
+    const double r = 1.0;  // columns per realisation
+    int improved = 0;
+    if (obj < st->opt_obj) {
+        st->opt_obj = obj;
+        improved = 1;
+    }
+    const double res_prim = sqrt(st->nJM2 + jn2);
+    const double res_dual = mu * sqrt(dAtY2 + dZ2);
+    const double res_comb = sqrt(res_prim * res_prim + st->dY2 + dZ2);
+    const double mx1 = fmax(nAX, nY), mx2 = fmax(nX, nZ);
+    const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
+    const double t_dual = a.tol_abs * sqrt((double)n * r * 2) + a.tol_rel * sqrt(nAtY2 + nZ * nZ);
+    const double t_comb =
+        a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
+    st->iters = a.it;
+    const bool conv = (res_prim < t_prim && res_dual < t_dual) || (res_comb < t_comb);
+    bool stop = false;
+    if (conv) {
+        st->status |= ACE_ST_CONVERGED;
+        if (!a.fixed_iters) stop = true;
+    }
+    if (stop) {
+        st->done = 1;
+        atomicAdd(a.done_count, 1);
+    } else {
+        if (res_comb > st->last_res * 0.9) st->mu = mu * a.rho;
+        st->last_res = res_comb;
+    }
+    return improved;
+}
+
+}  // namespace
+}  // namespace ace

@@ -13,6 +13,7 @@
 // (:325, ArgMinX :404) and to its A'*Y residual terms (:330, :365, :369); it
 // replaces the n x n apply by m x m ones.
 #include "ace_common.hpp"
+#include "ace_zcommon.hpp"
 
 namespace ace {
 
@@ -20,71 +21,6 @@ namespace {
 constexpr int TXMAX = 32;
 constexpr int HS = TXMAX + 1;  // LDS row stride (complex) for 32x32 tiles
 constexpr int MAX_SWEEPS = 40;
-
-// upper-triangular enumeration of the 16x16 slot-pair blocks (ka <= kb)
-__constant__ unsigned char c_tri_a[136] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,2,2,2,2,2,2,2,2,2,2,2,2,2,2,3,3,3,3,3,3,3,3,3,3,3,3,3,4,4,4,4,4,4,4,4,4,4,4,4,5,5,5,5,5,5,5,5,5,5,5,6,6,6,6,6,6,6,6,6,6,7,7,7,7,7,7,7,7,7,8,8,8,8,8,8,8,8,9,9,9,9,9,9,9,10,10,10,10,10,10,11,11,11,11,11,12,12,12,12,13,13,13,14,14,15};
-__constant__ unsigned char c_tri_b[136] = {0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,2,3,4,5,6,7,8,9,10,11,12,13,14,15,3,4,5,6,7,8,9,10,11,12,13,14,15,4,5,6,7,8,9,10,11,12,13,14,15,5,6,7,8,9,10,11,12,13,14,15,6,7,8,9,10,11,12,13,14,15,7,8,9,10,11,12,13,14,15,8,9,10,11,12,13,14,15,9,10,11,12,13,14,15,10,11,12,13,14,15,11,12,13,14,15,12,13,14,15,13,14,15,14,15,15};
-
-// Jacobi rotation J = [[cs, sn], [-sn e*, cs e*]] annihilating h_pq of the Hermitian
-// 2x2 block [[ap, c], [c*, aq]] (c = |c| e): tan(theta) = t with
-// t = sign(aq - ap) 2|c| / (|aq - ap| + sqrt((aq - ap)^2 + 4|c|^2)).
-struct Rot {
-    double cs, sn;
-    d2 e;
-    bool on;
-};
-// v_rsq_f64 / v_rcp_f64 seeds refined by two Newton steps (~1 ulp); operands are
-// positive and finite here (guarded by the rotation threshold).
-__device__ __forceinline__ double frsq(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
-    y = fma(y * fma(-x * y, y, 1.0), 0.5, y);
-    return y;
-}
-__device__ __forceinline__ double frcp(double x) {
-    double y = __builtin_amdgcn_rcp(x);
-    y = fma(y, fma(-x, y, 1.0), y);
-    y = fma(y, fma(-x, y, 1.0), y);
-    return y;
-}
-// rotate pair (p,q) unless |h_pq| is negligible: |h_pq| <= 1e-18 tr(H) (absolute, below
-// LAPACK's normwise eps) or |h_pq|^2 <= 1e-32 |h_pp h_qq| (relative, the classical
-// Jacobi test)
-__device__ __forceinline__ bool needs_rot(double ap, double aq, d2 c, double abs_tol) {
-    const double ac2 = cabs2(c);
-    return ac2 > abs_tol * abs_tol && ac2 > 1e-32 * fabs(ap * aq) && ac2 > 1e-300;
-}
-__device__ __forceinline__ Rot make_rot(double ap, double aq, d2 c, double abs_tol) {
-    Rot r{1.0, 0.0, make_double2(1.0, 0.0), false};
-    const double ac2 = cabs2(c);
-    if (needs_rot(ap, aq, c, abs_tol)) {
-        const double ir = frsq(ac2), ac = ac2 * ir;
-        r.e = make_double2(c.x * ir, c.y * ir);
-        const double d = aq - ap;
-        const double q = fma(d, d, 4.0 * ac2);
-        const double D = q * frsq(q);
-        double tt = 2.0 * ac * frcp(fabs(d) + D);
-        if (d < 0.0) tt = -tt;
-        r.cs = frsq(fma(tt, tt, 1.0));
-        r.sn = tt * r.cs;
-        r.on = true;
-    }
-    return r;
-}
-
-// Packed upper-triangular index of (i, j), i <= j < 32 (528 entries).
-__device__ __forceinline__ int up_idx(int i, int j) { return i * 32 - ((i * (i - 1)) >> 1) + (j - i); }
-
-// Circle-method position map for n (even) positions with pairs (2k, 2k+1): position
-// 0 is fixed, the "top" elements 2k move right, the "bottom" elements 2k+1 move left.
-__device__ __forceinline__ int circ_next(int n, int p) {
-    if (n == 2) return p;
-    const int P = n >> 1;
-    if (p == 0) return 0;
-    if (p == 1) return 2;
-    if ((p & 1) == 0) return (p == 2 * P - 2) ? 2 * P - 1 : p + 2;
-    return p - 2;
-}
 
 // 32x32 complex product from LDS tiles (row stride HS) on the f64 matrix cores:
 // C = opA(A) * opB(B), op = identity or conjugate transpose.  Wave w computes the
@@ -443,41 +379,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
     }
     block_sum<6>(v6, red);
-    if (t == 0) {
-        const double nX = sqrt(v6[0]), nZ = sqrt(v6[1]), jn2 = v6[2], dZ2 = v6[3];
-        const double dAtY2 = fmax(0.0, v6[4]), nAtY2 = fmax(0.0, v6[5]);
-        const double obj = sqrt(st->obj2);
-        const double nAX = sqrt(st->nAX2), nY = sqrt(st->nY2);
-        const double r = 1.0;  // columns per realisation
-        int improved = 0;
-        if (obj < st->opt_obj) {  // :344-351
-            st->opt_obj = obj;
-            improved = 1;
-        }
-        flag_improved = improved;
-        const double res_prim = sqrt(st->nJM2 + jn2);  // :364-366
-        const double res_dual = mu * sqrt(dAtY2 + dZ2);
-        const double res_comb = sqrt(res_prim * res_prim + st->dY2 + dZ2);
-        const double mx1 = fmax(nAX, nY), mx2 = fmax(nX, nZ);  // :368-370
-        const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
-        const double t_dual = a.tol_abs * sqrt((double)n * r * 2) + a.tol_rel * sqrt(nAtY2 + nZ * nZ);
-        const double t_comb = a.tol_abs * sqrt((double)(m + n) * r * 2) +
-                              a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
-        st->iters = a.it;
-        const bool conv = (res_prim < t_prim && res_dual < t_dual) || (res_comb < t_comb);  // :372
-        bool stop = false;
-        if (conv) {
-            st->status |= ACE_ST_CONVERGED;
-            if (!a.fixed_iters) stop = true;
-        }
-        if (stop) {
-            st->done = 1;
-            atomicAdd(a.done_count, 1);
-        } else {
-            if (res_comb > st->last_res * 0.9) st->mu = mu * a.rho;  // :379-381
-            st->last_res = res_comb;
-        }
-    }
+    if (t == 0) flag_improved = iter_control(a, st, mu, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]);
     __syncthreads();
     if (flag_improved) {
         d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
@@ -635,10 +537,21 @@ __global__ __launch_bounds__(256) void conj_transpose_kernel(int rows, int cols,
 }
 }  // namespace
 
+// ACE_ZSTEP_4WAVE=1 selects the four-wave A2only kernel above (A/B comparisons).
+static bool use_4wave_zstep() {
+    static const bool v = [] {
+        const char* e = getenv("ACE_ZSTEP_4WAVE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st) {
     if (variant == ACE_VARIANT_NUCLEAR) {
         if (init) hipLaunchKernelGGL((zstep_kernel<ACE_VARIANT_NUCLEAR, true>), dim3(batch), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((zstep_kernel<ACE_VARIANT_NUCLEAR, false>), dim3(batch), dim3(256), 0, st, a);
+    } else if (!use_4wave_zstep()) {
+        launch_zstep1w(init, a, batch, st);
     } else {
         if (init) hipLaunchKernelGGL((zstep_kernel<ACE_VARIANT_A2ONLY, true>), dim3(batch), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((zstep_kernel<ACE_VARIANT_A2ONLY, false>), dim3(batch), dim3(256), 0, st, a);

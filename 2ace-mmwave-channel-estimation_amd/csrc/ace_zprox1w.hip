@@ -1,0 +1,505 @@
+// A2only Z-step, one wave per realisation (inferLowRankV4_multi.m:423-485 with the
+// residual / stopping / mu logic of :340-382).
+//
+// Layout of one realisation on its wave:
+//   LDS  T0: one 32x33 complex tile (16.9 KiB) -- E, F, the packed double-buffered
+//        Hermitian matrix during the sweeps, R / Qnew afterwards.  With ~17 KiB per
+//        wave the CU keeps every realisation of a 4096-batch resident at once.
+//   VGPR R : the accumulated Jacobi rotations in the position frame: lane (g, k) =
+//        (lane >> 4, lane & 15) holds R[i][2k], R[i][2k+1] for rows i = g + 4r.  The
+//        circle-method position permutation after each step is a one-lane shift
+//        inside each 16-lane DPP row (row_shr:1 / row_shl:1).
+// Products (all on v_mfma_f64_16x16x4_f64, 16x16 complex output blocks):
+//   warm  F = Qprev^H E,   H = F F^H   (= Qprev^H E E^H Qprev: nearly diagonal)
+//   cold  H = E E^H
+//   post  Qnew = Qprev R,  T = diag(sqrt(scale)) Qnew^H E,  Z^T = T^T Qnew^T
+// where the accumulator of T is used directly as the A operand of the last product
+// (the f64 MFMA accumulator row map (l>>4)+4q equals the operand k map), and Z^T
+// puts consecutive vec(Z) indices on consecutive lanes for coalesced stores.
+#include "ace_common.hpp"
+#include "ace_zcommon.hpp"
+
+namespace ace {
+
+namespace {
+
+__device__ __forceinline__ double dpp_shr1(double x) {  // lane k <- lane k-1 within each 16-lane row
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x111, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x111, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_shl1(double x) {  // lane k <- lane k+1 within each 16-lane row
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x101, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x101, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void mfma_c(d2 a, d2 b, d4v& cr, d4v& ci) {  // (cr, ci) += a * b (complex)
+    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, cr, 0, 0, 0);
+    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.y, b.y, cr, 0, 0, 0);
+    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.y, ci, 0, 0, 0);
+    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b.x, ci, 0, 0, 0);
+}
+
+// 16x16 complex block C = sum_k A[row][k] B[k][col] over k < 32.  fa(row, k) and
+// fb(k0, k, col) return operand values for this lane (row/col in 0..15 within the
+// block, k the absolute inner index; k0 the 4-aligned step base, compile-time after
+// unrolling, for register-resident operands).
+template <class FA, class FB>
+__device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
+    cr = d4v{0.0, 0.0, 0.0, 0.0};
+    ci = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 4) {
+        const int kk = k0 + (lane >> 4);
+        mfma_c(fa(lane & 15, kk), fb(k0, kk, lane & 15), cr, ci);
+    }
+}
+
+template <bool INIT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zstep1w_kernel(ZArgs a) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int n = a.n, m = a.m, tx = a.tx, rx = a.rx;
+    RealState* st = a.st + b;
+    if (!INIT && st->done) return;
+    __shared__ __attribute__((aligned(16))) d2 T0[ZT * ZHS];
+    __shared__ double4 RotS[16];
+    __shared__ double wv[ZT], scl[ZT], rs2[ZT];
+    __shared__ int ord[ZT], ascp[ZT];
+    __shared__ int flag_any, flag_fast;
+
+    const double mu = INIT ? 1.0 : st->mu;
+    const d2* X = reinterpret_cast<const d2*>(a.X) + (long long)b * n;
+    d2* N = reinterpret_cast<d2*>(a.N) + (long long)b * n;
+    d2* Z = reinterpret_cast<d2*>(a.Z) + (long long)b * n;
+    d2* Qg = reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx;
+    const bool warm = (!INIT) && a.warm;
+    auto evalE = [&](int k) -> d2 {  // X + N/mu (:424), true division as in the reference
+        const d2 x = X[k], nn = N[k];
+        return make_double2(x.x + nn.x / mu, x.y + nn.y / mu);
+    };
+    const d2 zero = make_double2(0.0, 0.0);
+#ifdef ACE_DEBUG_SWEEPS
+    const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long dbg_t1 = dbg_t0, dbg_t2 = dbg_t0, dbg_t3 = dbg_t0;
+    int sweeps = -1;
+#else
+    int sweeps = 0;
+#endif
+
+    // ---- E = reshape(X + N/mu, tx, []) (:424-426), zero padded to 32x32
+    for (int e = lane; e < ZT * ZT; e += 64) {
+        const int i = e & 31, j = e >> 5;
+        T0[i * ZHS + j] = (i < tx && j < rx) ? evalE(i + tx * j) : zero;
+    }
+    __syncthreads();
+    // Qprev with identity padding
+    auto qprev = [&](int i, int k) -> d2 {
+        if (i < tx && k < tx) return Qg[i * tx + k];
+        return make_double2(i == k ? 1.0 : 0.0, 0.0);
+    };
+    d4v cr[2][2], ci[2][2];
+    if (warm) {  // F = Qprev^H E -> T0
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int J = 0; J < 2; ++J)
+                mm16([&](int r, int k) { const d2 q = qprev(k, 16 * I + r); return make_double2(q.x, -q.y); },
+                     [&](int, int k, int c) { return T0[k * ZHS + 16 * J + c]; }, cr[I][J], ci[I][J], lane);
+        __syncthreads();
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int J = 0; J < 2; ++J)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    T0[(16 * I + (lane >> 4) + 4 * r) * ZHS + 16 * J + (lane & 15)] =
+                        make_double2(cr[I][J][r], ci[I][J][r]);
+        __syncthreads();
+    }
+    // ---- Spectral certificate.  The tail rescaling (:469-480) fires only when some
+    // profile entry has  sum(top-r eigenvalues) < f * trace.  By Ky Fan, the sum of the r
+    // largest diagonal entries of Qprev^H H Qprev (= squared row norms of F) is a lower
+    // bound on sum(top-r eigenvalues) for any unitary Qprev, and the diagonal sums to the
+    // trace.  When every entry clears its threshold by a relative margin far above the
+    // rounding of the reference's eig, no rescaling happens there either and Z = E
+    // exactly: the eigendecomposition is skipped (Q keeps its warm start).
+    if (!INIT) {
+        if (lane < ZT) {
+            double d = 0.0;
+            for (int j = 0; j < ZT; ++j) d += cabs2(T0[lane * ZHS + j]);
+            wv[lane] = d;
+        }
+        __syncthreads();
+        if (lane < ZT) {
+            const double dk = wv[lane];
+            int rank = 0;
+            for (int j = 0; j < ZT; ++j) rank += (wv[j] > dk) || (wv[j] == dk && j < lane);
+            rs2[rank] = dk;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            double v = 0.0;
+            for (int k = 0; k < ZT; ++k) v += rs2[k];
+            int ok = v > 0.0;
+            for (int pi = 0; pi < a.np; ++pi) {
+                double vr = 0.0;
+                for (int k = 0; k < a.rl[pi]; ++k) vr += rs2[k];
+                ok &= vr > a.fl[pi] * v * (1.0 + 1e-9);
+            }
+            flag_fast = ok;
+        }
+        __syncthreads();
+    } else if (lane == 0) {
+        flag_fast = 0;
+    }
+    __syncthreads();
+    const bool fast = flag_fast;
+    if (lane == 0) flag_any = 0;
+    if (!fast) {
+    // H = F F^H (:428), upper blocks (0,0), (0,1), (1,1) -> packed buffer 0
+    {
+        d4v hr[3], hi[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int I = q == 2 ? 1 : 0, J = q == 0 ? 0 : 1;
+            mm16([&](int r, int k) { return T0[(16 * I + r) * ZHS + k]; },
+                 [&](int, int k, int c) { const d2 f = T0[(16 * J + c) * ZHS + k]; return make_double2(f.x, -f.y); },
+                 hr[q], hi[q], lane);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int I = q == 2 ? 1 : 0, J = q == 0 ? 0 : 1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * I + (lane >> 4) + 4 * r, col = 16 * J + (lane & 15);
+                if (row <= col) T0[up_idx(row, col)] = make_double2(hr[q][r], row == col ? 0.0 : hi[q][r]);
+            }
+        }
+        __syncthreads();
+    }
+    double tr = 0.0;
+    if (lane < tx) tr = fabs(T0[up_idx(lane, lane)].x);
+    tr = wave_sum(tr);
+    const double abs_tol = 1e-18 * tr;
+    const int P = tx >> 1;
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_t1 = __builtin_amdgcn_s_memrealtime();
+    sweeps = 0;
+#endif
+
+    // ---- Jacobi sweeps in the position frame (see ace_zprox.hip for the scheme)
+    const int kl = lane & 15, g = lane >> 4;
+    // R (position frame), rows i = g + 4r, columns (2kl, 2kl+1)
+    double Rt[8][2], Rb[8][2];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int i = g + 4 * r;
+        Rt[r][0] = (i == 2 * kl) ? 1.0 : 0.0;
+        Rt[r][1] = 0.0;
+        Rb[r][0] = (i == 2 * kl + 1) ? 1.0 : 0.0;
+        Rb[r][1] = 0.0;
+    }
+    // this lane's H blocks: slots lane, lane+64, lane+128 of the triangular enumeration
+    int ta[3], tb[3];
+    unsigned pk[3][4];   // rd | wr << 11 | (write conj) << 22 | (diag block) << 23
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int e = lane + 64 * q;
+        ta[q] = -1;
+        tb[q] = 0;
+        if (e < 136) {
+            const int A_ = c_tri_a[e], B_ = c_tri_b[e];
+            if (B_ < P) {
+                ta[q] = A_;
+                tb[q] = B_;
+            }
+        }
+        const int sa = ta[q] < 0 ? 0 : ta[q], sb = tb[q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 2 * sa + (r >> 1), j = 2 * sb + (r & 1);
+            const unsigned rd = i <= j ? up_idx(i, j) : up_idx(j, i);
+            const int ii = circ_next(tx, i), jj = circ_next(tx, j);
+            const unsigned wr = ii <= jj ? up_idx(ii, jj) : up_idx(jj, ii);
+            pk[q][r] = rd | (wr << 11) | ((ii <= jj ? 0u : 1u) << 22) | ((sa == sb ? 1u : 0u) << 23);
+        }
+    }
+    const int rp = up_idx(2 * kl, 2 * kl), rq = up_idx(2 * kl + 1, 2 * kl + 1), rc = up_idx(2 * kl, 2 * kl + 1);
+    int cur = 0;
+    for (; sweeps < 40; ++sweeps) {
+        // convergence pre-check over the off-diagonal entries of this lane's blocks
+        bool need = false;
+        {
+            const d2* H = T0 + cur * ZPACK;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (ta[q] < 0) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 2 * ta[q] + (r >> 1), j = 2 * tb[q] + (r & 1);
+                    if (i < j) need |= needs_rot(H[up_idx(i, i)].x, H[up_idx(j, j)].x, H[up_idx(i, j)], abs_tol);
+                }
+            }
+        }
+        if (!__any(need)) break;
+        for (int s = 0; s < tx - 1; ++s) {
+            const d2* H = T0 + cur * ZPACK;
+            d2* Hn = T0 + (cur ^ 1) * ZPACK;
+            Rot Jl{1.0, 0.0, make_double2(1.0, 0.0), false};
+            if (kl < P) Jl = make_rot(H[rp].x, H[rq].x, H[rc], abs_tol);
+            if (lane < 16) RotS[lane] = make_double4(Jl.cs, Jl.sn, Jl.e.x, Jl.e.y);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (ta[q] < 0) continue;
+                const double4 ra = RotS[ta[q]], rb = RotS[tb[q]];
+                const unsigned p0 = pk[q][0], p1 = pk[q][1], p2 = pk[q][2], p3 = pk[q][3];
+                const bool diagblk = (p0 >> 23) & 1u;
+                const d2 h00 = H[p0 & 2047u], h01 = H[p1 & 2047u], h11 = H[p3 & 2047u];
+                d2 h10 = H[p2 & 2047u];
+                if (diagblk) h10.y = -h10.y;
+                // H'[a,b] = Ja^H H[a,b] Jb,  J = [[cs, sn], [-sn e*, cs e*]]
+                const d2 ebc = make_double2(rb.z, -rb.w), ea = make_double2(ra.z, ra.w);
+                const d2 t01 = cmul(h01, ebc), t11 = cmul(h11, ebc);
+                const d2 T00 = csub(cscale(h00, rb.x), cscale(t01, rb.y));
+                const d2 T01 = cadd(cscale(h00, rb.y), cscale(t01, rb.x));
+                const d2 T10 = csub(cscale(h10, rb.x), cscale(t11, rb.y));
+                const d2 T11 = cadd(cscale(h10, rb.y), cscale(t11, rb.x));
+                const d2 u10 = cmul(ea, T10), u11 = cmul(ea, T11);
+                const d2 n00 = csub(cscale(T00, ra.x), cscale(u10, ra.y));
+                const d2 n01 = csub(cscale(T01, ra.x), cscale(u11, ra.y));
+                const d2 n10 = cadd(cscale(T00, ra.y), cscale(u10, ra.x));
+                const d2 n11 = cadd(cscale(T01, ra.y), cscale(u11, ra.x));
+                auto put = [&](unsigned pw, d2 v) {
+                    Hn[(pw >> 11) & 2047u] = make_double2(v.x, ((pw >> 22) & 1u) ? -v.y : v.y);
+                };
+                put(p0, n00);
+                put(p1, n01);
+                put(p3, n11);
+                if (!diagblk) put(p2, n10);
+            }
+            // R <- R J for this lane's column pair, then the circle-method column permutation
+            {
+                const double cs = Jl.cs, sn = Jl.sn, ex = Jl.e.x, ey = -Jl.e.y;  // e* = (ex, ey)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const double tpr = Rt[r][0], tpi = Rt[r][1];
+                    const double bqr = Rb[r][0] * ex - Rb[r][1] * ey, bqi = Rb[r][0] * ey + Rb[r][1] * ex;
+                    Rt[r][0] = cs * tpr - sn * bqr;
+                    Rt[r][1] = cs * tpi - sn * bqi;
+                    Rb[r][0] = sn * tpr + cs * bqr;
+                    Rb[r][1] = sn * tpi + cs * bqi;
+                }
+                // new top(k) = top(0) | bot(0) | top(k-1) for k = 0 | 1 | >=2; new bot(k) = bot(k+1) | top(P-1).
+                // The shifts run on every lane (DPP sources must be active); lanes k >= P keep theirs.
+                const bool act = P > 1 && kl < P;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    {
+                        const double st0 = dpp_shr1(Rt[r][0]), st1 = dpp_shr1(Rt[r][1]);
+                        const double sb0 = dpp_shr1(Rb[r][0]), sb1 = dpp_shr1(Rb[r][1]);
+                        const double lb0 = dpp_shl1(Rb[r][0]), lb1 = dpp_shl1(Rb[r][1]);
+                        const double nt0 = kl == 0 ? Rt[r][0] : (kl == 1 ? sb0 : st0);
+                        const double nt1 = kl == 0 ? Rt[r][1] : (kl == 1 ? sb1 : st1);
+                        const double nb0 = kl == P - 1 ? Rt[r][0] : lb0;
+                        const double nb1 = kl == P - 1 ? Rt[r][1] : lb1;
+                        if (act) {
+                            Rt[r][0] = nt0;
+                            Rt[r][1] = nt1;
+                            Rb[r][0] = nb0;
+                            Rb[r][1] = nb1;
+                        }
+                    }
+                }
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+    }
+    if (sweeps >= 40 && lane == 0) atomicOr(&st->status, (int)ACE_ST_EIG_NOCONV);
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_t2 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+    // ---- eigen order (LAPACK ascending, then MATLAB's stable descending sort, :429-430)
+    if (lane < tx) wv[lane] = T0[cur * ZPACK + up_idx(lane, lane)].x;
+    __syncthreads();
+    if (lane < tx) {
+        const double wk = wv[lane];
+        int asc = 0;
+        for (int j = 0; j < tx; ++j) asc += (wv[j] < wk) || (wv[j] == wk && j < lane);
+        ascp[lane] = asc;
+    }
+    __syncthreads();
+    if (lane < tx) {
+        const double sk = fmax(0.0, wv[lane]);
+        const int asc = ascp[lane];
+        int rank = 0;
+        for (int j = 0; j < tx; ++j) {
+            const double sj = fmax(0.0, wv[j]);
+            rank += (sj > sk) || (sj == sk && ascp[j] < asc);
+        }
+        ord[rank] = lane;
+    }
+    if (lane < ZT) scl[lane] = 1.0;
+    __syncthreads();
+    if (lane == 0) {  // rank-profile tail rescaling (:469-480), sequential sums
+        for (int k = 0; k < tx; ++k) rs2[k] = fmax(0.0, wv[ord[k]]);
+        for (int pi = 0; pi < a.np; ++pi) {
+            const int r = a.rl[pi];
+            const double f = a.fl[pi];
+            double vr = 0.0, v = 0.0;
+            for (int k = 0; k < r; ++k) vr += rs2[k];
+            for (int k = 0; k < tx; ++k) v += rs2[k];
+            if (vr < v * f) {
+                const double sc = fmin(1.0, vr / (v - vr) * (1.0 / f - 1.0));
+                for (int k = r; k < tx; ++k) {
+                    rs2[k] *= sc;
+                    scl[ord[k]] *= sc;
+                }
+            }
+        }
+        int any = 0;
+        for (int k = 0; k < tx; ++k) any |= scl[k] < 1.0;
+        flag_any = any;
+    }
+    // ---- R -> T0, Qnew = Qprev R -> T0 and global (next iteration's warm start)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int i = g + 4 * r;
+        T0[i * ZHS + 2 * kl] = make_double2(Rt[r][0], Rt[r][1]);
+        T0[i * ZHS + 2 * kl + 1] = make_double2(Rb[r][0], Rb[r][1]);
+    }
+    __syncthreads();
+    if (warm) {
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int J = 0; J < 2; ++J)
+                mm16([&](int r, int k) { return qprev(16 * I + r, k); },
+                     [&](int, int k, int c) { return T0[k * ZHS + 16 * J + c]; }, cr[I][J], ci[I][J], lane);
+        __syncthreads();
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int J = 0; J < 2; ++J)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    T0[(16 * I + (lane >> 4) + 4 * r) * ZHS + 16 * J + (lane & 15)] =
+                        make_double2(cr[I][J][r], ci[I][J][r]);
+        __syncthreads();
+    }
+    if (a.Q) {
+        for (int e = lane; e < tx * tx; e += 64) Qg[e] = T0[(e / tx) * ZHS + (e % tx)];
+    }
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_t3 = __builtin_amdgcn_s_memrealtime();
+#endif
+    }  // !fast
+    __syncthreads();
+
+    // per-element update + reductions: nX2, nZ2, nJN2, dZ2
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    auto emit = [&](int k, d2 znew) {
+        const d2 x = X[k];
+        if (!INIT) {
+            const d2 zo = Z[k];
+            const d2 d = csub(x, znew);
+            N[k] = cadd(N[k], cscale(d, mu));
+            acc[0] += cabs2(x);
+            acc[1] += cabs2(znew);
+            acc[2] += cabs2(d);
+            acc[3] += cabs2(csub(znew, zo));
+        }
+        Z[k] = znew;
+    };
+    if (flag_any) {
+        // per column block J of E: T(:, J) = diag(sqrt(scl)) Qnew^H E(:, J) (rows = eigen indices),
+        // then Z^T(J, :) = T(:, J)^T Qnew^T with A = T^T straight from the accumulators and
+        // B = Qnew^T from T0.  Output block (J, I): row j (Z column), col i (Z row), so the
+        // vec index i + tx*j runs along the lanes.
+#pragma unroll
+        for (int J = 0; J < 2; ++J) {
+#pragma unroll
+            for (int K = 0; K < 2; ++K) {
+                mm16([&](int r, int k) { const d2 q = T0[k * ZHS + 16 * K + r]; return make_double2(q.x, -q.y); },
+                     [&](int, int k, int c) {
+                         const int j = 16 * J + c;
+                         return (k < tx && j < rx) ? evalE(k + tx * j) : zero;
+                     },
+                     cr[K][0], ci[K][0], lane);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double w = sqrt(scl[16 * K + (lane >> 4) + 4 * r]);
+                    cr[K][0][r] *= w;
+                    ci[K][0][r] *= w;
+                }
+            }
+#pragma unroll
+            for (int I = 0; I < 2; ++I) {
+                d4v zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int K = 0; K < 2; ++K)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int kk = 16 * K + 4 * q + (lane >> 4);
+                        const d2 av = make_double2(cr[K][0][q], ci[K][0][q]);       // T[kk][16J + (lane&15)]
+                        const d2 bv = T0[(16 * I + (lane & 15)) * ZHS + kk];          // Qnew[16I + c][kk]
+                        mfma_c(av, bv, zr, zi);
+                    }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 * J + (lane >> 4) + 4 * r, i = 16 * I + (lane & 15);
+                    if (i < tx && j < rx) emit(i + tx * j, make_double2(zr[r], zi[r]));
+                }
+            }
+        }
+    } else {
+        for (int k = lane; k < n; k += 64) emit(k, evalE(k));
+    }
+#ifdef ACE_DEBUG_SWEEPS
+    const unsigned long long dbg_t4 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && (b == 0 || b == 2000) && (a.it < 4 || a.it % 20 == 0))
+        printf("1w b %d it %d sweeps %d pre %llu jac %llu order+Q %llu emit %llu (x10ns)\n", b, a.it, sweeps,
+               dbg_t1 - dbg_t0, dbg_t2 - dbg_t1, dbg_t3 - dbg_t2, dbg_t4 - dbg_t3);
+#endif
+    if (INIT) return;
+
+    // m-space dual terms: ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0),  ||A^H Y||^2 = Y^H K Y
+    double dAtY = 0.0, nAtY = 0.0;
+    {
+        const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
+        const d2* Yo = reinterpret_cast<const d2*>(a.Yold) + (long long)b * m;
+        const d2* Kn = reinterpret_cast<const d2*>(a.KYnew) + (long long)b * m;
+        const d2* Ko = reinterpret_cast<const d2*>(a.KYold) + (long long)b * m;
+        for (int i = lane; i < m; i += 64) {
+            const d2 yn = Yn[i], kn = Kn[i];
+            const d2 dy = csub(yn, Yo[i]), dk = csub(kn, Ko[i]);
+            dAtY += dy.x * dk.x + dy.y * dk.y;
+            nAtY += yn.x * kn.x + yn.y * kn.y;
+        }
+    }
+    const double s_nX2 = wave_sum(acc[0]), s_nZ2 = wave_sum(acc[1]), s_jn2 = wave_sum(acc[2]),
+                 s_dZ2 = wave_sum(acc[3]), s_dAtY = wave_sum(dAtY), s_nAtY = wave_sum(nAtY);
+    int improved = 0;
+    if (lane == 0)
+        improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
+    improved = __shfl(improved, 0, 64);
+    if (improved) {
+        d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
+        d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
+        const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
+        for (int k = lane; k < n; k += 64) oX[k] = X[k];
+        for (int i = lane; i < m; i += 64) oY[i] = Yn[i];
+    }
+}
+}  // namespace
+
+void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st) {
+    if (init) hipLaunchKernelGGL(zstep1w_kernel<true>, dim3(batch), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(zstep1w_kernel<false>, dim3(batch), dim3(64), 0, st, a);
+}
+
+}  // namespace ace

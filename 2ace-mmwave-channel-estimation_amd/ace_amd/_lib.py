@@ -24,6 +24,7 @@ ACE_VARIANT_NUCLEAR = 1
 ACE_ST_CONVERGED = 1
 ACE_ST_NO_OPT = 2
 ACE_ST_EIG_NOCONV = 4
+ACE_ST_ROLLBACK = 8
 
 KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final"]
 
@@ -52,6 +53,23 @@ class AdmmCfg(C.Structure):
     ]
 
 
+class PipelineCfg(C.Structure):
+    """Mirror of ``ace_pipeline_cfg`` (include/ace.h)."""
+    _fields_ = [
+        ("variant", C.c_int),
+        ("restarts", C.c_int),
+        ("r", C.c_int),
+        ("maxiter", C.c_int),
+        ("eig_warm", C.c_int),
+        ("reserved", C.c_int * 3),
+        ("mu0", C.c_double),
+        ("rho", C.c_double),
+        ("cc_frac", C.c_double),
+        ("tol_rel", C.c_double),
+        ("tol_abs", C.c_double),
+    ]
+
+
 def _load():
     if not LIB_PATH.exists():
         raise ImportError(
@@ -71,6 +89,17 @@ def _load():
     lib.ace_admm_solve_host.argtypes = [cfgp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         dp, dp, dp, dp, dp, ip, up, dp]
     lib.ace_admm_solve_host.restype = C.c_int
+    pcfgp = C.POINTER(PipelineCfg)
+    lib.ace_pipeline_cfg_default.argtypes = [pcfgp, C.c_int]
+    lib.ace_pipeline_cfg_default.restype = None
+    lib.ace_pipeline_workspace_size.argtypes = [pcfgp, C.c_int, C.c_int, C.c_int]
+    lib.ace_pipeline_workspace_size.restype = C.c_size_t
+    lib.ace_pipeline_solve_batch.argtypes = [pcfgp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             vp, vp, ip, vp, vp, vp, vp, vp, vp, C.c_size_t, vp]
+    lib.ace_pipeline_solve_batch.restype = C.c_int
+    lib.ace_pipeline_solve_host.argtypes = [pcfgp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            dp, dp, ip, dp, dp, dp, ip, up]
+    lib.ace_pipeline_solve_host.restype = C.c_int
     lib.ace_synth_codebook.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, vp, vp]
     lib.ace_synth_codebook.restype = C.c_int
     lib.ace_synth_channels.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -102,5 +131,15 @@ def default_cfg(**kw) -> AdmmCfg:
     for k, v in kw.items():
         if not hasattr(cfg, k):
             raise TypeError(f"unknown ace_admm_cfg field {k!r}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+def pipeline_cfg(variant, **kw) -> PipelineCfg:
+    cfg = PipelineCfg()
+    LIB.ace_pipeline_cfg_default(C.byref(cfg), int(variant))
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise TypeError(f"unknown ace_pipeline_cfg field {k!r}")
         setattr(cfg, k, v)
     return cfg

@@ -1,0 +1,188 @@
+"""Host-side mirror of the reference's full recovery functions, backed by the HIP pipeline.
+
+Reference (main/src/my_recovery_algorithms/ADMM_v2/):
+  [X, Y, quality] = inferLowRankV4_multi(A, B, tx, rx, lambda, r, mu0, rho, cc_frac,
+                                         tol_rel, tol_abs, maxiter)      (inferLowRankV4_multi.m:5)
+  [X, Y, quality] = inferLowRank_Nuclear(...)                            (inferLowRank_Nuclear.m)
+  inferLowRankV4 (Numerical_Simulation/src/my_recovery_algorithms/ADMM_v2/inferLowRankV4.m):
+  the one-restart form of inferLowRankV4_multi.
+
+MATLAB's ``randsample(m, floor(m*cc_frac))`` (:48) is replaced by explicit train
+partitions: ``train_idx`` ([restarts][m_t] shared by a batch, or [batch][restarts][m_t])
+or, when omitted, a numpy Generator drawing a random permutation prefix per restart
+(the same distribution as randsample without replacement; MATLAB's stream itself is
+not reproducible outside MATLAB).
+
+Entry points:
+  * ``inferLowRankV4_multi`` / ``inferLowRankV4`` / ``inferLowRank_Nuclear`` -- one
+    realisation, MATLAB argument order, numpy in / out ((n,1), (m,1), quality).
+  * ``infer_low_rank_pipeline_host`` -- a batch on host arrays; realisations whose
+    partitions coincide are solved in one GPU batch (ace_pipeline_solve_host).
+  * ``infer_low_rank_pipeline_batch`` -- device tensors already in HBM, one shared
+    partition set (ace_pipeline_solve_batch); the throughput path.
+There is no CPU fallback: every call goes through libace.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import LIB, check, pipeline_cfg, ACE_ST_ROLLBACK
+from .solver import VARIANTS
+
+
+@dataclass
+class PipelineResult:
+    X: object            # [batch][n] complex128
+    Y: object            # [batch][m] complex128
+    quality: object      # [batch] float64 (last restart's, as the reference returns)
+    stage_iters: object  # [batch][4*restarts+1] int32
+    status: object       # [batch] uint32 (ACE_ST_* bits)
+
+    @property
+    def rolled_back(self):
+        return (self.status & ACE_ST_ROLLBACK) != 0
+
+
+def _cfg(variant, restarts, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm):
+    v = VARIANTS[variant]
+    kw = dict(r=int(r), mu0=float(mu0), rho=float(rho), cc_frac=float(cc_frac), tol_rel=float(tol_rel),
+              tol_abs=float(tol_abs), maxiter=int(maxiter), eig_warm=int(bool(eig_warm)))
+    if restarts is not None:
+        kw["restarts"] = int(restarts)
+    return pipeline_cfg(v, **kw)
+
+
+def draw_partitions(rng, m, restarts, cc_frac=0.95):
+    """randsample(m, floor(m*cc_frac)) per restart (inferLowRankV4_multi.m:48), 0-based."""
+    mt = math.floor(m * cc_frac)
+    return np.stack([rng.permutation(m)[:mt] for _ in range(restarts)]).astype(np.int32)
+
+
+def infer_low_rank_pipeline_host(A, B, tx, rx, train_idx, *, variant="A2only", restarts=None, r=20, mu0=1e-3,
+                                 rho=1.03, cc_frac=0.95, tol_rel=1e-4, tol_abs=1e-8, maxiter=500,
+                                 eig_warm=True) -> PipelineResult:
+    """Pipeline on host arrays.  A: [m][n] (one codebook), B: [batch][m],
+    train_idx: [restarts][m_t] (shared) or [batch][restarts][m_t]."""
+    A = np.ascontiguousarray(A, dtype=np.complex128)
+    if A.ndim == 3 and A.shape[0] == 1:
+        A = A[0]
+    B = np.ascontiguousarray(np.atleast_2d(np.asarray(B, dtype=np.float64)))
+    batch, m = B.shape
+    if A.ndim != 2 or A.shape[0] != m:
+        raise ValueError(f"shape mismatch: A{A.shape} B{B.shape}")
+    n = A.shape[1]
+    tr = np.asarray(train_idx, dtype=np.int32)
+    if tr.ndim == 2:
+        tr = np.broadcast_to(tr, (batch,) + tr.shape)
+    if tr.ndim != 3 or tr.shape[0] != batch:
+        raise ValueError(f"train_idx must be [restarts][m_t] or [batch][restarts][m_t], got {tr.shape}")
+    nres = tr.shape[1] if restarts is None else int(restarts)
+    cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
+    if tr.shape[1] != cfg.restarts:
+        raise ValueError(f"train_idx holds {tr.shape[1]} partitions, cfg.restarts = {cfg.restarts}")
+    ld = 4 * cfg.restarts + 1
+    X = np.empty((batch, n), np.complex128)
+    Y = np.empty((batch, m), np.complex128)
+    q = np.empty(batch, np.float64)
+    its = np.empty((batch, ld), np.int32)
+    stt = np.empty(batch, np.uint32)
+    groups = {}
+    for b in range(batch):
+        groups.setdefault(tr[b].tobytes(), []).append(b)
+    for key, members in groups.items():
+        idx = np.asarray(members)
+        part = np.ascontiguousarray(tr[idx[0]])
+        Bg = np.ascontiguousarray(B[idx])
+        g = len(idx)
+        Xg = np.empty((g, n), np.complex128)
+        Yg = np.empty((g, m), np.complex128)
+        qg = np.empty(g, np.float64)
+        ig = np.empty((g, ld), np.int32)
+        sg = np.empty(g, np.uint32)
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        check(LIB.ace_pipeline_solve_host(
+            C.byref(cfg), g, m, n, tx, rx, dp(A.view(np.float64)), dp(Bg),
+            part.ctypes.data_as(C.POINTER(C.c_int32)), dp(Xg.view(np.float64)), dp(Yg.view(np.float64)),
+            dp(qg), ig.ctypes.data_as(C.POINTER(C.c_int32)), sg.ctypes.data_as(C.POINTER(C.c_uint32))))
+        X[idx], Y[idx], q[idx], its[idx], stt[idx] = Xg, Yg, qg, ig, sg
+    return PipelineResult(X, Y, q, its, stt)
+
+
+def _single(A, B, tx, rx, lambda_, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, train_idx, rng, variant,
+            restarts):
+    if lambda_ != 0:
+        raise NotImplementedError("lambda != 0 is unreachable from the reference drivers and not implemented")
+    A = np.asarray(A, dtype=np.complex128)
+    m = A.shape[0]
+    if train_idx is None:
+        train_idx = draw_partitions(rng if rng is not None else np.random.default_rng(), m, restarts, cc_frac)
+    res = infer_low_rank_pipeline_host(A, np.asarray(B, dtype=np.float64).reshape(1, m), tx, rx,
+                                       np.asarray(train_idx).reshape(restarts, -1), variant=variant,
+                                       restarts=restarts, r=r, mu0=mu0, rho=rho, cc_frac=cc_frac,
+                                       tol_rel=tol_rel, tol_abs=tol_abs, maxiter=maxiter)
+    n = A.shape[1]
+    return res.X[0].reshape(n, 1), res.Y[0].reshape(m, 1), float(res.quality[0])
+
+
+def inferLowRankV4_multi(A, B, tx, rx, lambda_=0.0, r=20, mu0=1e-3, rho=1.03, cc_frac=0.95, tol_rel=1e-4,
+                         tol_abs=1e-8, maxiter=500, *, train_idx=None, rng=None):
+    """[X, Y, quality] = inferLowRankV4_multi(...) (3 restarts, keep the best)."""
+    return _single(A, B, tx, rx, lambda_, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, train_idx, rng,
+                   "A2only", 3)
+
+
+def inferLowRankV4(A, B, tx, rx, lambda_=0.0, r=20, mu0=1e-3, rho=1.03, cc_frac=0.95, tol_rel=1e-4,
+                   tol_abs=1e-8, maxiter=500, *, train_idx=None, rng=None):
+    """Numerical_Simulation's inferLowRankV4: the one-restart pipeline."""
+    return _single(A, B, tx, rx, lambda_, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, train_idx, rng,
+                   "A2only", 1)
+
+
+def inferLowRank_Nuclear(A, B, tx, rx, lambda_=0.0, r=20, mu0=1e-3, rho=1.03, cc_frac=0.95, tol_rel=1e-4,
+                         tol_abs=1e-8, maxiter=500, *, train_idx=None, rng=None):
+    """[X, Y, quality] = inferLowRank_Nuclear(...) (one restart, nuclear-norm Z-prox)."""
+    return _single(A, B, tx, rx, lambda_, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, train_idx, rng,
+                   "A2nuclear", 1)
+
+
+def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", restarts=None, r=20, mu0=1e-3,
+                                  rho=1.03, cc_frac=0.95, tol_rel=1e-4, tol_abs=1e-8, maxiter=500,
+                                  eig_warm=True, workspace=None, stream=None) -> PipelineResult:
+    """Batched pipeline on device tensors: A [m][n] complex128 (shared codebook),
+    B [batch][m] float64, train_idx [restarts][m_t] (host, shared by the batch)."""
+    import torch
+    from .solver import _DEFAULT_WS
+    if not (A.is_cuda and B.is_cuda):
+        raise ValueError("infer_low_rank_pipeline_batch needs device tensors")
+    if A.dtype != torch.complex128 or B.dtype != torch.float64:
+        raise TypeError("A must be complex128 and B float64")
+    if A.dim() == 3 and A.shape[0] == 1:
+        A = A[0]
+    A, B = A.contiguous(), B.contiguous()
+    batch, m = B.shape
+    n = A.shape[1]
+    tr = np.ascontiguousarray(np.asarray(train_idx, dtype=np.int32))
+    nres = tr.shape[0] if restarts is None else int(restarts)
+    cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
+    ld = 4 * cfg.restarts + 1
+    dev = A.device
+    out = PipelineResult(torch.empty((batch, n), dtype=torch.complex128, device=dev),
+                         torch.empty((batch, m), dtype=torch.complex128, device=dev),
+                         torch.empty(batch, dtype=torch.float64, device=dev),
+                         torch.empty((batch, ld), dtype=torch.int32, device=dev),
+                         torch.empty(batch, dtype=torch.int32, device=dev))
+    nbytes = int(LIB.ace_pipeline_workspace_size(C.byref(cfg), batch, m, n)) + 256
+    if nbytes <= 256:
+        raise ValueError(LIB.ace_last_error().decode() or "invalid pipeline configuration")
+    ws = (workspace or _DEFAULT_WS).get(nbytes, dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    check(LIB.ace_pipeline_solve_batch(C.byref(cfg), batch, m, n, tx, rx, A.data_ptr(), B.data_ptr(),
+                                       tr.ctypes.data_as(C.POINTER(C.c_int32)), out.X.data_ptr(),
+                                       out.Y.data_ptr(), out.quality.data_ptr(), out.stage_iters.data_ptr(),
+                                       out.status.data_ptr(), ws.data_ptr(), ws.numel(), stream.cuda_stream))
+    return out

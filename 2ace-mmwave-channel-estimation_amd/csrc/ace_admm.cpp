@@ -1,0 +1,166 @@
+// The batched InferADMM driver (main/src/my_recovery_algorithms/ADMM_v2/
+// inferLowRankV4_multi.m:281-386), shared by the unit solve (ace_admm_solve_batch,
+// r = 1) and the pipeline stages (ace_pipeline.cpp: r = 20 row / column modes of
+// inferLowRankImpl :258/:270, and the r = 1 refinement :92/:100).
+//
+//   setup   K = A A^H, G = (I + K)^{-1}          (replaces U = inv(A'A+I), :242/:286-289)
+//   init    :296-310
+//   iterate :318-383, one kernel sequence per iteration:
+//     pre    V = Z - N/mu, S = Y - M/mu
+//     T = S - A V          (MFMA GEMM over batch*r vectors, shared A | GEMV, private A)
+//     g = G T
+//     ystep  AX = S - g, ArgMinY, M update        (:326-337)
+//     KY = K Y                                    (for ||A'Y||, ||A'(Y-Y0)||)
+//     X = V + A^H g                               (ArgMinX, :325)
+//     zstep  ArgMinZ, N update, residuals, stop test, best tracking, mu update
+//   finalize opt_X / opt_Y (:384-385)
+#include "ace_host.hpp"
+
+namespace ace {
+
+size_t linops_bytes(bool shared, int batch, int m, int n) {
+    Carver cv{nullptr};
+    LinOps L;
+    linops_carve(cv, shared, batch, m, n, &L);
+    return cv.off;
+}
+
+void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
+    const size_t cz = 16, mats = shared ? 1 : (size_t)batch;
+    L->shared = shared;
+    L->m = m;
+    L->n = n;
+    L->AH = shared ? cv.take(cz * n * m) : nullptr;
+    L->K = cv.take(cz * mats * m * m);
+    L->G = cv.take(cz * mats * m * m);
+}
+
+int linops_setup(LinOps& L, int batch, hipStream_t st) {
+    const int m = L.m, n = L.n;
+    const int mats = L.shared ? 1 : batch;
+    const long long mm = (long long)m * m, mn = (long long)m * n;
+    ProfScope ps(ACE_K_SETUP, st);
+    // K[j][i] = sum_k conj(A[i][k]) A[j][k]  : GEMM with L = conj(A), V = rows of A
+    launch_zgemm(0, true, m, n, m, L.A, n, mn, L.A, n, mn, L.K, nullptr, m, mm, mats, st);
+    ACE_HIP(hipMemcpyAsync(L.G, L.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
+    launch_inv_ipk(m, mats, L.G, mm, st);
+    if (L.shared) launch_conj_transpose(m, n, L.A, L.AH, st);
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) {
+    const size_t cz = 16, bn = (size_t)batch * r * n, bm = (size_t)batch * r * m;
+    s->X = cv.take(cz * bn);
+    s->Z = cv.take(cz * bn);
+    s->N = cv.take(cz * bn);
+    s->V = cv.take(cz * bn);
+    s->optX = cv.take(cz * bn);
+    s->Q = cv.take(cz * (size_t)batch * 32 * 32);
+    for (int i = 0; i < 2; ++i) s->Y[i] = cv.take(cz * bm);
+    for (int i = 0; i < 2; ++i) s->KY[i] = cv.take(cz * bm);
+    s->M = cv.take(cz * bm);
+    s->S = cv.take(cz * bm);
+    s->T = cv.take(cz * bm);
+    s->g = cv.take(cz * bm);
+    s->optY = cv.take(cz * bm);
+    s->st = cv.take<RealState>(sizeof(RealState) * (size_t)batch);
+    s->done = cv.take<int>(256);
+}
+
+int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch, const double* B,
+             const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu_out,
+             hipStream_t st) {
+    const int m = L.m, n = L.n, r = p.r;
+    if (!L.shared && r != 1) return fail(ACE_ERR_UNSUPPORTED, "private sensing matrices support r = 1 only");
+    const int row_mode = (r == 1) ? 1 : p.row_mode;   // the two modes coincide at r = 1
+    const int nv = batch * r;                         // vectors per apply
+    const long long mm = (long long)m * m, mn = (long long)m * n;
+    const bool fast = (r == 1);                       // r = 1 kernels (ystep, one-wave zstep)
+
+    auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
+        if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
+        else launch_zgemv_rows(mode, m, n, batch, L.A, mn, Vin, n, C, E, m, st);
+    };
+    auto applyMM = [&](const double* Lm, const double* Vin, double* C) {  // C = L Vin, L = G or K
+        if (L.shared) launch_zgemm(0, false, m, m, nv, Lm, m, 0, Vin, m, 0, C, nullptr, m, 0, 1, st);
+        else launch_zgemv_rows(0, m, m, batch, Lm, mm, Vin, m, C, nullptr, m, st);
+    };
+    auto applyAH = [&](const double* gin, double* C, const double* E) {  // C = E + A^H gin
+        if (L.shared) launch_zgemm(2, false, n, m, nv, L.AH, m, 0, gin, m, 0, C, E, n, 0, 1, st);
+        else launch_zgemv_cols(2, m, n, batch, L.A, mn, gin, m, C, E, n, st);
+    };
+
+    ZArgs za{};
+    za.n = n;
+    za.m = m;
+    za.tx = p.tx;
+    za.rx = p.rx;
+    za.r = r;
+    za.row_mode = row_mode;
+    za.X = w.X;
+    za.N = w.N;
+    za.Z = w.Z;
+    za.Q = w.Q;
+    za.st = w.st;
+    za.optX = w.optX;
+    za.optY = w.optY;
+    za.done_count = w.done;
+    za.np = rank_profile(p.tx, p.rx, m, n, p.rank_one ? 0 : p.use_rank_one, za.rl, za.fl);
+    za.rank_one = p.rank_one;
+    za.tol_rel = p.tol_rel;
+    za.tol_abs = p.tol_abs;
+    za.rho = p.rho;
+    za.fixed_iters = p.fixed_iters;
+    za.warm = p.eig_warm;
+
+    // ---- init (:296-310)
+    ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
+    {
+        ProfScope ps(ACE_K_INIT, st);
+        applyA(0, X0, w.T, nullptr);                             // AX = A*X0
+        launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st);
+        za.it = 0;
+        launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)
+        applyMM(L.K, w.Y[0], w.KY[0]);                           // K*Y (for A'*Y terms)
+    }
+    ACE_HIP(hipGetLastError());
+
+    int q = 0;
+    const int poll = 8;
+    for (int it = 1; it <= p.maxiter; ++it) {
+        { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
+        { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }          // T = S - A V
+        { ProfScope ps(ACE_K_APPLY_G, st); applyMM(L.G, w.T, w.g); }            // g = G T
+        {
+            ProfScope ps(ACE_K_YSTEP, st);
+            if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+            else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+        }
+        { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
+        { ProfScope ps(ACE_K_APPLY_AH, st); applyAH(w.g, w.X, w.V); }           // X = V + A^H g
+        za.it = it;
+        za.Ynew = w.Y[1 - q];
+        za.Yold = w.Y[q];
+        za.KYnew = w.KY[1 - q];
+        za.KYold = w.KY[q];
+        { ProfScope ps(ACE_K_ZSTEP, st); launch_zstep(p.variant, false, za, batch, st); }
+        q = 1 - q;
+        if (!p.fixed_iters && (it % poll == 0) && it < p.maxiter) {
+            int h_done = 0;
+            ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
+            ACE_HIP(hipStreamSynchronize(st));
+            if (h_done >= batch) break;
+        }
+    }
+    ACE_HIP(hipGetLastError());
+    {
+        ProfScope ps(ACE_K_FINAL, st);
+        launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, w.X, w.Y[q], Xo, Yo, iters, status,
+                          mu_out, w.st, st);
+    }
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+}  // namespace ace

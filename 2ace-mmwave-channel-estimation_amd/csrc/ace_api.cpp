@@ -1,136 +1,14 @@
-// Host driver and C-ABI (include/ace.h) of the MI355X 2ACE ADMM hot path.
-//
-// ace_admm_solve_batch runs InferADMM (main/src/my_recovery_algorithms/ADMM_v2/
-// inferLowRankV4_multi.m:281-386) for a batch of independent realisations:
-//   setup   K = A A^H, G = (I + K)^{-1}          (replaces U = inv(A'A+I), :286-289)
-//   init    :296-310
-//   iterate :318-383, one kernel sequence per iteration:
-//     pre    V = Z - N/mu, S = Y - M/mu
-//     T = S - A V          (MFMA GEMM, shared A  | GEMV, private A)
-//     g = G T
-//     ystep  AX = S - g, ArgMinY, M update        (:326-337)
-//     KY = K Y                                    (for ||A'Y||, ||A'(Y-Y0)||)
-//     X = V + A^H g                               (ArgMinX, :325)
-//     zstep  ArgMinZ, N update, residuals, stop test, best tracking, mu update
-//   finalize opt_X / opt_Y (:384-385)
-#include <hip/hip_runtime.h>
-
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
+// C-ABI (include/ace.h) of the MI355X 2ACE ADMM hot path: the unit solve
+// ace_admm_solve_batch (InferADMM at r = 1, main/src/my_recovery_algorithms/ADMM_v2/
+// inferLowRankV4_multi.m:281-386, driven by admm_run in ace_admm.cpp), its host-buffer
+// wrapper, synthetic traces, kernel timing, error text and version.
 #include <cstring>
-#include <string>
-#include <vector>
 
-#include "ace_common.hpp"
+#include "ace_host.hpp"
 
 using namespace ace;
 
 namespace {
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-#define ACE_HIP(call)                                                                                  \
-    do {                                                                                               \
-        hipError_t e_ = (call);                                                                        \
-        if (e_ != hipSuccess) return fail(ACE_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
-                                          __FILE__, __LINE__);                                         \
-    } while (0)
-
-// ArgMinZ rank profile (inferLowRankV4_multi.m:437-464)
-int rank_profile(int tx, int rx, int m, int n, int use_rank_one, int* rl, double* fl) {
-    const int sz = tx < rx ? tx : rx;
-    const int r0 = (int)std::ceil(std::sqrt((double)sz) * 0.5), r1 = (int)std::ceil(std::sqrt((double)sz) * 0.7);
-    const int r2 = (int)std::ceil(std::sqrt((double)sz));
-    int r3 = (int)std::ceil(std::sqrt((double)sz) * 2.0);
-    if (r3 > sz) r3 = sz;
-    if (use_rank_one) { rl[0] = 1; fl[0] = 0.95; return 1; }
-    if (m >= n * 3) { rl[0] = r3; fl[0] = 0.995; return 1; }
-    if (r1 <= 2) { rl[0] = r2; fl[0] = 0.95; return 1; }
-    if (r0 <= 2) {
-        rl[0] = r1; rl[1] = r2; rl[2] = r3;
-        fl[0] = 0.9; fl[1] = 0.95; fl[2] = 0.995;
-        return 3;
-    }
-    rl[0] = r0; rl[1] = r1; rl[2] = r2; rl[3] = r3;
-    fl[0] = 0.8; fl[1] = 0.9; fl[2] = 0.95; fl[3] = 0.995;
-    return 4;
-}
-
-// Workspace carve-up (all chunks 256-B aligned).
-struct Ws {
-    double *AH, *K, *G;                      // shared: AH n x m; K, G: [mats][m][m]
-    double *X, *Z, *N, *V, *optX, *Q;        // [batch][n], Q [batch][tx*tx]
-    double *Y[2], *KY[2], *M, *S, *T, *g, *optY;  // [batch][m]
-    RealState* st;
-    int* done;
-    size_t bytes;
-};
-
-size_t carve(const ace_admm_cfg* c, int batch, int m, int n, int tx, char* base, Ws* w) {
-    size_t off = 0;
-    auto take = [&](size_t bytes) -> char* {
-        char* p = base ? base + off : nullptr;
-        off += (bytes + 255) & ~(size_t)255;
-        return p;
-    };
-    const size_t cz = 16;
-    const size_t mats = c->a_shared ? 1 : (size_t)batch;
-    w->AH = c->a_shared ? (double*)take(cz * n * m) : nullptr;
-    w->K = (double*)take(cz * mats * m * m);
-    w->G = (double*)take(cz * mats * m * m);
-    w->X = (double*)take(cz * batch * n);
-    w->Z = (double*)take(cz * batch * n);
-    w->N = (double*)take(cz * batch * n);
-    w->V = (double*)take(cz * batch * n);
-    w->optX = (double*)take(cz * batch * n);
-    w->Q = (c->variant == ACE_VARIANT_A2ONLY) ? (double*)take(cz * batch * tx * tx) : nullptr;
-    for (int i = 0; i < 2; ++i) w->Y[i] = (double*)take(cz * batch * m);
-    for (int i = 0; i < 2; ++i) w->KY[i] = (double*)take(cz * batch * m);
-    w->M = (double*)take(cz * batch * m);
-    w->S = (double*)take(cz * batch * m);
-    w->T = (double*)take(cz * batch * m);
-    w->g = (double*)take(cz * batch * m);
-    w->optY = (double*)take(cz * batch * m);
-    w->st = (RealState*)take(sizeof(RealState) * batch);
-    w->done = (int*)take(256);
-    w->bytes = off;
-    return off;
-}
-
-// ---- event-pair kernel timing (ace_prof_start / ace_prof_stop)
-struct Prof {
-    bool on = false;
-    std::vector<hipEvent_t> ev;   // 2 per record
-    std::vector<int> cls;
-    size_t used = 0;
-} g_prof;
-
-struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
-    hipStream_t st;
-    int idx = -1;
-    ProfScope(int c, hipStream_t s) : st(s) {
-        if (g_prof.on && g_prof.used < g_prof.cls.size()) {
-            idx = (int)g_prof.used++;
-            g_prof.cls[idx] = c;
-            (void)hipEventRecord(g_prof.ev[2 * idx], st);
-        }
-    }
-    ~ProfScope() {
-        if (idx >= 0) (void)hipEventRecord(g_prof.ev[2 * idx + 1], st);
-    }
-};
-
 int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
     if (!c) return fail(ACE_ERR_ARG, "cfg is NULL");
     if (batch < 1 || m < 1 || n < 1) return fail(ACE_ERR_ARG, "batch/m/n must be >= 1 (got %d/%d/%d)", batch, m, n);
@@ -202,8 +80,12 @@ void ace_admm_cfg_default(ace_admm_cfg* c) {
 
 size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n) {
     if (!cfg || batch < 1 || m < 1 || n < 1) return 0;
-    Ws w;  // Q is sized for the largest supported tx (32)
-    return carve(cfg, batch, m, n, 32, nullptr, &w) + 256;
+    Carver cv{nullptr};
+    LinOps L;
+    AdmmState w;
+    linops_carve(cv, cfg->a_shared != 0, batch, m, n, &L);
+    admm_state_carve(cv, batch, m, n, 1, &w);
+    return cv.off + 256;
 }
 
 int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
@@ -214,102 +96,32 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     if (rc) return rc;
     if (!A || !B || !X0 || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
-    Ws w;
-    char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-    const size_t need = carve(cfg, batch, m, n, 32, nullptr, &w) + (size_t)(base - (char*)workspace);
+    const size_t need = ace_admm_workspace_size(cfg, batch, m, n);
     if (need > workspace_bytes)
         return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
-    carve(cfg, batch, m, n, 32, base, &w);
-    const bool shared = cfg->a_shared != 0;
-    const long long mm = (long long)m * m, mn = (long long)m * n;
-
-    // ---- setup: K = A A^H, G = (I + K)^{-1}, A^H (shared regime)
-    const int mats = shared ? 1 : batch;
-    {
-    ProfScope ps(ACE_K_SETUP, st);
-    // K[j][i] = sum_k conj(A[i][k]) A[j][k]  : GEMM with L = conj(A), V = rows of A
-    launch_zgemm(0, true, m, n, m, A, n, mn, A, n, mn, w.K, nullptr, m, mm, mats, st);
-    ACE_HIP(hipMemcpyAsync(w.G, w.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
-    launch_inv_ipk(m, mats, w.G, mm, st);
-    if (shared) launch_conj_transpose(m, n, A, w.AH, st);
-    }
-    ACE_HIP(hipGetLastError());
-
-    auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
-        if (shared) launch_zgemm(mode, false, m, n, batch, A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
-        else launch_zgemv_rows(mode, m, n, batch, A, mn, Vin, n, C, E, m, st);
-    };
-    auto applyMM = [&](const double* Lm, const double* Vin, double* C) {  // C = L Vin, L = G or K
-        if (shared) launch_zgemm(0, false, m, m, batch, Lm, m, 0, Vin, m, 0, C, nullptr, m, 0, 1, st);
-        else launch_zgemv_rows(0, m, m, batch, Lm, mm, Vin, m, C, nullptr, m, st);
-    };
-    auto applyAH = [&](const double* gin, double* C, const double* E) {  // C = E + A^H gin
-        if (shared) launch_zgemm(2, false, n, m, batch, w.AH, m, 0, gin, m, 0, C, E, n, 0, 1, st);
-        else launch_zgemv_cols(2, m, n, batch, A, mn, gin, m, C, E, n, st);
-    };
-
-    ZArgs za{};
-    za.n = n;
-    za.m = m;
-    za.tx = tx;
-    za.rx = rx;
-    za.X = w.X;
-    za.N = w.N;
-    za.Z = w.Z;
-    za.Q = w.Q;
-    za.st = w.st;
-    za.optX = w.optX;
-    za.optY = w.optY;
-    za.done_count = w.done;
-    za.np = rank_profile(tx, rx, m, n, cfg->use_rank_one, za.rl, za.fl);
-    za.tol_rel = cfg->tol_rel;
-    za.tol_abs = cfg->tol_abs;
-    za.rho = cfg->rho;
-    za.fixed_iters = cfg->fixed_iters;
-    za.warm = cfg->eig_warm;
-
-    // ---- init (:296-310)
-    ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
-    {
-        ProfScope ps(ACE_K_INIT, st);
-        applyA(0, X0, w.T, nullptr);                             // AX = A*X0
-        launch_init(n, m, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, cfg->mu0, st);
-        za.it = 0;
-        launch_zstep(cfg->variant, true, za, batch, st);         // Z = ArgMinZ(X, N=0, mu=1)
-        applyMM(w.K, w.Y[0], w.KY[0]);                           // K*Y (for A'*Y terms)
-    }
-    ACE_HIP(hipGetLastError());
-
-    int p = 0;
-    const int poll = 8;
-    for (int it = 1; it <= cfg->maxiter; ++it) {
-        { ProfScope ps(ACE_K_PRE, st); launch_pre(n, m, batch, w.Z, w.N, w.Y[p], w.M, w.V, w.S, w.st, st); }
-        { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }          // T = S - A V
-        { ProfScope ps(ACE_K_APPLY_G, st); applyMM(w.G, w.T, w.g); }            // g = G T
-        { ProfScope ps(ACE_K_YSTEP, st); launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[p], w.Y[1 - p], w.st, st); }
-        { ProfScope ps(ACE_K_APPLY_K, st); applyMM(w.K, w.Y[1 - p], w.KY[1 - p]); }  // K Y
-        { ProfScope ps(ACE_K_APPLY_AH, st); applyAH(w.g, w.X, w.V); }           // X = V + A^H g
-        za.it = it;
-        za.Ynew = w.Y[1 - p];
-        za.Yold = w.Y[p];
-        za.KYnew = w.KY[1 - p];
-        za.KYold = w.KY[p];
-        { ProfScope ps(ACE_K_ZSTEP, st); launch_zstep(cfg->variant, false, za, batch, st); }
-        p = 1 - p;
-        if (!cfg->fixed_iters && (it % poll == 0) && it < cfg->maxiter) {
-            int h_done = 0;
-            ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
-            ACE_HIP(hipStreamSynchronize(st));
-            if (h_done >= batch) break;
-        }
-    }
-    ACE_HIP(hipGetLastError());
-    {
-        ProfScope ps(ACE_K_FINAL, st);
-        launch_finalize(n, m, batch, w.optX, w.optY, w.X, w.Y[p], Xo, Yo, iters, status, mu_out, w.st, st);
-    }
-    ACE_HIP(hipGetLastError());
-    return ACE_OK;
+    Carver cv{(char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255)};
+    LinOps L;
+    AdmmState w;
+    linops_carve(cv, cfg->a_shared != 0, batch, m, n, &L);
+    admm_state_carve(cv, batch, m, n, 1, &w);
+    L.A = A;
+    ACE_TRY(linops_setup(L, batch, st));
+    AdmmParams p{};
+    p.variant = cfg->variant;
+    p.r = 1;
+    p.row_mode = 1;
+    p.maxiter = cfg->maxiter;
+    p.fixed_iters = cfg->fixed_iters;
+    p.eig_warm = cfg->eig_warm;
+    p.mu0 = cfg->mu0;
+    p.rho = cfg->rho;
+    p.tol_rel = cfg->tol_rel;
+    p.tol_abs = cfg->tol_abs;
+    p.tx = tx;
+    p.rx = rx;
+    p.use_rank_one = cfg->use_rank_one;
+    p.rank_one = nullptr;
+    return admm_run(L, p, w, batch, B, X0, Xo, Yo, iters, status, mu_out, st);
 }
 
 int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,

@@ -23,7 +23,7 @@ struct RealState {
     // written by the Y-step kernel each iteration
     double obj2, nAX2, nY2, nJM2, dY2;
     double pad0, pad1, pad2;
-    int32_t iters, done, status, pad3;
+    int32_t iters, done, status, objcol;  // objcol: argmin column of the per-column objective
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -76,36 +76,68 @@ void launch_inv_ipk(int m, int count, double* G, long long strideG, hipStream_t 
 // Arguments of the Z-step kernel (ace_zprox.hip).
 struct ZArgs {
     int n, m, tx, rx;
-    const double* X;   // [b][n] c128
-    double* N;         // [b][n]
-    double* Z;         // [b][n]  (in: Z0, out: Z)
+    int r;             // columns per realisation: X, N, Z are [b][r][n], Y, KY [b][r][m]
+    int row_mode;      // scale_by_row: objective over all rows (1) or per column with argmin (0)
+    const double* X;   // [b][r][n] c128
+    double* N;         // [b][r][n]
+    double* Z;         // [b][r][n]  (in: Z0, out: Z)
     double* Q;         // [b][tx*tx] c128 warm-start eigenvectors (may be null)
     RealState* st;
-    double* optX;      // [b][n]
-    double* optY;      // [b][m]
+    double* optX;      // [b][row_mode ? r : 1][n]
+    double* optY;      // [b][row_mode ? r : 1][m]
     const double* Ynew;
     const double* Yold;
     const double* KYnew;
     const double* KYold;
     int* done_count;
-    int np;            // rank-profile length
+    int np;            // rank-profile length (use_rank_one = 0)
     int rl[4];
     double fl[4];
+    const unsigned char* rank_one;  // per-realisation use_rank_one (null: all 0); profile [1], [0.95]
     double tol_rel, tol_abs, rho;
     int it, fixed_iters, warm, ld_state;
 };
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st);
+
+// ArgMinZ rank profile of realisation b (inferLowRankV4_multi.m:437-464; use_rank_one -> :448-450).
+struct ZProfile {
+    int np;
+    int rl[4];
+    double fl[4];
+};
+__device__ __forceinline__ ZProfile z_profile(const ZArgs& a, int b) {
+    ZProfile p;
+    if (a.rank_one && a.rank_one[b]) {
+        p.np = 1;
+        p.rl[0] = 1;
+        p.fl[0] = 0.95;
+        for (int i = 1; i < 4; ++i) { p.rl[i] = 0; p.fl[i] = 0.0; }
+    } else {
+        p.np = a.np;
+        for (int i = 0; i < 4; ++i) { p.rl[i] = a.rl[i]; p.fl[i] = a.fl[i]; }
+    }
+    return p;
+}
 void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st);  // A2only, one wave per realisation
 void launch_pre(int n, int m, int batch, const double* Z, const double* N, const double* Y, const double* M, double* V,
                 double* S, const RealState* rs, hipStream_t st);
 void launch_ystep(int m, int batch, const double* S, const double* g, double* M, const double* B, const double* Yold,
                   double* Ynew, RealState* rs, hipStream_t st);
-void launch_init(int n, int m, int batch, const double* X0, const double* P0, const double* B, double* X, double* Y,
-                 double* M, double* N, RealState* rs, double mu0, hipStream_t st);
-void launch_finalize(int n, int m, int batch, const double* optX, const double* optY, const double* Xc,
-                     const double* Yc, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu,
-                     RealState* rs, hipStream_t st);
+// r-column stage kernels (ace_stage.hip).  State is [b][r][n] / [b][r][m].
+// init: InferADMM :296-310 given P0 = A X0 (row mode: one scale, normalize_rows by row
+// norms; column mode: per-column scale and entrywise normalisation).
+void launch_init_r(int row_mode, int n, int m, int r, int batch, const double* X0, const double* P0,
+                   const double* B, double* X, double* Y, double* M, double* N, RealState* rs, double mu0,
+                   hipStream_t st);
+// ystep at r columns (ArgMinY :511-533 row / column mode, M update, reductions, and
+// in column mode the per-column objective with its first argmin, :352-361).
+void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, const double* g, double* M,
+                    const double* B, const double* Yold, double* Ynew, RealState* rs, hipStream_t st);
+// opt_X / opt_Y (nc columns) or, if the objective never was finite, the current iterate.
+void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
+                       const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters,
+                       uint32_t* status, double* mu, RealState* rs, hipStream_t st);
 void launch_conj_transpose(int rows, int cols, const double* A, double* AH, hipStream_t st);
 void launch_synth_codebook(uint64_t seed, long long first, int count, int m, int n, double* A, hipStream_t st);
 void launch_synth_channels(uint64_t seed, long long first, int count, int m, int tx, int rx, int L, double snr_db,

@@ -1,0 +1,136 @@
+// Host-side helpers shared by the C-ABI translation units (ace_api.cpp, ace_admm.cpp,
+// ace_pipeline.cpp): thread-local error text, HIP error checks, the event-pair kernel
+// timer behind ace_prof_start/stop, and the ArgMinZ rank profile.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "ace_common.hpp"
+
+namespace ace {
+
+inline thread_local std::string g_err;
+
+__attribute__((format(printf, 2, 3))) inline int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define ACE_HIP(call)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess) return fail(ACE_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                         \
+    } while (0)
+
+#define ACE_TRY(call)          \
+    do {                       \
+        int rc_ = (call);      \
+        if (rc_) return rc_;   \
+    } while (0)
+
+// ---- event-pair kernel timing (ace_prof_start / ace_prof_stop)
+struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> ev;   // 2 per record
+    std::vector<int> cls;
+    size_t used = 0;
+};
+inline Prof g_prof;
+
+struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
+    hipStream_t st;
+    int idx = -1;
+    ProfScope(int c, hipStream_t s) : st(s) {
+        if (g_prof.on && g_prof.used < g_prof.cls.size()) {
+            idx = (int)g_prof.used++;
+            g_prof.cls[idx] = c;
+            (void)hipEventRecord(g_prof.ev[2 * idx], st);
+        }
+    }
+    ~ProfScope() {
+        if (idx >= 0) (void)hipEventRecord(g_prof.ev[2 * idx + 1], st);
+    }
+};
+
+// ArgMinZ rank profile for use_rank_one = 0 / 1 (inferLowRankV4_multi.m:437-464).
+inline int rank_profile(int tx, int rx, int m, int n, int use_rank_one, int* rl, double* fl) {
+    const int sz = tx < rx ? tx : rx;
+    const int r0 = (int)std::ceil(std::sqrt((double)sz) * 0.5), r1 = (int)std::ceil(std::sqrt((double)sz) * 0.7);
+    const int r2 = (int)std::ceil(std::sqrt((double)sz));
+    int r3 = (int)std::ceil(std::sqrt((double)sz) * 2.0);
+    if (r3 > sz) r3 = sz;
+    if (use_rank_one) { rl[0] = 1; fl[0] = 0.95; return 1; }
+    if (m >= n * 3) { rl[0] = r3; fl[0] = 0.995; return 1; }
+    if (r1 <= 2) { rl[0] = r2; fl[0] = 0.95; return 1; }
+    if (r0 <= 2) {
+        rl[0] = r1; rl[1] = r2; rl[2] = r3;
+        fl[0] = 0.9; fl[1] = 0.95; fl[2] = 0.995;
+        return 3;
+    }
+    rl[0] = r0; rl[1] = r1; rl[2] = r2; rl[3] = r3;
+    fl[0] = 0.8; fl[1] = 0.9; fl[2] = 0.95; fl[3] = 0.995;
+    return 4;
+}
+
+// Bump allocator over a caller-provided device workspace (256-B aligned chunks);
+// with base == nullptr it only measures.
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <class T = double>
+    T* take(size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~(size_t)255;
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+// ---- one ADMM solve (InferADMM, inferLowRankV4_multi.m:281-386) over a batch -------
+// The sensing operator of the solve.  Shared regime: one A (m x n) for the batch with
+// its A^H; private regime: A_b per realisation (r = 1 only).  K = A A^H and
+// G = (I + K)^{-1} ([1 | batch][m][m]) are built by admm_setup.
+struct LinOps {
+    bool shared;
+    int m, n;
+    const double* A;
+    double* AH;
+    double* K;
+    double* G;
+};
+size_t linops_bytes(bool shared, int batch, int m, int n);
+void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L);
+int linops_setup(LinOps& L, int batch, hipStream_t st);  // K, G, A^H from L.A
+
+struct AdmmParams {
+    int variant, r, row_mode, maxiter, fixed_iters, eig_warm;
+    double mu0, rho, tol_rel, tol_abs;
+    int tx, rx;
+    int use_rank_one;                  // batch-wide flag (ignored where rank_one is given)
+    const unsigned char* rank_one;     // per-realisation use_rank_one (device, may be null)
+};
+// Per-iteration state of a batch of `batch` realisations with r columns each.
+struct AdmmState {
+    double *X, *Z, *N, *V, *optX, *Q;
+    double *Y[2], *KY[2], *M, *S, *T, *g, *optY;
+    RealState* st;
+    int* done;
+};
+void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s);
+// Runs init (:296-310), the iterations (:318-383) and returns the best-objective iterate
+// (:384-385) in Xo [batch][row_mode ? r : 1][n], Yo [..][m].  iters/status/mu optional.
+int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& s, int batch, const double* B,
+             const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu,
+             hipStream_t st);
+
+}  // namespace ace

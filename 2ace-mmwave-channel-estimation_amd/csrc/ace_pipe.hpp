@@ -1,0 +1,49 @@
+// Launchers of the recovery-pipeline kernels (ace_stage.hip, ace_spectral.hip) used by
+// ace_pipeline.cpp.  Shapes follow main/src/my_recovery_algorithms/ADMM_v2/
+// inferLowRankV4_multi.m: m_t train rows, m_te = m - m_t test rows, r columns.
+#pragma once
+#include "ace_common.hpp"
+
+namespace ace {
+
+// A_norm = ||A||_F / sqrt(m) with the tol_abs guard (:27-30), one shared A.
+void launch_anorm(int m, int n, const double* A, double tol_abs, double* anorm, hipStream_t st);
+// dst[i][:] = src[rows[i]][:] / anorm[0]  (complex rows of length n)
+void launch_gather_rows(int nrows, int n, const double* src, const int* rows, const double* anorm, double* dst,
+                        hipStream_t st);
+// B_norm per realisation (:32-35) and Bn = B / B_norm
+void launch_bnorm(int m, int batch, const double* B, double tol_abs, double* bnorm, double* Bn, hipStream_t st);
+// dst[b][i] = src[b][rows[i]]  (f64)
+void launch_gather_b(int m, int nrows, int batch, const double* src, const int* rows, double* dst, hipStream_t st);
+// per-realisation blocks of `len` doubles: dst[k] = src[idx[k]] (gather) / dst[idx[k]] = src[k] (scatter)
+void launch_move_rows(int count, long long len, const double* src, double* dst, const int* idx, bool scatter,
+                      hipStream_t st);
+// X[b] (n x r) <- X[b] V, V = eigenvectors of X^H X in ascending order (:263-264)
+void launch_gram_rotate(int n, int r, int batch, double* X, int* status, hipStream_t st);
+// quality = 1 - ||abs(A_te x) - B_te|| / ||B_te||  (:68)
+void launch_quality(int n, int mte, int batch, const double* Ate, const double* X, const double* Bte, double* q,
+                    hipStream_t st);
+// best of restarts (:79-83): X [b][n], Y [b][m] (c128)
+void launch_keep_best(int n, int m, int batch, bool first, const double* q, double* qmax, const double* X,
+                      const double* Y, double* Xmax, double* Ymax, hipStream_t st);
+// rollback (:89-98) and rescale (:106-107)
+void launch_finish(int n, int m, int mt, int batch, const double* qlast, const double* Xr, const double* Yr,
+                   const double* Xmax, const double* Ymax, const double* anorm, const double* bnorm, double* Xo,
+                   double* Yo, uint32_t* status, hipStream_t st);
+
+// dst[(idx ? idx[k] : k) * ld + col] = src[k] (or_mask 0) or |= src[k] & or_mask, k < count
+void launch_put_col(int count, const int* src, const int* idx, int* dst, int ld, int col, unsigned or_mask,
+                    hipStream_t st);
+void launch_fill(long long count, double v, double* dst, hipStream_t st);
+
+// ---- SpectralInitialize (:561-574) through the m_t x m_t dual Gram (ace_spectral.hip)
+// C_b = D_b K D_b with K = A_t A_t^H and D_b = diag(B_t[b][i] / ||a_i||) has the nonzero
+// spectrum of As^H As (As = D_b A_t); for an eigenpair (lam, u) of C_b, As^H u is the
+// eigenvector of As^H As for lam scaled by sqrt(lam) -- exactly one column of
+// X = V(:, 1:r) * diag(sqrt(s(1:r))).  The kernels leave W[b][k] = D_b u_k (k-th largest
+// eigenvalue first) and X = A_t^H W is one GEMM over batch*r vectors.
+size_t spectral_scratch_bytes(int mt, int batch, int r);
+int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
+                    int* status, hipStream_t st);
+
+}  // namespace ace

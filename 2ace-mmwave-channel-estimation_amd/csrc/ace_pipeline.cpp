@@ -1,0 +1,359 @@
+// Batched recovery pipeline: inferLowRankV4_multi (main/src/my_recovery_algorithms/
+// ADMM_v2/inferLowRankV4_multi.m:5-109), inferLowRankV4 (Numerical_Simulation, one
+// restart) and inferLowRank_Nuclear (one restart, nuclear Z-prox), every stage on the GPU.
+//
+//   :27-38   A_norm = ||A||_F/sqrt(m), B_norm = ||B|| per realisation      anorm/bnorm
+//   :42-53   per restart: train rows (caller's partition), test = setdiff   gather_rows/_b
+//   :58      SpectralInitialize on (A_t, B_t)                               ace_spectral.hip + GEMM
+//   :65      inferLowRankImpl (U = inv(A_t'A_t+I) as Woodbury K_t, G_t;
+//            r-column row-scaled ADMM :258, X = X eig(X'X) :263-264,
+//            per-column ADMM :270, best column)                             admm_run x2, gram_rotate
+//   :68      quality on the test rows                                      quality
+//   :73-77   rank-one retry for realisations with quality < 0.6: the retry
+//            set is gathered into a contiguous sub-batch and scattered back  move_rows
+//   :79-83   best of restarts (A2only; the nuclear driver keeps the last)   keep_best
+//   :89-101  refinement on the full A at r = 1 with the last restart's
+//            use_rank_one (per realisation)                                 admm_run (fast r = 1 path)
+//   :93-107  rollback when the last quality > 0.6 and the similarity < 0.6; rescale   finish
+#include <algorithm>
+#include <cstring>
+
+#include "ace_host.hpp"
+#include "ace_pipe.hpp"
+
+using namespace ace;
+
+namespace {
+
+// status bits a stage contributes to the pipeline status (its CONVERGED bit does not)
+constexpr unsigned kStageBits = ACE_ST_NO_OPT | ACE_ST_EIG_NOCONV;
+
+struct PipeDims {
+    int batch, m, n, tx, rx, r, mt, mte, restarts;
+};
+
+struct PipeWs {
+    double *anorm, *bnorm, *Bn, *Bt, *Bte, *Bt_s, *Bte_s;
+    double *An, *At, *Ate;
+    LinOps Lt, Lf;
+    double *W, *spec, *Xs, *Xs_s;
+    double *X1, *Y1;                 // stage-1 output (r columns), reused by both stages' chains
+    double *X2, *Y2, *X2_s, *Y2_s;   // impl outputs (best column)
+    double *q, *q_s, *qmax, *qlast, *Xmax, *Ymax, *Xr, *Yr;
+    int *iters, *stat, *idx_rows, *idx_sub, *stage_dev, *status_dev;
+    unsigned char* rank_one;
+    AdmmState sr, s1;                // r-column state (m_t rows), refinement state (r = 1, m rows)
+};
+
+void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
+    const size_t cz = 16, B = (size_t)d.batch;
+    w->anorm = cv.take(256);
+    w->bnorm = cv.take(8 * B);
+    w->Bn = cv.take(8 * B * d.m);
+    w->Bt = cv.take(8 * B * d.mt);
+    w->Bte = cv.take(8 * B * std::max(d.mte, 1));
+    w->Bt_s = cv.take(8 * B * d.mt);
+    w->Bte_s = cv.take(8 * B * std::max(d.mte, 1));
+    w->An = cv.take(cz * d.m * d.n);
+    w->At = cv.take(cz * d.mt * d.n);
+    w->Ate = cv.take(cz * std::max(d.mte, 1) * d.n);
+    linops_carve(cv, true, d.batch, d.mt, d.n, &w->Lt);
+    linops_carve(cv, true, d.batch, d.m, d.n, &w->Lf);
+    w->W = cv.take(cz * B * d.r * d.mt);
+    w->spec = cv.take(spectral_scratch_bytes(d.mt, d.batch, d.r));
+    w->Xs = cv.take(cz * B * d.r * d.n);
+    w->Xs_s = cv.take(cz * B * d.r * d.n);
+    w->X1 = cv.take(cz * B * d.r * d.n);
+    w->Y1 = cv.take(cz * B * d.r * d.mt);
+    w->X2 = cv.take(cz * B * d.n);
+    w->Y2 = cv.take(cz * B * d.mt);
+    w->X2_s = cv.take(cz * B * d.n);
+    w->Y2_s = cv.take(cz * B * d.mt);
+    w->q = cv.take(8 * B);
+    w->q_s = cv.take(8 * B);
+    w->qmax = cv.take(8 * B);
+    w->qlast = cv.take(8 * B);
+    w->Xmax = cv.take(cz * B * d.n);
+    w->Ymax = cv.take(cz * B * d.mt);
+    w->Xr = cv.take(cz * B * d.n);
+    w->Yr = cv.take(cz * B * d.m);
+    w->iters = cv.take<int>(4 * B);
+    w->stat = cv.take<int>(4 * B);
+    w->idx_rows = cv.take<int>(4 * (size_t)d.m);
+    w->idx_sub = cv.take<int>(4 * B);
+    w->stage_dev = cv.take<int>(4 * B * (4 * d.restarts + 1));
+    w->status_dev = cv.take<int>(4 * B);
+    w->rank_one = cv.take<unsigned char>(B);
+    admm_state_carve(cv, d.batch, d.mt, d.n, d.r, &w->sr);
+    admm_state_carve(cv, d.batch, d.m, d.n, 1, &w->s1);
+}
+
+int validate_dims(const ace_pipeline_cfg* c, int batch, int m, int n, PipeDims* d) {
+    if (!c) return fail(ACE_ERR_ARG, "cfg is NULL");
+    if (batch < 1 || m < 1 || n < 1) return fail(ACE_ERR_ARG, "batch/m/n must be >= 1 (got %d/%d/%d)", batch, m, n);
+    if (c->variant != ACE_VARIANT_A2ONLY && c->variant != ACE_VARIANT_NUCLEAR)
+        return fail(ACE_ERR_ARG, "unknown variant %d", c->variant);
+    if (c->restarts < 1 || c->restarts > 16) return fail(ACE_ERR_ARG, "restarts must be in [1,16]");
+    if (c->maxiter < 1) return fail(ACE_ERR_ARG, "maxiter must be >= 1");
+    if (!(c->mu0 > 0) || !(c->rho > 0)) return fail(ACE_ERR_ARG, "mu0 and rho must be > 0");
+    if (!(c->cc_frac > 0) || !(c->cc_frac <= 1)) return fail(ACE_ERR_ARG, "cc_frac must be in (0, 1]");
+    const int r = std::min(std::min(c->r, m), n);                     // :19
+    const int mt = (int)std::floor((double)m * c->cc_frac);           // :48
+    if (r < 1 || r > 32) return fail(ACE_ERR_UNSUPPORTED, "r = min(r, m, n) must be in [1, 32] (got %d)", r);
+    if (mt < r)
+        return fail(ACE_ERR_UNSUPPORTED, "floor(m*cc_frac) = %d train rows < r = %d: the spectral initialisation "
+                    "would take eigenvectors of the null space (ill-posed, not supported)", mt, r);
+    if (mt > 1600) return fail(ACE_ERR_UNSUPPORTED, "train rows %d > 1600 (spectral tridiagonalisation LDS limit)", mt);
+    if (n > 4096) return fail(ACE_ERR_UNSUPPORTED, "n must be <= 4096 (got %d)", n);
+    *d = PipeDims{batch, m, n, 0, 0, r, mt, m - mt, c->restarts};
+    return ACE_OK;
+}
+
+int validate(const ace_pipeline_cfg* c, int batch, int m, int n, int tx, int rx, PipeDims* d) {
+    ACE_TRY(validate_dims(c, batch, m, n, d));
+    if (tx * rx != n) return fail(ACE_ERR_ARG, "n (%d) != tx*rx (%d*%d)", n, tx, rx);
+    if (tx < 2 || tx > 32 || (tx & 1) || rx > 32)
+        return fail(ACE_ERR_UNSUPPORTED, "pipeline needs even tx in [2,32] and rx <= 32 (got %d, %d)", tx, rx);
+    d->tx = tx;
+    d->rx = rx;
+    return ACE_OK;
+}
+
+// inferLowRankImpl (:111-271) for `nb` realisations: Xs [nb][r][n], Bt [nb][mt] ->
+// X2 [nb][n], Y2 [nb][mt] (best column of the per-column stage); iteration counts of the
+// two stages into stage_dev columns col, col + 1 (rows idx[k] or k).
+int run_impl(const PipeDims& d, PipeWs& w, const AdmmParams& base, int nb, const double* Xs, const double* Bt,
+             double* X2, double* Y2, const int* idx, int col, hipStream_t st) {
+    const int ld = 4 * d.restarts + 1;
+    AdmmParams p = base;
+    p.r = d.r;
+    p.row_mode = 1;                                               // :258 scale_by_row = true
+    ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, Xs, w.X1, w.Y1, w.iters, (uint32_t*)w.stat, nullptr, st));
+    launch_put_col(nb, w.iters, idx, w.stage_dev, ld, col, 0, st);
+    launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
+    launch_gram_rotate(d.n, d.r, nb, w.X1, nullptr, st);         // :263-264
+    p.row_mode = 0;                                               // :270 scale_by_row = false
+    ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, w.X1, X2, Y2, w.iters, (uint32_t*)w.stat, nullptr, st));
+    launch_put_col(nb, w.iters, idx, w.stage_dev, ld, col + 1, 0, st);
+    launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void ace_pipeline_cfg_default(ace_pipeline_cfg* c, int variant) {
+    std::memset(c, 0, sizeof *c);
+    c->variant = variant;
+    c->restarts = variant == ACE_VARIANT_NUCLEAR ? 1 : 3;
+    c->r = 20;
+    c->maxiter = 500;
+    c->eig_warm = 1;
+    c->mu0 = 1e-3;
+    c->rho = 1.03;
+    c->cc_frac = 0.95;
+    c->tol_rel = 1e-4;
+    c->tol_abs = 1e-8;
+}
+
+size_t ace_pipeline_workspace_size(const ace_pipeline_cfg* cfg, int batch, int m, int n) {
+    PipeDims d;
+    const std::string keep = g_err;
+    if (validate_dims(cfg, batch, m, n, &d)) {
+        g_err = keep;
+        return 0;
+    }
+    Carver cv{nullptr};
+    PipeWs w;
+    pipe_carve(cv, d, &w);
+    return cv.off + 256;
+}
+
+int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
+                             const double* B, const int32_t* train_idx, double* Xo, double* Yo, double* quality,
+                             int32_t* stage_iters, uint32_t* status, void* workspace, size_t workspace_bytes,
+                             void* stream) {
+    g_err.clear();
+    PipeDims d;
+    ACE_TRY(validate(cfg, batch, m, n, tx, rx, &d));
+    if (!A || !B || !train_idx || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
+    // partitions (host): train rows in sampled order, test rows = sorted complement (:48-49)
+    std::vector<std::vector<int>> tr(d.restarts), te(d.restarts);
+    for (int i = 0; i < d.restarts; ++i) {
+        std::vector<char> seen(m, 0);
+        for (int k = 0; k < d.mt; ++k) {
+            const int v = train_idx[(size_t)i * d.mt + k];
+            if (v < 0 || v >= m || seen[v])
+                return fail(ACE_ERR_ARG, "train_idx[%d][%d] = %d: out of range or repeated", i, k, v);
+            seen[v] = 1;
+            tr[i].push_back(v);
+        }
+        for (int v = 0; v < m; ++v)
+            if (!seen[v]) te[i].push_back(v);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    Carver sz{nullptr};
+    PipeWs w;
+    pipe_carve(sz, d, &w);
+    if (sz.off + 256 > workspace_bytes)
+        return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", sz.off + 256, workspace_bytes);
+    Carver cv{(char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255)};
+    pipe_carve(cv, d, &w);
+    const int ld = 4 * d.restarts + 1;
+
+    AdmmParams base{};
+    base.variant = cfg->variant;
+    base.maxiter = cfg->maxiter;
+    base.fixed_iters = 0;
+    base.eig_warm = cfg->eig_warm;
+    base.mu0 = cfg->mu0;
+    base.rho = cfg->rho;
+    base.tol_rel = cfg->tol_rel;
+    base.tol_abs = cfg->tol_abs;
+    base.tx = tx;
+    base.rx = rx;
+
+    // ---- :27-38 normalisation
+    std::vector<int> iota(m);
+    for (int i = 0; i < m; ++i) iota[i] = i;
+    launch_anorm(m, n, A, cfg->tol_abs, w.anorm, st);
+    ACE_HIP(hipMemcpyAsync(w.idx_rows, iota.data(), 4 * (size_t)m, hipMemcpyHostToDevice, st));
+    launch_gather_rows(m, n, A, w.idx_rows, w.anorm, w.An, st);
+    launch_bnorm(m, batch, B, cfg->tol_abs, w.bnorm, w.Bn, st);
+    launch_fill(batch, -1.0, w.qmax, st);                                 // max_quality = -1 (:40)
+    ACE_HIP(hipMemsetAsync(w.stage_dev, 0, 4 * (size_t)batch * ld, st));
+    ACE_HIP(hipMemsetAsync(w.status_dev, 0, 4 * (size_t)batch, st));
+    std::vector<double> hq(batch);
+    std::vector<int> fails;
+    std::vector<unsigned char> ro(batch);
+
+    for (int i = 0; i < d.restarts; ++i) {
+        // ---- :47-53 partition
+        std::vector<int> rows(tr[i]);
+        rows.insert(rows.end(), te[i].begin(), te[i].end());
+        ACE_HIP(hipMemcpyAsync(w.idx_rows, rows.data(), 4 * (size_t)m, hipMemcpyHostToDevice, st));
+        launch_gather_rows(d.mt, n, A, w.idx_rows, w.anorm, w.At, st);
+        launch_gather_rows(d.mte, n, A, w.idx_rows + d.mt, w.anorm, w.Ate, st);
+        launch_gather_b(m, d.mt, batch, w.Bn, w.idx_rows, w.Bt, st);
+        launch_gather_b(m, d.mte, batch, w.Bn, w.idx_rows + d.mt, w.Bte, st);
+        w.Lt.A = w.At;
+        ACE_TRY(linops_setup(w.Lt, batch, st));                          // K_t, G_t (U, :242), A_t^H
+        // ---- :58 SpectralInitialize: W = D u_k, X = A_t^H W
+        {
+            ProfScope ps(ACE_K_SETUP, st);
+            if (launch_spectral(d.mt, d.r, batch, w.Lt.K, w.Bt, w.spec, w.W, w.status_dev, st))
+                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
+            launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
+        }
+        ACE_HIP(hipGetLastError());
+        // ---- :65-68 impl (use_rank_one = false) and test quality
+        AdmmParams p = base;
+        p.use_rank_one = 0;
+        p.rank_one = nullptr;
+        ACE_TRY(run_impl(d, w, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
+        launch_quality(n, d.mte, batch, w.Ate, w.X2, w.Bte, w.q, st);
+        // ---- :73-77 rank-one retry on the realisations with quality < 0.6
+        ACE_HIP(hipMemcpyAsync(hq.data(), w.q, 8 * (size_t)batch, hipMemcpyDeviceToHost, st));
+        ACE_HIP(hipStreamSynchronize(st));
+        fails.clear();
+        for (int b = 0; b < batch; ++b) {
+            ro[b] = hq[b] < 0.6;
+            if (ro[b]) fails.push_back(b);
+        }
+        ACE_HIP(hipMemcpyAsync(w.rank_one, ro.data(), batch, hipMemcpyHostToDevice, st));
+        const int nf = (int)fails.size();
+        if (nf > 0) {
+            ACE_HIP(hipMemcpyAsync(w.idx_sub, fails.data(), 4 * (size_t)nf, hipMemcpyHostToDevice, st));
+            launch_move_rows(nf, 2LL * d.r * n, w.Xs, w.Xs_s, w.idx_sub, false, st);
+            launch_move_rows(nf, d.mt, w.Bt, w.Bt_s, w.idx_sub, false, st);
+            launch_move_rows(nf, std::max(d.mte, 1), w.Bte, w.Bte_s, w.idx_sub, false, st);
+            p.use_rank_one = 1;
+            ACE_TRY(run_impl(d, w, p, nf, w.Xs_s, w.Bt_s, w.X2_s, w.Y2_s, w.idx_sub, 4 * i + 2, st));
+            launch_quality(n, d.mte, nf, w.Ate, w.X2_s, w.Bte_s, w.q_s, st);
+            launch_move_rows(nf, 2LL * n, w.X2_s, w.X2, w.idx_sub, true, st);
+            launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
+            launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
+        }
+        // ---- :79-83 best of restarts (A2only); the nuclear pipeline keeps the last X
+        if (cfg->variant == ACE_VARIANT_A2ONLY) {
+            launch_keep_best(n, d.mt, batch, i == 0, w.q, w.qmax, w.X2, w.Y2, w.Xmax, w.Ymax, st);
+        } else {
+            ACE_HIP(hipMemcpyAsync(w.Xmax, w.X2, 16 * (size_t)batch * n, hipMemcpyDeviceToDevice, st));
+            ACE_HIP(hipMemcpyAsync(w.Ymax, w.Y2, 16 * (size_t)batch * d.mt, hipMemcpyDeviceToDevice, st));
+        }
+        ACE_HIP(hipMemcpyAsync(w.qlast, w.q, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+        ACE_HIP(hipGetLastError());
+    }
+
+    // ---- :89-101 refinement on the full A, r = 1, the last restart's use_rank_one
+    w.Lf.A = w.An;
+    ACE_TRY(linops_setup(w.Lf, batch, st));
+    AdmmParams p = base;
+    p.r = 1;
+    p.row_mode = 1;
+    p.rank_one = w.rank_one;
+    ACE_TRY(admm_run(w.Lf, p, w.s1, batch, w.Bn, w.Xmax, w.Xr, w.Yr, w.iters, (uint32_t*)w.stat, nullptr, st));
+    launch_put_col(batch, w.iters, nullptr, w.stage_dev, ld, ld - 1, 0, st);
+    launch_put_col(batch, w.stat, nullptr, w.status_dev, 1, 0, ~0u, st);
+    // ---- :93-107 rollback and rescale
+    launch_finish(n, m, d.mt, batch, w.qlast, w.Xr, w.Yr, w.Xmax, w.Ymax, w.anorm, w.bnorm, Xo, Yo,
+                  (uint32_t*)w.status_dev, st);
+    if (quality) ACE_HIP(hipMemcpyAsync(quality, w.qlast, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+    if (stage_iters)
+        ACE_HIP(hipMemcpyAsync(stage_iters, w.stage_dev, 4 * (size_t)batch * ld, hipMemcpyDeviceToDevice, st));
+    if (status) ACE_HIP(hipMemcpyAsync(status, w.status_dev, 4 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+int ace_pipeline_solve_host(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
+                            const double* B, const int32_t* train_idx, double* X, double* Y, double* quality,
+                            int32_t* stage_iters, uint32_t* status) {
+    g_err.clear();
+    PipeDims d;
+    ACE_TRY(validate(cfg, batch, m, n, tx, rx, &d));
+    const int ld = 4 * d.restarts + 1;
+    const size_t nA = (size_t)m * n * 16, nB = (size_t)batch * m * 8, nX = (size_t)batch * n * 16,
+                 nY = (size_t)batch * m * 16, ws = ace_pipeline_workspace_size(cfg, batch, m, n);
+    std::vector<void*> bufs;
+    auto cleanup = [&]() {
+        for (void* q : bufs) (void)hipFree(q);
+        bufs.clear();
+    };
+    auto dalloc = [&](size_t bytes, void** q) -> hipError_t {
+        hipError_t e = hipMalloc(q, bytes);
+        if (e == hipSuccess) bufs.push_back(*q);
+        return e;
+    };
+    void *dA, *dB, *dX, *dY, *dQ, *dI, *dS, *dW;
+    hipError_t e;
+    if ((e = dalloc(nA, &dA)) || (e = dalloc(nB, &dB)) || (e = dalloc(nX, &dX)) || (e = dalloc(nY, &dY)) ||
+        (e = dalloc(8 * (size_t)batch, &dQ)) || (e = dalloc(4 * (size_t)batch * ld, &dI)) ||
+        (e = dalloc(4 * (size_t)batch, &dS)) || (e = dalloc(ws, &dW))) {
+        cleanup();
+        return fail(ACE_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
+    }
+    int rc = ACE_OK;
+    if ((e = hipMemcpy(dA, A, nA, hipMemcpyHostToDevice)) || (e = hipMemcpy(dB, B, nB, hipMemcpyHostToDevice))) {
+        cleanup();
+        return fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
+    }
+    rc = ace_pipeline_solve_batch(cfg, batch, m, n, tx, rx, (const double*)dA, (const double*)dB, train_idx,
+                                  (double*)dX, (double*)dY, (double*)dQ, (int32_t*)dI, (uint32_t*)dS, dW, ws, nullptr);
+    if (rc == ACE_OK) {
+        if ((e = hipDeviceSynchronize()) || (e = hipMemcpy(X, dX, nX, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(Y, dY, nY, hipMemcpyDeviceToHost)) ||
+            (quality && (e = hipMemcpy(quality, dQ, 8 * (size_t)batch, hipMemcpyDeviceToHost))) ||
+            (stage_iters && (e = hipMemcpy(stage_iters, dI, 4 * (size_t)batch * ld, hipMemcpyDeviceToHost))) ||
+            (status && (e = hipMemcpy(status, dS, 4 * (size_t)batch, hipMemcpyDeviceToHost))))
+            rc = fail(ACE_ERR_HIP, "pipeline: %s", hipGetErrorString(e));
+    }
+    const std::string keep = g_err;
+    cleanup();
+    g_err = keep;
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,384 @@
+// SpectralInitialize (main/src/my_recovery_algorithms/ADMM_v2/inferLowRankV4_multi.m:561-574)
+// for a batch of realisations sharing one train matrix A_t (m_t x n).
+//
+// The reference forms As^H As (n x n, As = rows of A_t scaled by B_i/||a_i||), calls eig
+// and keeps the r largest eigenpairs as X = V diag(sqrt(s)).  Its nonzero spectrum is
+// that of the m_t x m_t dual Gram C = D K D (K = A_t A_t^H, shared by the batch;
+// D = diag(B_i/||a_i||), per realisation), and As^H u = sqrt(lam) v for an eigenpair
+// (lam, u) of C.  So per realisation we need the top-r eigenpairs of a dense m_t x m_t
+// Hermitian matrix (243 x 243 at the 32-antenna configuration):
+//
+//   hetrd_kernel     one work-group per realisation: build C, reduce it to real
+//                    symmetric tridiagonal form by Householder reflectors (LAPACK zhetd2,
+//                    lower, with full Hermitian storage in global memory so that the
+//                    Hermitian matrix-vector product reads rows coalesced); reflector k is
+//                    left in row k of C
+//   trieig_kernel    one wave per realisation, lane k <-> k-th largest eigenvalue:
+//                    Sturm-count bisection to full precision, then inverse iteration on
+//                    the tridiagonal (partial-pivoting LU as LAPACK dgttrf/dgttrs, three
+//                    solves) and Gram-Schmidt inside eigenvalue clusters (relative
+//                    separation < 1e-3, as dstein)
+//   backxf_kernel    one work-group per realisation: u_k = H_0 H_1 ... H_{m_t-2} z_k,
+//                    W_k = D u_k
+//
+// X = A_t^H W is then one MFMA GEMM over batch*r vectors (ace_pipeline.cpp).
+// Realisations are processed in chunks so the C matrices of a chunk stay in the L2/MALL.
+#include "ace_common.hpp"
+#include "ace_pipe.hpp"
+
+namespace ace {
+
+namespace {
+constexpr int SPEC_CHUNK = 256;   // realisations per launch (C = 0.9 MiB each at m_t = 243)
+constexpr int TRI_LANES = 64;
+
+// per-realisation scratch layout (units: doubles)
+struct SpecLayout {
+    long long C, dv, dd, ee, tau, lu, z, lam, stride;
+    SpecLayout(int mt, int r) {
+        long long o = 0;
+        auto take = [&](long long nd) { long long p = o; o += (nd + 31) & ~31LL; return p; };
+        C = take(2LL * mt * mt);
+        dv = take(mt);
+        dd = take(mt);
+        ee = take(mt);
+        tau = take(2LL * mt);
+        lu = take(6LL * mt * TRI_LANES);   // dl, d, du, du2, ipiv, y  (lane-interleaved)
+        z = take((long long)r * mt);
+        lam = take(r);
+        stride = o;
+    }
+};
+
+__global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
+                                                    SpecLayout lay) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    extern __shared__ double smem[];
+    d2* v = reinterpret_cast<d2*>(smem);   // reflector / x (mt)
+    d2* w = v + mt;                        // p, w (mt)
+    double* dvs = reinterpret_cast<double*>(w + mt);
+    __shared__ double red[16 * 2];
+    __shared__ d2 s_tau, s_scal;
+    double* base = scratch + b * lay.stride;
+    d2* C = reinterpret_cast<d2*>(base + lay.C);
+    const d2* K = reinterpret_cast<const d2*>(Kp);
+    double* dd = base + lay.dd;
+    double* ee = base + lay.ee;
+    d2* taus = reinterpret_cast<d2*>(base + lay.tau);
+
+    // D = diag(B_i / ||a_i||), ||a_i||^2 = K_ii  (SpectralInitialize :563-567; zero rows stay zero)
+    for (int i = t; i < mt; i += 256) {
+        const double kii = K[(long long)i * mt + i].x;
+        const double d = kii > 0.0 ? Bt[(long long)b * mt + i] / sqrt(kii) : 0.0;
+        dvs[i] = d;
+        base[lay.dv + i] = d;
+    }
+    __syncthreads();
+    // C = D (K + K^H)/2 D, exactly Hermitian (real diagonal)
+    for (long long e = t; e < (long long)mt * mt; e += 256) {
+        const int i = (int)(e / mt), j = (int)(e % mt);
+        const d2 kij = K[e], kji = K[(long long)j * mt + i];
+        const double s = dvs[i] * dvs[j];
+        C[e] = i == j ? make_double2(s * kij.x, 0.0) : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
+    }
+    __syncthreads();
+
+    for (int k = 0; k + 1 < mt; ++k) {
+        const int L = mt - k - 1;
+        const long long r0 = (long long)(k + 1) * mt + (k + 1);   // C22 origin
+        // x = C(k+1:m, k) = conj(C(k, k+1:m))
+        double s1[1] = {0.0};
+        for (int i = t; i < L; i += 256) {
+            const d2 c = C[(long long)k * mt + k + 1 + i];
+            v[i] = make_double2(c.x, -c.y);
+            if (i > 0) s1[0] += cabs2(c);
+        }
+        block_sum<1>(s1, red);
+        if (t == 0) {  // zlarfg
+            const d2 alpha = v[0];
+            const double xn2 = s1[0];
+            d2 tau = make_double2(0.0, 0.0), scal = make_double2(0.0, 0.0);
+            double beta = alpha.x;
+            if (!(xn2 == 0.0 && alpha.y == 0.0)) {
+                beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn2), alpha.x);
+                tau = make_double2((beta - alpha.x) / beta, -alpha.y / beta);
+                const d2 den = make_double2(alpha.x - beta, alpha.y);      // scal = 1 / (alpha - beta)
+                const double dn = 1.0 / cabs2(den);
+                scal = make_double2(den.x * dn, -den.y * dn);
+            }
+            s_tau = tau;
+            s_scal = scal;
+            ee[k] = beta;
+            dd[k] = C[(long long)k * mt + k].x;
+            taus[k] = tau;
+        }
+        __syncthreads();
+        const d2 tau = s_tau;
+        if (tau.x == 0.0 && tau.y == 0.0) continue;  // H = I (uniform branch)
+        const d2 scal = s_scal;
+        for (int i = t; i < L; i += 256) {
+            const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
+            v[i] = vi;
+            C[(long long)k * mt + k + 1 + i] = vi;  // reflector k kept in row k (for the back transform)
+        }
+        __syncthreads();
+        // p = tau C22 v: p_i = tau sum_j conj(C22[j][i]) v_j (Hermitian; column reads are row-coalesced)
+        for (int i = t; i < L; i += 256) {
+            double ar = 0.0, ai = 0.0;
+            const d2* col = C + r0 + i;
+            int j = 0;
+            for (; j + 4 <= L; j += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const d2 c = col[(long long)(j + u) * mt], vj = v[j + u];
+                    ar += c.x * vj.x + c.y * vj.y;
+                    ai += c.x * vj.y - c.y * vj.x;
+                }
+            }
+            for (; j < L; ++j) {
+                const d2 c = col[(long long)j * mt], vj = v[j];
+                ar += c.x * vj.x + c.y * vj.y;
+                ai += c.x * vj.y - c.y * vj.x;
+            }
+            w[i] = cmul(tau, make_double2(ar, ai));
+        }
+        __syncthreads();
+        double s2[2] = {0.0, 0.0};  // p^H v
+        for (int i = t; i < L; i += 256) {
+            const d2 q = cmulc(w[i], v[i]);
+            s2[0] += q.x;
+            s2[1] += q.y;
+        }
+        block_sum<2>(s2, red);
+        const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
+        for (int i = t; i < L; i += 256) w[i] = cadd(w[i], cmul(alpha2, v[i]));
+        __syncthreads();
+        // C22 -= v w^H + w v^H  (thread per column j, rows i: coalesced row segments)
+        for (int j = t; j < L; j += 256) {
+            const d2 vj = v[j], wj = w[j];
+            const d2 cvj = make_double2(vj.x, -vj.y), cwj = make_double2(wj.x, -wj.y);
+            d2* col = C + r0 + j;
+            for (int i = 0; i < L; ++i) {
+                d2 c = col[(long long)i * mt];
+                c = csub(c, cadd(cmul(v[i], cwj), cmul(w[i], cvj)));
+                col[(long long)i * mt] = c;
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        dd[mt - 1] = C[(long long)(mt - 1) * mt + mt - 1].x;
+        ee[mt - 1] = 0.0;
+    }
+}
+
+// Sturm count: number of eigenvalues of the tridiagonal (d, e) below x.
+__device__ __forceinline__ int sturm_count(const double* d, const double* e, int n, double x, double pivmin) {
+    int cnt = 0;
+    double q = d[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < n; ++i) {
+        q = d[i] - x - e[i - 1] * e[i - 1] / q;
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(TRI_LANES) void trieig_kernel(int mt, int r, double* scratch, SpecLayout lay,
+                                                           int* status, int status_off) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    extern __shared__ double smem[];
+    double* d = smem;
+    double* e = smem + mt;
+    double* base = scratch + b * lay.stride;
+    for (int i = lane; i < mt; i += TRI_LANES) {
+        d[i] = base[lay.dd + i];
+        e[i] = base[lay.ee + i];
+    }
+    __syncthreads();
+    // Gershgorin interval and pivmin (LAPACK dstebz)
+    double gl = INFINITY, gu = -INFINITY, emax = 0.0;
+    for (int i = lane; i < mt; i += TRI_LANES) {
+        const double a = i > 0 ? fabs(e[i - 1]) : 0.0, c = i + 1 < mt ? fabs(e[i]) : 0.0;
+        gl = fmin(gl, d[i] - a - c);
+        gu = fmax(gu, d[i] + a + c);
+        if (i + 1 < mt) emax = fmax(emax, e[i] * e[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        gl = fmin(gl, __shfl_xor(gl, o, 64));
+        gu = fmax(gu, __shfl_xor(gu, o, 64));
+        emax = fmax(emax, __shfl_xor(emax, o, 64));
+    }
+    const double eps = 2.220446049250313e-16;
+    const double tn = fmax(fabs(gl), fabs(gu));
+    const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);
+    gl -= 2.0 * tn * eps * mt;
+    gu += 2.0 * tn * eps * mt;
+
+    double lam = 0.0;
+    if (lane < r) {  // bisection for the (mt-1-lane)-th ascending eigenvalue
+        const int j = mt - 1 - lane;
+        double lo = gl, hi = gu;
+        for (int it = 0; it < 200; ++it) {
+            if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+            const double mid = 0.5 * (lo + hi);
+            if (sturm_count(d, e, mt, mid, pivmin) > j) hi = mid;
+            else lo = mid;
+        }
+        lam = 0.5 * (lo + hi);
+        base[lay.lam + lane] = lam;
+    }
+    // inverse iteration: (T - lam I) = P L U (dgttrf), three solves (dgttrs), normalised
+    double* lu = base + lay.lu;
+    auto at = [&](int arr, int i) -> double& { return lu[((long long)arr * mt + i) * TRI_LANES + lane]; };
+    if (lane < r) {
+        for (int i = 0; i < mt; ++i) {
+            at(0, i) = e[i];           // dl
+            at(1, i) = d[i] - lam;     // d
+            at(2, i) = e[i];           // du
+            at(3, i) = 0.0;            // du2
+            at(4, i) = 0.0;            // row interchange flag
+            at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * lane);  // start vector
+        }
+        for (int i = 0; i + 1 < mt; ++i) {
+            const double di = at(1, i), dli = at(0, i);
+            if (fabs(di) >= fabs(dli)) {
+                if (di != 0.0) {
+                    const double f = dli / di;
+                    at(0, i) = f;
+                    at(1, i + 1) -= f * at(2, i);
+                }
+            } else {
+                const double f = di / dli;
+                at(1, i) = dli;
+                at(0, i) = f;
+                const double tmp = at(2, i);
+                at(2, i) = at(1, i + 1);
+                at(1, i + 1) = tmp - f * at(1, i + 1);
+                if (i + 2 < mt) {
+                    at(3, i) = at(2, i + 1);
+                    at(2, i + 1) = -f * at(2, i + 1);
+                }
+                at(4, i) = 1.0;
+            }
+        }
+        const double tiny = eps * tn;  // perturb (near-)zero pivots, as dlagts
+        for (int i = 0; i < mt; ++i) {
+            const double di = at(1, i);
+            if (fabs(di) < tiny) at(1, i) = di < 0.0 ? -tiny : tiny;
+        }
+        for (int sweep = 0; sweep < 3; ++sweep) {
+            for (int i = 0; i + 1 < mt; ++i) {
+                if (at(4, i) == 0.0) {
+                    at(5, i + 1) -= at(0, i) * at(5, i);
+                } else {
+                    const double tb = at(5, i);
+                    at(5, i) = at(5, i + 1);
+                    at(5, i + 1) = tb - at(0, i) * at(5, i);
+                }
+            }
+            at(5, mt - 1) /= at(1, mt - 1);
+            if (mt > 1) at(5, mt - 2) = (at(5, mt - 2) - at(2, mt - 2) * at(5, mt - 1)) / at(1, mt - 2);
+            for (int i = mt - 3; i >= 0; --i)
+                at(5, i) = (at(5, i) - at(2, i) * at(5, i + 1) - at(3, i) * at(5, i + 2)) / at(1, i);
+            double nrm = 0.0;
+            for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
+            const double inv = 1.0 / sqrt(nrm);
+            for (int i = 0; i < mt; ++i) at(5, i) *= inv;
+        }
+        double* z = base + lay.z + (long long)lane * mt;
+        for (int i = 0; i < mt; ++i) z[i] = at(5, i);
+    }
+    __syncthreads();
+    // Gram-Schmidt inside clusters (eigenvalues closer than 1e-3 ||T||, LAPACK dstein ORTOL)
+    const double* lams = base + lay.lam;
+    double* Z = base + lay.z;
+    for (int k = 1; k < r; ++k) {
+        const double lk = lams[k];
+        int j0 = k;
+        while (j0 > 0 && lams[j0 - 1] - lk < 1e-3 * tn) --j0;
+        if (j0 == k) continue;
+        double* zk = Z + (long long)k * mt;
+        for (int j = j0; j < k; ++j) {
+            const double* zj = Z + (long long)j * mt;
+            double s = 0.0;
+            for (int i = lane; i < mt; i += TRI_LANES) s += zj[i] * zk[i];
+            s = wave_sum(s);
+            for (int i = lane; i < mt; i += TRI_LANES) zk[i] -= s * zj[i];
+            __syncthreads();
+        }
+        double s = 0.0;
+        for (int i = lane; i < mt; i += TRI_LANES) s += zk[i] * zk[i];
+        s = 1.0 / sqrt(wave_sum(s));
+        for (int i = lane; i < mt; i += TRI_LANES) zk[i] *= s;
+        __syncthreads();
+    }
+    if (lane == 0 && status && !(tn > 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+}
+
+// u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),
+// W_k = D u_k.  Wave w owns vectors k = w, w + 4, ...
+__global__ __launch_bounds__(256) void backxf_kernel(int mt, int r, const double* scratch, SpecLayout lay,
+                                                     double* Wout) {
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const double* base = scratch + b * lay.stride;
+    const d2* C = reinterpret_cast<const d2*>(base + lay.C);
+    const d2* taus = reinterpret_cast<const d2*>(base + lay.tau);
+    d2* W = reinterpret_cast<d2*>(Wout) + (long long)b * r * mt;
+    for (int k = wv; k < r; k += 4) {
+        d2* u = W + (long long)k * mt;
+        const double* z = base + lay.z + (long long)k * mt;
+        for (int i = lane; i < mt; i += 64) u[i] = make_double2(z[i], 0.0);
+    }
+    for (int j = mt - 2; j >= 0; --j) {
+        const d2 tau = taus[j];
+        if (tau.x == 0.0 && tau.y == 0.0) continue;
+        const int L = mt - j - 1;
+        const d2* v = C + (long long)j * mt + j + 1;   // v[0] = 1
+        for (int k = wv; k < r; k += 4) {
+            d2* u = W + (long long)k * mt + j + 1;
+            double sr = 0.0, si = 0.0;
+            for (int i = lane; i < L; i += 64) {
+                const d2 q = cmulc(v[i], u[i]);
+                sr += q.x;
+                si += q.y;
+            }
+            sr = wave_sum(sr);
+            si = wave_sum(si);
+            const d2 f = cmul(tau, make_double2(sr, si));
+            for (int i = lane; i < L; i += 64) u[i] = csub(u[i], cmul(f, v[i]));
+        }
+    }
+    const double* dv = base + lay.dv;
+    for (int k = wv; k < r; k += 4) {
+        d2* u = W + (long long)k * mt;
+        for (int i = lane; i < mt; i += 64) u[i] = cscale(u[i], dv[i]);
+    }
+}
+}  // namespace
+
+size_t spectral_scratch_bytes(int mt, int batch, int r) {
+    const SpecLayout lay(mt, r);
+    const int chunk = batch < SPEC_CHUNK ? batch : SPEC_CHUNK;
+    return sizeof(double) * (size_t)lay.stride * chunk;
+}
+
+int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
+                    int* status, hipStream_t st) {
+    const SpecLayout lay(mt, r);
+    const size_t sm_h = (size_t)mt * (16 + 16 + 8), sm_t = (size_t)mt * 16;
+    if (sm_h > 160 * 1024) return ACE_ERR_UNSUPPORTED;
+    for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
+        const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
+        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(256), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay);
+        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(TRI_LANES), sm_t, st, mt, r, scratch, lay, status, b0);
+        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), 0, st, mt, r, scratch, lay,
+                           W + 2LL * b0 * r * mt);
+    }
+    return ACE_OK;
+}
+
+}  // namespace ace

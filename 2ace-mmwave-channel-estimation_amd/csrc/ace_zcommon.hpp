@@ -86,7 +86,7 @@ __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, doubl
     const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
     const double obj = sqrt(st->obj2);
     const double nAX = sqrt(st->nAX2), nY = sqrt(st->nY2);
-    const double r = 1.0;  // columns per realisation
+    const double r = (double)a.r;  // columns per realisation
     int improved = 0;
     if (obj < st->opt_obj) {
         st->opt_obj = obj;

@@ -59,6 +59,7 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
 template <bool INIT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zstep1w_kernel(ZArgs a) {
     const int b = blockIdx.x, lane = threadIdx.x;
+    const ZProfile pf = z_profile(a, b);
     const int n = a.n, m = a.m, tx = a.tx, rx = a.rx;
     RealState* st = a.st + b;
     if (!INIT && st->done) return;
@@ -142,10 +143,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
             double v = 0.0;
             for (int k = 0; k < ZT; ++k) v += rs2[k];
             int ok = v > 0.0;
-            for (int pi = 0; pi < a.np; ++pi) {
+            for (int pi = 0; pi < pf.np; ++pi) {
                 double vr = 0.0;
-                for (int k = 0; k < a.rl[pi]; ++k) vr += rs2[k];
-                ok &= vr > a.fl[pi] * v * (1.0 + 1e-9);
+                for (int k = 0; k < pf.rl[pi]; ++k) vr += rs2[k];
+                ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
             }
             flag_fast = ok;
         }
@@ -347,9 +348,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     __syncthreads();
     if (lane == 0) {  // rank-profile tail rescaling (:469-480), sequential sums
         for (int k = 0; k < tx; ++k) rs2[k] = fmax(0.0, wv[ord[k]]);
-        for (int pi = 0; pi < a.np; ++pi) {
-            const int r = a.rl[pi];
-            const double f = a.fl[pi];
+        for (int pi = 0; pi < pf.np; ++pi) {
+            const int r = pf.rl[pi];
+            const double f = pf.fl[pi];
             double vr = 0.0, v = 0.0;
             for (int k = 0; k < r; ++k) vr += rs2[k];
             for (int k = 0; k < tx; ++k) v += rs2[k];

@@ -12,6 +12,16 @@
  *                            inferLowRankV4_multi.m:92 / :100 is r = 1, scale_by_row = 1.
  *  ace_admm_solve_host    <- the same, on host arrays (drop-in for MATLAB Engine calls
  *                            that pass matlab.double buffers; main/main.py:427-437).
+ *  ace_pipeline_solve_batch <- [X,Y,quality] = inferLowRankV4_multi(A,B,tx,rx)
+ *                            main/src/my_recovery_algorithms/ADMM_v2/inferLowRankV4_multi.m:5-109
+ *                            (3 restarts), Numerical_Simulation/.../inferLowRankV4.m (1 restart)
+ *                            and inferLowRank_Nuclear.m (1 restart, nuclear Z-prox), as called by
+ *                            ADMM_v2(meas,FW,TX,RX,version) (ADMM_v2.m:30-32) and
+ *                            ADMM_v2_nuclear.m:30-32.  Spectral initialisation (:561-574),
+ *                            inferLowRankImpl (:111-271: r = 20 row-scaled stage, rotation by
+ *                            eig(X'X), per-column stage), test quality and rank-one retry
+ *                            (:68-77), best of restarts (:79-83), refinement (:89-101),
+ *                            rollback and rescale (:93-107) -- all on the GPU.
  *  ace_synth_*            <- synthetic trace generation with the semantics of
  *                            main/src/generate_channel/Generate_Channel.m:64-164,
  *                            generate_sensing_matrix/Generate_Sensing_Matrix.m:85-122
@@ -56,6 +66,7 @@ extern "C" {
 #define ACE_ST_CONVERGED 1u   /* convergence test (inferLowRankV4_multi.m:372) passed */
 #define ACE_ST_NO_OPT 2u      /* objective never finite: returned last iterate (reference would raise) */
 #define ACE_ST_EIG_NOCONV 4u  /* Z-prox Jacobi hit its sweep cap at least once */
+#define ACE_ST_ROLLBACK 8u    /* pipeline: refinement rolled back to X_max (inferLowRankV4_multi.m:94-98) */
 
 typedef struct ace_admm_cfg {
     int variant;       /* ACE_VARIANT_* */
@@ -101,6 +112,47 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
 int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx,
                         const double* A, const double* B, const double* X0,
                         double* X, double* Y, int32_t* iters, uint32_t* status, double* mu);
+
+/* ---- full recovery pipeline (inferLowRankV4_multi / inferLowRankV4 / inferLowRank_Nuclear) ----
+ * MATLAB's randsample (:48) is replaced by caller-supplied train partitions: train_idx is a
+ * HOST array [restarts][m_t] of 0-based row indices, m_t = floor(m * cc_frac), shared by the
+ * whole batch (one codebook, one partition per restart: every GEMM of the stages then runs
+ * on one shared A_t); test rows are the sorted complement (setdiff, :49).
+ * Per realisation, stage_iters holds 4*restarts + 1 counts: for each restart the two
+ * inferLowRankImpl stages (:258, :270), then the two stages of the rank-one retry (:73-77;
+ * 0 when not run), then the refinement (:92/:100) -- the order of the oracle's stage_iters. */
+typedef struct ace_pipeline_cfg {
+    int variant;       /* ACE_VARIANT_A2ONLY (keep best restart) or ACE_VARIANT_NUCLEAR (last restart) */
+    int restarts;      /* 3 (inferLowRankV4_multi.m:42), 1 (inferLowRankV4, inferLowRank_Nuclear) */
+    int r;             /* 20 (:7); clipped to min(r, m, n) (:19), must be <= 32 */
+    int maxiter;       /* 500 (:13), every stage */
+    int eig_warm;      /* warm-start the Z-prox eigensolver inside each stage */
+    int reserved[3];
+    double mu0;        /* 1e-3 */
+    double rho;        /* 1.03 */
+    double cc_frac;    /* 0.95 (:10) */
+    double tol_rel;    /* 1e-4 */
+    double tol_abs;    /* 1e-8 */
+} ace_pipeline_cfg;
+
+/* Reference defaults for `variant`: A2only -> 3 restarts, nuclear -> 1 restart. */
+void ace_pipeline_cfg_default(ace_pipeline_cfg* cfg, int variant);
+/* Workspace bytes for ace_pipeline_solve_batch (0 on invalid arguments). */
+size_t ace_pipeline_workspace_size(const ace_pipeline_cfg* cfg, int batch, int m, int n);
+/* Batched pipeline on device buffers (shared codebook A [m][n] c128, B [batch][m] f64).
+ * Outputs: X [batch][n], Y [batch][m] (c128; Y's last m - m_t entries are 0 after a
+ * rollback, whose Y_max lives on the train rows), quality [batch] (the LAST restart's, as
+ * the reference returns), stage_iters [batch][4*restarts+1], status [batch] (ACE_ST_*).
+ * quality, stage_iters and status may be NULL.  Synchronises `stream` once per restart
+ * (the rank-one retry set is decided on the host). */
+int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx,
+                             const double* A, const double* B, const int32_t* train_idx_host,
+                             double* X, double* Y, double* quality, int32_t* stage_iters, uint32_t* status,
+                             void* workspace, size_t workspace_bytes, void* stream);
+/* The same on host arrays (allocates, copies, solves, frees; synchronous). */
+int ace_pipeline_solve_host(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx,
+                            const double* A, const double* B, const int32_t* train_idx,
+                            double* X, double* Y, double* quality, int32_t* stage_iters, uint32_t* status);
 
 /* Synthetic traces (device).  Counter-based RNG (splitmix64 of seed/stream/counter),
  * identical integer streams to ace_amd.synth on the host.

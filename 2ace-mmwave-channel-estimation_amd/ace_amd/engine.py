@@ -1,0 +1,134 @@
+"""Drop-in for the MATLAB Engine session main.py drives (main/main.py:10, :308, :427-437).
+
+The reference calls, e.g.::
+
+    eng = matlab.engine.start_matlab()
+    H_amp, H_angle = eng.channel_recovery_ADMM_v2_simulation_A2only(
+        int(num_ant), int(num_ant), matlab.double(np.abs(cb).tolist()),
+        matlab.double(np.angle(cb).tolist()), matlab.double(rss.tolist()), eng.double(r+1), nargout=2)
+    H = np.squeeze(np.array(H_amp) * np.exp(1j * np.array(H_angle)))       # 8 x n
+
+With this module::
+
+    from ace_amd import engine as matlab_engine
+    eng = matlab_engine.start_matlab()
+    H_amp, H_angle = eng.channel_recovery_ADMM_v2_simulation_A2only(..., nargout=2)
+
+accepts the same arguments (``matlab.double`` lists, numpy arrays, ``eng.double``
+scalars), returns numpy arrays of MATLAB's shape (n_M, 1, n), and raises
+``MatlabExecutionError`` where the MATLAB function calls ``error``.  Each call runs
+the full recovery pipeline per sweep point on the GPU through
+``ace_recover_driver`` (libace.so); nothing falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import LIB, AceError, ACE_ERR_ARG
+
+DRIVER_A2ONLY, DRIVER_A2NUCLEAR, DRIVER_MULTIRES, DRIVER_PHASELIFT = 0, 1, 2, 3
+RSS_FCT = 1e5 / 3  # channel_recovery_ADMM_v2_simulation_A2only.m:125
+
+
+class MatlabExecutionError(RuntimeError):
+    """Raised where the reference MATLAB function raises (error(...))."""
+
+
+def double(x):
+    """matlab.double / eng.double stand-in: a float64 numpy array (or scalar)."""
+    a = np.asarray(x, dtype=np.float64)
+    return a if a.ndim else float(a)
+
+
+LIB.ace_recover_driver.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
+                                   C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+LIB.ace_recover_driver.restype = C.c_int
+LIB.ace_driver_m_sweep.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int32)]
+LIB.ace_driver_m_sweep.restype = C.c_int
+LIB.ace_driver_randperm.argtypes = [C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int32)]
+LIB.ace_driver_randperm.restype = C.c_int
+
+
+def m_sweep(tx, rx):
+    """The reference's 8-point M sweep (..._A2only.m:106-118)."""
+    out = (C.c_int32 * 8)()
+    k = LIB.ace_driver_m_sweep(int(tx), int(rx), out)
+    if k < 0:
+        raise MatlabExecutionError(LIB.ace_last_error().decode())
+    return np.array(out[:k], dtype=np.int64)
+
+
+def randperm(seed, stream, P, k):
+    """randperm(P, k) (0-based) from the build's counter RNG."""
+    out = np.empty(k, np.int32)
+    rc = LIB.ace_driver_randperm(int(seed), int(stream), int(P), int(k), out.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc < 0:
+        raise ValueError(LIB.ace_last_error().decode())
+    return out
+
+
+def recover(driver, tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id, M_list=None):
+    """ace_recover_driver on numpy inputs; returns (H_amp, H_angle) of shape (n_M, 1, n)."""
+    tx, rx = int(tx_ant_num), int(rx_ant_num)
+    amp = np.ascontiguousarray(np.asarray(cb_amp, dtype=np.float64))
+    ang = np.ascontiguousarray(np.asarray(cb_angle, dtype=np.float64))
+    rss = np.ascontiguousarray(np.asarray(rss_final, dtype=np.float64).reshape(-1))
+    n = tx * rx
+    if amp.ndim != 2 or amp.shape != ang.shape or amp.shape[1] != n or rss.size != amp.shape[0]:
+        raise MatlabExecutionError(f"codebook/rss shapes {amp.shape}/{ang.shape}/{rss.shape} do not match "
+                                   f"{tx}x{rx} antennas")
+    P = amp.shape[0]
+    if M_list is None:
+        Ms = None
+        nM = 8
+    else:
+        Ms = np.ascontiguousarray(np.asarray(M_list, dtype=np.int32).reshape(-1))
+        nM = Ms.size
+    H_amp = np.zeros((nM, n), np.float64)
+    H_ang = np.zeros((nM, n), np.float64)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    rc = LIB.ace_recover_driver(int(driver), tx, rx, P, dp(amp), dp(ang), dp(rss), int(seed_id), int(nM),
+                                None if Ms is None else Ms.ctypes.data_as(C.POINTER(C.c_int32)),
+                                dp(H_amp), dp(H_ang))
+    if rc < 0:
+        msg = LIB.ace_last_error().decode()
+        if rc == ACE_ERR_ARG:
+            raise MatlabExecutionError(msg)
+        raise AceError(rc, msg)
+    return H_amp[:rc, None, :], H_ang[:rc, None, :]
+
+
+class Engine:
+    """Object with the MATLAB function names main.py calls on its engine."""
+
+    @staticmethod
+    def double(x):
+        return double(x)
+
+    def _call(self, driver, args, nargout):
+        if nargout != 2:
+            raise MatlabExecutionError("these functions return [H_amp, H_angle] (nargout=2)")
+        return recover(driver, *args)
+
+    def channel_recovery_ADMM_v2_simulation_A2only(self, *args, nargout=2):
+        return self._call(DRIVER_A2ONLY, args, nargout)
+
+    def channel_recovery_ADMM_v2_simulation_A2nuclear(self, *args, nargout=2):
+        return self._call(DRIVER_A2NUCLEAR, args, nargout)
+
+    def channel_recovery_ADMM_v2_simulation_multiresolution(self, *args, nargout=2):
+        return self._call(DRIVER_MULTIRES, args, nargout)
+
+    def channel_recovery_ADMM_v2_simulation_phaselift(self, *args, nargout=2):
+        return self._call(DRIVER_PHASELIFT, args, nargout)
+
+    def quit(self):
+        pass
+
+
+def start_matlab(*_args, **_kw):
+    """matlab.engine.start_matlab() stand-in."""
+    return Engine()

@@ -171,13 +171,13 @@ __global__ __launch_bounds__(256) void ystep_r_kernel(int m, int r, const double
         RealState& s = st[b];
         if (ROW) {
             s.obj2 = v[0];
-        } else {  // [obj, j] = min(objs): first minimiser (:354)
+        } else {  // [obj, j] = min(objs): first minimiser, NaNs omitted as MATLAB's min (:354)
             int jm = 0;
             double best = sqrt(v[5]), o2 = v[5];
 #pragma unroll
             for (int j = 1; j < RMAX; ++j) {
                 const double o = sqrt(v[5 + j]);
-                if (j < r && o < best) { best = o; o2 = v[5 + j]; jm = j; }
+                if (j < r && (o < best || (best != best && o == o))) { best = o; o2 = v[5 + j]; jm = j; }
             }
             s.obj2 = o2;
             s.objcol = jm;

@@ -22,6 +22,10 @@
  *                            eig(X'X), per-column stage), test quality and rank-one retry
  *                            (:68-77), best of restarts (:79-83), refinement (:89-101),
  *                            rollback and rescale (:93-107) -- all on the GPU.
+ *  ace_recover_driver     <- [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_A2only /
+ *                            _A2nuclear / _multiresolution(tx,rx,cb_amp,cb_angle,rss_final,
+ *                            seed_id)  main/channel_recovery_ADMM_v2_simulation_A2only.m:9,
+ *                            called from main/main.py:427-437 through the MATLAB Engine.
  *  ace_synth_*            <- synthetic trace generation with the semantics of
  *                            main/src/generate_channel/Generate_Channel.m:64-164,
  *                            generate_sensing_matrix/Generate_Sensing_Matrix.m:85-122
@@ -153,6 +157,33 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
 int ace_pipeline_solve_host(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx,
                             const double* A, const double* B, const int32_t* train_idx,
                             double* X, double* Y, double* quality, int32_t* stage_iters, uint32_t* status);
+
+/* ---- driver-level boundary (MATLAB Engine calls of main/main.py:308, :427-437) ------------
+ *   [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution>(
+ *                         tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id)
+ *   main/channel_recovery_ADMM_v2_simulation_A2only.m:9-179 (A2nuclear, multiresolution alike).
+ * cb_amp / cb_angle: HOST [P][n] row-major f64 (codebook row p = beam p; MATLAB callers pass
+ * the transpose of their P x n arrays), rss_dbm: [P] (dBm).  M_list = NULL selects the
+ * reference sweep round(linspace(2, sqrt(4*tx*rx), 8)).^2 (:106-118).  Outputs H_amp, H_angle:
+ * HOST [n_M][n] row-major (MATLAB's n_M x 1 x n squeezed), element k in vec(H) order
+ * (i + tx*j).  Returns the number of sweep points (>= 1) or a negative error code.
+ * Row selection uses the build's RNG seeded from the reference seed lists (MATLAB streams are
+ * not reproducible outside MATLAB).  Sweep points with floor(0.95 M) < min(20, M) train rows
+ * (M = 4) are ill-posed for the spectral initialisation and return 0 (the reference's
+ * NaN -> 0 of :176). */
+#define ACE_DRIVER_A2ONLY 0     /* channel_recovery_ADMM_v2_simulation_A2only.m */
+#define ACE_DRIVER_A2NUCLEAR 1  /* channel_recovery_ADMM_v2_simulation_A2nuclear.m */
+#define ACE_DRIVER_MULTIRES 2   /* channel_recovery_ADMM_v2_simulation_multiresolution.m */
+#define ACE_DRIVER_PHASELIFT 3  /* channel_recovery_ADMM_v2_simulation_phaselift.m (not implemented) */
+int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
+                       const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list,
+                       double* H_amp, double* H_angle);
+/* The reference M sweep for (tx, rx) into M_out[8]; returns 8 or a negative error code
+ * (..._A2only.m:106-118, error :117). */
+int ace_driver_m_sweep(int tx, int rx, int32_t* M_out);
+/* First k entries of a uniform random permutation of 0..P-1 (randperm(P,k) / randsample,
+ * 0-based, sampled order) from the build's counter RNG (seed, stream).  Host only. */
+int ace_driver_randperm(uint64_t seed, uint64_t stream, int P, int k, int32_t* out);
 
 /* Synthetic traces (device).  Counter-based RNG (splitmix64 of seed/stream/counter),
  * identical integer streams to ace_amd.synth on the host.

@@ -232,7 +232,8 @@ def infer_admm(A, B, X0, scale_by_row, use_rank_one, tx, rx, *, mu0=1e-3, rho=1.
                 opt_obj, opt_X, opt_Y = obj, X.copy(), Y.copy()
         else:                                                   # :352-361
             objs = np.sqrt(np.sum((np.abs(AX) - B[:, None]) ** 2, axis=0))
-            j = int(np.argmin(objs))
+            # MATLAB's min omits NaN and returns the first minimiser (index 1 if all NaN)
+            j = 0 if np.all(np.isnan(objs)) else int(np.nanargmin(objs))
             obj = float(objs[j])
             if obj < opt_obj:
                 opt_obj, opt_X, opt_Y = obj, X[:, [j]].copy(), Y[:, [j]].copy()

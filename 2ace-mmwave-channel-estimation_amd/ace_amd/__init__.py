@@ -10,6 +10,7 @@ from .solver import InferADMM, infer_admm_batch, infer_admm_host, synth_problem,
 from .pipeline import (inferLowRankV4_multi, inferLowRankV4, inferLowRank_Nuclear,  # noqa: F401
                        infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, draw_partitions,
                        PipelineResult)
+from .phaselift import MyPhaseLift, phaselift_host, phaselift_batch, PhaseLiftResult  # noqa: F401
 from . import synth, engine  # noqa: F401
 
 __version__ = LIB.ace_version().decode()

@@ -46,4 +46,19 @@ size_t spectral_scratch_bytes(int mt, int batch, int r);
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
                     int* status, hipStream_t st);
 
+// ---- batched Hermitian eigenpairs (ace_spectral.hip) for PhaseLift's prox_trace
+// (TFOCS/prox_trace.m:88-147) and MyPhaseLift's final eig (MyPhaseLift.m:106-107).
+// Each realisation's d x d Hermitian matrix sits in the scratch at `C` (doubles, complex
+// row-major) within a per-realisation `stride`; tau != null selects all eigenvalues > tau[b]
+// (at most kmax), tau == null the kmax largest; descending.  V [batch][kmax][d] receives
+// eigenvector q as row q; the scratch's `misc` slot holds {k_b, sum(lam - tau)}, `lam` the
+// eigenvalues.  The matrix is destroyed; realisations with active[b] == 0 are skipped.
+struct HeevLayout {
+    long long stride, C, misc, lam;
+};
+HeevLayout heev_layout(int d, int kmax);
+size_t heev_scratch_bytes(int d, int kmax, int batch);
+int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
+                const int* active, hipStream_t st);
+
 }  // namespace ace

@@ -13,11 +13,12 @@
 //                    lower, with full Hermitian storage in global memory so that the
 //                    Hermitian matrix-vector product reads rows coalesced); reflector k is
 //                    left in row k of C
-//   trieig_kernel    one wave per realisation, lane k <-> k-th largest eigenvalue:
-//                    Sturm-count bisection to full precision, then inverse iteration on
-//                    the tridiagonal (partial-pivoting LU as LAPACK dgttrf/dgttrs, three
-//                    solves) and Gram-Schmidt inside eigenvalue clusters (relative
-//                    separation < 1e-3, as dstein)
+//   trieig_kernel    one work-group per realisation: the r largest eigenvalues (or, for
+//                    PhaseLift's prox_trace, all above a threshold) by Sturm-count
+//                    bisection to full precision, then inverse iteration on the
+//                    tridiagonal (partial-pivoting LU as LAPACK dgttrf/dgttrs, three
+//                    solves), one thread per eigenvalue cluster (relative separation
+//                    < 1e-3, as dstein) with the cluster's earlier vectors projected out
 //   backxf_kernel    one work-group per realisation: u_k = H_0 H_1 ... H_{m_t-2} z_k,
 //                    W_k = D u_k
 //
@@ -30,12 +31,14 @@ namespace ace {
 
 namespace {
 constexpr int SPEC_CHUNK = 256;   // realisations per launch (C = 0.9 MiB each at m_t = 243)
-constexpr int TRI_LANES = 64;
 
 // per-realisation scratch layout (units: doubles)
 struct SpecLayout {
-    long long C, dv, dd, ee, tau, lu, z, lam, stride;
-    SpecLayout(int mt, int r) {
+    long long C, dv, dd, ee, tau, lu, z, lam, cl, misc, stride;
+    int kmax, lanes;
+    SpecLayout(int mt, int kmax_) {
+        kmax = kmax_;
+        lanes = kmax <= 64 ? 64 : 256;   // inverse-iteration lanes (one eigenvalue cluster each)
         long long o = 0;
         auto take = [&](long long nd) { long long p = o; o += (nd + 31) & ~31LL; return p; };
         C = take(2LL * mt * mt);
@@ -43,16 +46,19 @@ struct SpecLayout {
         dd = take(mt);
         ee = take(mt);
         tau = take(2LL * mt);
-        lu = take(6LL * mt * TRI_LANES);   // dl, d, du, du2, ipiv, y  (lane-interleaved)
-        z = take((long long)r * mt);
-        lam = take(r);
+        lu = take(6LL * mt * lanes);       // dl, d, du, du2, ipiv, y  (lane-interleaved)
+        z = take((long long)kmax * mt);
+        lam = take(kmax);
+        cl = take(kmax + 1);               // cluster starts (as doubles)
+        misc = take(8);                    // [0] k, [1] sum(lam - tau)
         stride = o;
     }
 };
 
 __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
-                                                    SpecLayout lay) {
+                                                    SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
+    if (active && !active[b]) return;
     extern __shared__ double smem[];
     d2* v = reinterpret_cast<d2*>(smem);   // reflector / x (mt)
     d2* w = v + mt;                        // p, w (mt)
@@ -66,6 +72,7 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
     double* ee = base + lay.ee;
     d2* taus = reinterpret_cast<d2*>(base + lay.tau);
 
+    if (Kp) {
     // D = diag(B_i / ||a_i||), ||a_i||^2 = K_ii  (SpectralInitialize :563-567; zero rows stay zero)
     for (int i = t; i < mt; i += 256) {
         const double kii = K[(long long)i * mt + i].x;
@@ -80,6 +87,7 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
         const d2 kij = K[e], kji = K[(long long)j * mt + i];
         const double s = dvs[i] * dvs[j];
         C[e] = i == j ? make_double2(s * kij.x, 0.0) : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
+    }
     }
     __syncthreads();
 
@@ -186,21 +194,30 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     return cnt;
 }
 
-__global__ __launch_bounds__(TRI_LANES) void trieig_kernel(int mt, int r, double* scratch, SpecLayout lay,
-                                                           int* status, int status_off) {
-    const int b = blockIdx.x, lane = threadIdx.x;
+// Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
+// (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
+// Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
+// LU of LAPACK dgttrf/dgttrs, three solves, one thread per eigenvalue cluster (relative
+// separation < 1e-3 ||T||, LAPACK dstein's ORTOL) with the cluster's earlier vectors
+// projected out after every solve (as dstein).  Writes z[k][mt], lam[k], misc = {k, sum(lam - tau)}.
+__global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p, double* scratch, SpecLayout lay,
+                                                     int* status, int status_off, const int* active) {
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (active && !active[b]) return;
     extern __shared__ double smem[];
     double* d = smem;
     double* e = smem + mt;
+    __shared__ double red[3 * 4];
+    __shared__ int s_k, s_ncl;
     double* base = scratch + b * lay.stride;
-    for (int i = lane; i < mt; i += TRI_LANES) {
+    for (int i = t; i < mt; i += 256) {
         d[i] = base[lay.dd + i];
         e[i] = base[lay.ee + i];
     }
     __syncthreads();
     // Gershgorin interval and pivmin (LAPACK dstebz)
     double gl = INFINITY, gu = -INFINITY, emax = 0.0;
-    for (int i = lane; i < mt; i += TRI_LANES) {
+    for (int i = t; i < mt; i += 256) {
         const double a = i > 0 ? fabs(e[i - 1]) : 0.0, c = i + 1 < mt ? fabs(e[i]) : 0.0;
         gl = fmin(gl, d[i] - a - c);
         gu = fmax(gu, d[i] + a + c);
@@ -212,15 +229,31 @@ __global__ __launch_bounds__(TRI_LANES) void trieig_kernel(int mt, int r, double
         gu = fmax(gu, __shfl_xor(gu, o, 64));
         emax = fmax(emax, __shfl_xor(emax, o, 64));
     }
+    if (lane == 0) { red[wv] = gl; red[4 + wv] = gu; red[8 + wv] = emax; }
+    __syncthreads();
+    gl = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+    gu = fmax(fmax(red[4], red[5]), fmax(red[6], red[7]));
+    emax = fmax(fmax(red[8], red[9]), fmax(red[10], red[11]));
     const double eps = 2.220446049250313e-16;
     const double tn = fmax(fabs(gl), fabs(gu));
     const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax);
     gl -= 2.0 * tn * eps * mt;
     gu += 2.0 * tn * eps * mt;
-
-    double lam = 0.0;
-    if (lane < r) {  // bisection for the (mt-1-lane)-th ascending eigenvalue
-        const int j = mt - 1 - lane;
+    const double tau = tau_p ? tau_p[status_off + b] : 0.0;
+    if (t == 0) {
+        int k = lay.kmax < mt ? lay.kmax : mt;
+        if (tau_p) {  // eigenvalues strictly above tau (prox_trace keeps s = lam - tau > 0)
+            const int kk = mt - sturm_count(d, e, mt, tau, pivmin);
+            if (kk > k && status) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+            k = kk < k ? kk : k;
+        }
+        s_k = k;
+    }
+    __syncthreads();
+    const int k = s_k;
+    double* lam = base + lay.lam;
+    for (int q = t; q < k; q += 256) {  // bisection for the (mt-1-q)-th ascending eigenvalue
+        const int j = mt - 1 - q;
         double lo = gl, hi = gu;
         for (int it = 0; it < 200; ++it) {
             if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
@@ -228,106 +261,110 @@ __global__ __launch_bounds__(TRI_LANES) void trieig_kernel(int mt, int r, double
             if (sturm_count(d, e, mt, mid, pivmin) > j) hi = mid;
             else lo = mid;
         }
-        lam = 0.5 * (lo + hi);
-        base[lay.lam + lane] = lam;
-    }
-    // inverse iteration: (T - lam I) = P L U (dgttrf), three solves (dgttrs), normalised
-    double* lu = base + lay.lu;
-    auto at = [&](int arr, int i) -> double& { return lu[((long long)arr * mt + i) * TRI_LANES + lane]; };
-    if (lane < r) {
-        for (int i = 0; i < mt; ++i) {
-            at(0, i) = e[i];           // dl
-            at(1, i) = d[i] - lam;     // d
-            at(2, i) = e[i];           // du
-            at(3, i) = 0.0;            // du2
-            at(4, i) = 0.0;            // row interchange flag
-            at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * lane);  // start vector
-        }
-        for (int i = 0; i + 1 < mt; ++i) {
-            const double di = at(1, i), dli = at(0, i);
-            if (fabs(di) >= fabs(dli)) {
-                if (di != 0.0) {
-                    const double f = dli / di;
-                    at(0, i) = f;
-                    at(1, i + 1) -= f * at(2, i);
-                }
-            } else {
-                const double f = di / dli;
-                at(1, i) = dli;
-                at(0, i) = f;
-                const double tmp = at(2, i);
-                at(2, i) = at(1, i + 1);
-                at(1, i + 1) = tmp - f * at(1, i + 1);
-                if (i + 2 < mt) {
-                    at(3, i) = at(2, i + 1);
-                    at(2, i + 1) = -f * at(2, i + 1);
-                }
-                at(4, i) = 1.0;
-            }
-        }
-        const double tiny = eps * tn;  // perturb (near-)zero pivots, as dlagts
-        for (int i = 0; i < mt; ++i) {
-            const double di = at(1, i);
-            if (fabs(di) < tiny) at(1, i) = di < 0.0 ? -tiny : tiny;
-        }
-        for (int sweep = 0; sweep < 3; ++sweep) {
-            for (int i = 0; i + 1 < mt; ++i) {
-                if (at(4, i) == 0.0) {
-                    at(5, i + 1) -= at(0, i) * at(5, i);
-                } else {
-                    const double tb = at(5, i);
-                    at(5, i) = at(5, i + 1);
-                    at(5, i + 1) = tb - at(0, i) * at(5, i);
-                }
-            }
-            at(5, mt - 1) /= at(1, mt - 1);
-            if (mt > 1) at(5, mt - 2) = (at(5, mt - 2) - at(2, mt - 2) * at(5, mt - 1)) / at(1, mt - 2);
-            for (int i = mt - 3; i >= 0; --i)
-                at(5, i) = (at(5, i) - at(2, i) * at(5, i + 1) - at(3, i) * at(5, i + 2)) / at(1, i);
-            double nrm = 0.0;
-            for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
-            const double inv = 1.0 / sqrt(nrm);
-            for (int i = 0; i < mt; ++i) at(5, i) *= inv;
-        }
-        double* z = base + lay.z + (long long)lane * mt;
-        for (int i = 0; i < mt; ++i) z[i] = at(5, i);
+        lam[q] = 0.5 * (lo + hi);
     }
     __syncthreads();
-    // Gram-Schmidt inside clusters (eigenvalues closer than 1e-3 ||T||, LAPACK dstein ORTOL)
-    const double* lams = base + lay.lam;
-    double* Z = base + lay.z;
-    for (int k = 1; k < r; ++k) {
-        const double lk = lams[k];
-        int j0 = k;
-        while (j0 > 0 && lams[j0 - 1] - lk < 1e-3 * tn) --j0;
-        if (j0 == k) continue;
-        double* zk = Z + (long long)k * mt;
-        for (int j = j0; j < k; ++j) {
-            const double* zj = Z + (long long)j * mt;
-            double s = 0.0;
-            for (int i = lane; i < mt; i += TRI_LANES) s += zj[i] * zk[i];
-            s = wave_sum(s);
-            for (int i = lane; i < mt; i += TRI_LANES) zk[i] -= s * zj[i];
-            __syncthreads();
+    double* cl = base + lay.cl;
+    if (t == 0) {
+        int nc = 0;
+        double sum = 0.0;
+        for (int q = 0; q < k; ++q) {
+            if (q == 0 || lam[q - 1] - lam[q] >= 1e-3 * tn) cl[nc++] = q;
+            sum += lam[q] - tau;
         }
-        double s = 0.0;
-        for (int i = lane; i < mt; i += TRI_LANES) s += zk[i] * zk[i];
-        s = 1.0 / sqrt(wave_sum(s));
-        for (int i = lane; i < mt; i += TRI_LANES) zk[i] *= s;
-        __syncthreads();
+        cl[nc] = k;
+        s_ncl = nc;
+        base[lay.misc] = k;
+        base[lay.misc + 1] = sum;
     }
-    if (lane == 0 && status && !(tn > 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+    __syncthreads();
+    const int ncl = s_ncl;
+    double* lu = base + lay.lu;
+    double* Z = base + lay.z;
+    const double tiny = eps * tn;  // perturb (near-)zero pivots, as dlagts
+    for (int c = t; c < ncl; c += 256) {
+        const int ln = c % lay.lanes;
+        auto at = [&](int arr, int i) -> double& { return lu[((long long)arr * mt + i) * lay.lanes + ln]; };
+        const int q0 = (int)cl[c], q1 = (int)cl[c + 1];
+        for (int q = q0; q < q1; ++q) {
+            const double lq = lam[q];
+            for (int i = 0; i < mt; ++i) {
+                at(0, i) = e[i];
+                at(1, i) = d[i] - lq;
+                at(2, i) = e[i];
+                at(3, i) = 0.0;
+                at(4, i) = 0.0;
+                at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * q);  // start vector
+            }
+            for (int i = 0; i + 1 < mt; ++i) {  // dgttrf
+                const double di = at(1, i), dli = at(0, i);
+                if (fabs(di) >= fabs(dli)) {
+                    if (di != 0.0) {
+                        const double f = dli / di;
+                        at(0, i) = f;
+                        at(1, i + 1) -= f * at(2, i);
+                    }
+                } else {
+                    const double f = di / dli;
+                    at(1, i) = dli;
+                    at(0, i) = f;
+                    const double tmp = at(2, i);
+                    at(2, i) = at(1, i + 1);
+                    at(1, i + 1) = tmp - f * at(1, i + 1);
+                    if (i + 2 < mt) {
+                        at(3, i) = at(2, i + 1);
+                        at(2, i + 1) = -f * at(2, i + 1);
+                    }
+                    at(4, i) = 1.0;
+                }
+            }
+            for (int i = 0; i < mt; ++i) {
+                const double di = at(1, i);
+                if (fabs(di) < tiny) at(1, i) = di < 0.0 ? -tiny : tiny;
+            }
+            double* zq = Z + (long long)q * mt;
+            for (int sweep = 0; sweep < 3; ++sweep) {
+                for (int i = 0; i + 1 < mt; ++i) {  // dgttrs
+                    if (at(4, i) == 0.0) {
+                        at(5, i + 1) -= at(0, i) * at(5, i);
+                    } else {
+                        const double tb = at(5, i);
+                        at(5, i) = at(5, i + 1);
+                        at(5, i + 1) = tb - at(0, i) * at(5, i);
+                    }
+                }
+                at(5, mt - 1) /= at(1, mt - 1);
+                if (mt > 1) at(5, mt - 2) = (at(5, mt - 2) - at(2, mt - 2) * at(5, mt - 1)) / at(1, mt - 2);
+                for (int i = mt - 3; i >= 0; --i)
+                    at(5, i) = (at(5, i) - at(2, i) * at(5, i + 1) - at(3, i) * at(5, i + 2)) / at(1, i);
+                for (int p = q0; p < q; ++p) {  // project out the cluster's earlier vectors
+                    const double* zp = Z + (long long)p * mt;
+                    double s = 0.0;
+                    for (int i = 0; i < mt; ++i) s += zp[i] * at(5, i);
+                    for (int i = 0; i < mt; ++i) at(5, i) -= s * zp[i];
+                }
+                double nrm = 0.0;
+                for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
+                const double inv = 1.0 / sqrt(nrm);
+                for (int i = 0; i < mt; ++i) at(5, i) *= inv;
+            }
+            for (int i = 0; i < mt; ++i) zq[i] = at(5, i);
+        }
+    }
+    if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
 }
 
 // u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),
 // W_k = D u_k.  Wave w owns vectors k = w, w + 4, ...
-__global__ __launch_bounds__(256) void backxf_kernel(int mt, int r, const double* scratch, SpecLayout lay,
-                                                     double* Wout) {
+__global__ __launch_bounds__(256) void backxf_kernel(int mt, int ldw, const double* scratch, SpecLayout lay,
+                                                     double* Wout, int scale_d, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (active && !active[b]) return;
     const double* base = scratch + b * lay.stride;
+    const int r = (int)base[lay.misc];
     const d2* C = reinterpret_cast<const d2*>(base + lay.C);
     const d2* taus = reinterpret_cast<const d2*>(base + lay.tau);
-    d2* W = reinterpret_cast<d2*>(Wout) + (long long)b * r * mt;
+    d2* W = reinterpret_cast<d2*>(Wout) + (long long)b * ldw * mt;
     for (int k = wv; k < r; k += 4) {
         d2* u = W + (long long)k * mt;
         const double* z = base + lay.z + (long long)k * mt;
@@ -352,6 +389,7 @@ __global__ __launch_bounds__(256) void backxf_kernel(int mt, int r, const double
             for (int i = lane; i < L; i += 64) u[i] = csub(u[i], cmul(f, v[i]));
         }
     }
+    if (!scale_d) return;
     const double* dv = base + lay.dv;
     for (int k = wv; k < r; k += 4) {
         d2* u = W + (long long)k * mt;
@@ -370,14 +408,33 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
                     int* status, hipStream_t st) {
     const SpecLayout lay(mt, r);
     const size_t sm_h = (size_t)mt * (16 + 16 + 8), sm_t = (size_t)mt * 16;
-    if (sm_h > 160 * 1024) return ACE_ERR_UNSUPPORTED;
+    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
-        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(256), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay);
-        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(TRI_LANES), sm_t, st, mt, r, scratch, lay, status, b0);
-        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), 0, st, mt, r, scratch, lay,
-                           W + 2LL * b0 * r * mt);
+        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(256), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay,
+                           nullptr);
+        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr);
+        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), 0, st, mt, r, scratch, lay, W + 2LL * b0 * r * mt, 1,
+                           nullptr);
     }
+    return ACE_OK;
+}
+
+// ---- thresholded / top-k Hermitian eigen (PhaseLift prox_trace and its final eig): see ace_pipe.hpp
+HeevLayout heev_layout(int d, int kmax) {
+    const SpecLayout lay(d, kmax);
+    return HeevLayout{lay.stride, lay.C, lay.misc, lay.lam};
+}
+size_t heev_scratch_bytes(int d, int kmax, int batch) { return sizeof(double) * (size_t)SpecLayout(d, kmax).stride * batch; }
+
+int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
+                const int* active, hipStream_t st) {
+    const SpecLayout lay(d, kmax);
+    const size_t sm_h = (size_t)d * (16 + 16 + 8), sm_t = (size_t)d * 16;
+    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(256), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
+    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
+    hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), 0, st, d, kmax, scratch, lay, V, 0, active);
     return ACE_OK;
 }
 

@@ -22,6 +22,9 @@
  *                            eig(X'X), per-column stage), test quality and rank-one retry
  *                            (:68-77), best of restarts (:79-83), refinement (:89-101),
  *                            rollback and rescale (:93-107) -- all on the GPU.
+ *  ace_phaselift_solve_batch <- recoveredSig = MyPhaseLift(measurements, measurementMat)
+ *                            main/src/my_recovery_algorithms/MyPhaseLift.m:69-107 (TFOCS
+ *                            solver_TraceLS + tfocs_AT, prox_trace), batched over realisations.
  *  ace_recover_driver     <- [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_A2only /
  *                            _A2nuclear / _multiresolution(tx,rx,cb_amp,cb_angle,rss_final,
  *                            seed_id)  main/channel_recovery_ADMM_v2_simulation_A2only.m:9,
@@ -157,6 +160,31 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
 int ace_pipeline_solve_host(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx,
                             const double* A, const double* B, const int32_t* train_idx,
                             double* X, double* Y, double* quality, int32_t* stage_iters, uint32_t* status);
+
+/* ---- PhaseLift (MyPhaseLift.m:69-107 via TFOCS solver_TraceLS / tfocs_AT) ----------------
+ *   recoveredSig = MyPhaseLift(measurements, measurementMat)
+ *   main/src/my_recovery_algorithms/MyPhaseLift.m:69 (called by Recover_Channel.m:34 with
+ *   measurements = (rss/2e5).^2*1e10).  A batch of measurement vectors b [batch][m] sharing one
+ *   measurement matrix Phi [m][n] (c128, row-major, DEVICE pointers); sig [batch][n] c128 out.
+ *   The iteration runs in the coordinates of range(Phi^H) (exact for MyPhaseLift's zero start);
+ *   m <= n needs full row rank (else ACE_ERR_UNSUPPORTED).  status: ACE_ST_CONVERGED when the
+ *   TFOCS step tolerance stopped the run before maxIts. */
+typedef struct ace_phaselift_cfg {
+    int maxIts;        /* 4000 (MyPhaseLift.m:82) */
+    int restart;       /* 200  (:84) */
+    int cntr_reset;    /* 50   (tfocs_initialize.m; 10 when tol < 1e-12) */
+    int reserved;
+    double tol;        /* 1e-10 (:83), stopCrit 1 */
+    double lambda;     /* 5e-2  (:91) */
+    double L0, alpha, beta;  /* 1, 0.9, 0.5 (tfocs_initialize.m defaults) */
+} ace_phaselift_cfg;
+void ace_phaselift_cfg_default(ace_phaselift_cfg* cfg);
+size_t ace_phaselift_workspace_size(const ace_phaselift_cfg* cfg, int batch, int m, int n);
+int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                              const double* b, double* sig, int32_t* iters, uint32_t* status,
+                              void* workspace, size_t workspace_bytes, void* stream);
+int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                             const double* b, double* sig, int32_t* iters, uint32_t* status);
 
 /* ---- driver-level boundary (MATLAB Engine calls of main/main.py:308, :427-437) ------------
  *   [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution>(

@@ -95,7 +95,7 @@ def recover(driver, tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id
                                 dp(H_amp), dp(H_ang))
     if rc < 0:
         msg = LIB.ace_last_error().decode()
-        if rc == ACE_ERR_ARG:
+        if rc == ACE_ERR_ARG and "unknown driver" not in msg:
             raise MatlabExecutionError(msg)
         raise AceError(rc, msg)
     return H_amp[:rc, None, :], H_ang[:rc, None, :]

@@ -1,5 +1,5 @@
 // Driver-level boundary: the MATLAB functions main.py calls through the MATLAB Engine,
-//   [H_amp, H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution>(
+//   [H_amp, H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution|phaselift>(
 //                          tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id)
 // (main/channel_recovery_ADMM_v2_simulation_A2only.m:9-179, ..._A2nuclear.m,
 //  ..._multiresolution.m; call sites main/main.py:308, :427-437).
@@ -10,6 +10,8 @@
 //   picked_beams = 1:M (Random_Phase_State, Generate_Sensing_Matrix_with_candidate.m:13)
 //   X = ADMM_v2(rss_train, cb_train, tx, rx, 4) = inferLowRankV4_multi / inferLowRank_Nuclear
 //       (Recover_Channel.m:27-31, ADMM_v2.m:30-32)  -> ace_pipeline_solve_batch on the GPU
+//   phaselift: X = MyPhaseLift((rss_train/2e5).^2*1e10, cb_train)/sqrt(1e10)*2e5
+//       (Recover_Channel.m:32-35)                   -> ace_phaselift_solve_batch on the GPU
 //   H_out(i,1,:) = X / rss_fct, NaN -> 0, H_amp = abs, H_angle = angle  (:170-178)
 // The drivers' Generate_Channel / Sparse_Channel_Formulation calls (:146-149) feed only the
 // baseline methods (their outputs never reach the ADMM recovery) and are not performed.
@@ -92,11 +94,9 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
                        const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list, double* H_amp,
                        double* H_angle) {
     g_err.clear();
-    if (driver != ACE_DRIVER_A2ONLY && driver != ACE_DRIVER_A2NUCLEAR && driver != ACE_DRIVER_MULTIRES) {
-        if (driver == ACE_DRIVER_PHASELIFT)
-            return fail(ACE_ERR_UNSUPPORTED, "PhaseLift driver (MyPhaseLift/TFOCS) is not implemented");
+    if (driver != ACE_DRIVER_A2ONLY && driver != ACE_DRIVER_A2NUCLEAR && driver != ACE_DRIVER_MULTIRES &&
+        driver != ACE_DRIVER_PHASELIFT)
         return fail(ACE_ERR_ARG, "unknown driver %d", driver);
-    }
     if (!cb_amp || !cb_angle || !rss_dbm || !H_amp || !H_angle) return fail(ACE_ERR_ARG, "NULL buffer");
     if (tx < 1 || rx < 1 || P < 1) return fail(ACE_ERR_ARG, "tx, rx, P must be >= 1");
     if (seed_id < 1 || seed_id > 40) return fail(ACE_ERR_ARG, "seed_id must be in 1..40 (MATLAB seeds(seed_id))");
@@ -128,7 +128,11 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
         }
         if (M < 1 || M > avail) return fail(ACE_ERR_ARG, "M = %d must be in [1, %d]", M, avail);
     }
-    const uint64_t seed = driver == ACE_DRIVER_A2NUCLEAR ? kNuclearSeeds[(seed_id - 1) % 4] : kSeeds[seed_id - 1];
+    // seeds: A2only / multiresolution rng(seeds(seed_id)) (:103-104); A2nuclear rng(seeds(randi(4)))
+    // (the build picks by seed_id); phaselift rng(4096) whatever seed_id (..._phaselift.m:127)
+    const uint64_t seed = driver == ACE_DRIVER_A2NUCLEAR   ? kNuclearSeeds[(seed_id - 1) % 4]
+                          : driver == ACE_DRIVER_PHASELIFT ? 4096
+                                                           : kSeeds[seed_id - 1];
 
     ace_pipeline_cfg cfg;
     ace_pipeline_cfg_default(&cfg, driver == ACE_DRIVER_A2NUCLEAR ? ACE_VARIANT_NUCLEAR : ACE_VARIANT_A2ONLY);
@@ -154,11 +158,20 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
             }
             B[r] = std::sqrt(std::pow(10.0, rss_dbm[row] / 10.0) / 1000.0) * kRssFct;   // db2pow
         }
-        // ---- Recover_Channel -> ADMM_v2(..., 4): the pipeline with its own train partitions
         std::vector<double> X(2 * (size_t)n), Y(2 * (size_t)M);
         double q = 0.0;
         int rc = ACE_OK;
-        if (n != tx * rx) return fail(ACE_ERR_ARG, "n != tx*rx");
+        if (driver == ACE_DRIVER_PHASELIFT) {
+            // ---- Recover_Channel.m:32-35: MyPhaseLift((meas/2e5).^2*1e10, beams)/sqrt(1e10)*2e5
+            ace_phaselift_cfg pcfg;
+            ace_phaselift_cfg_default(&pcfg);
+            std::vector<double> bq(M);
+            for (int r = 0; r < M; ++r) bq[r] = (B[r] / 2e5) * (B[r] / 2e5) * 1e10;
+            rc = ace_phaselift_solve_host(&pcfg, 1, M, n, A.data(), bq.data(), X.data(), nullptr, nullptr);
+            if (rc) return rc;
+            for (int k = 0; k < 2 * n; ++k) X[k] = X[k] / std::sqrt(1e10) * 2e5;
+        } else {
+        // ---- Recover_Channel -> ADMM_v2(..., 4): the pipeline with its own train partitions
         {
             const int r = std::min(std::min(cfg.r, M), n);
             const int mt = (int)std::floor(M * cfg.cc_frac);
@@ -175,6 +188,7 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
                                          &q, nullptr, nullptr);
         }
         if (rc) return rc;
+        }
         // ---- :170-178 H_out = X / rss_fct, NaN -> 0, amplitude and angle
         for (int k = 0; k < n; ++k) {
             std::complex<double> h(X[2 * k] / kRssFct, X[2 * k + 1] / kRssFct);

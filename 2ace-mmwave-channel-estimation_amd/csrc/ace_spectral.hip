@@ -30,7 +30,8 @@
 namespace ace {
 
 namespace {
-constexpr int SPEC_CHUNK = 256;   // realisations per launch (C = 0.9 MiB each at m_t = 243)
+constexpr int SPEC_CHUNK = 256;
+constexpr double kOrtol = 1e-5;   // cluster separation, relative to ||T|| (see trieig_kernel)   // realisations per launch (C = 0.9 MiB each at m_t = 243)
 
 // per-realisation scratch layout (units: doubles)
 struct SpecLayout {
@@ -197,9 +198,12 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
-// LU of LAPACK dgttrf/dgttrs, three solves, one thread per eigenvalue cluster (relative
-// separation < 1e-3 ||T||, LAPACK dstein's ORTOL) with the cluster's earlier vectors
-// projected out after every solve (as dstein).  Writes z[k][mt], lam[k], misc = {k, sum(lam - tau)}.
+// LU of LAPACK dgttrf/dgttrs, three solves, one thread per eigenvalue cluster with the
+// cluster's earlier vectors projected out after every solve (as dstein).  Clusters are runs of
+// eigenvalues closer than kOrtol ||T||.  LAPACK's dstein uses 1e-3; on PhaseLift's prox inputs
+// that chains up to ~100 eigenvalues into one sequential cluster, while at 1e-5 the largest
+// cluster has two members.  Inverse-iteration vectors of eigenvalues separated by more than
+// kOrtol ||T|| are orthogonal to ~eps / kOrtol (2e-11) without projection.  Writes z[k][mt], lam[k], misc = {k, sum(lam - tau)}.
 __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p, double* scratch, SpecLayout lay,
                                                      int* status, int status_off, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         int nc = 0;
         double sum = 0.0;
         for (int q = 0; q < k; ++q) {
-            if (q == 0 || lam[q - 1] - lam[q] >= 1e-3 * tn) cl[nc++] = q;
+            if (q == 0 || lam[q - 1] - lam[q] >= kOrtol * tn) cl[nc++] = q;
             sum += lam[q] - tau;
         }
         cl[nc] = k;

@@ -187,9 +187,10 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
                              const double* b, double* sig, int32_t* iters, uint32_t* status);
 
 /* ---- driver-level boundary (MATLAB Engine calls of main/main.py:308, :427-437) ------------
- *   [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution>(
+ *   [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution|phaselift>(
  *                         tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id)
- *   main/channel_recovery_ADMM_v2_simulation_A2only.m:9-179 (A2nuclear, multiresolution alike).
+ *   main/channel_recovery_ADMM_v2_simulation_A2only.m:9-179 (A2nuclear, multiresolution, phaselift
+ *   alike; phaselift runs MyPhaseLift per sweep point, Recover_Channel.m:32-35).
  * cb_amp / cb_angle: HOST [P][n] row-major f64 (codebook row p = beam p; MATLAB callers pass
  * the transpose of their P x n arrays), rss_dbm: [P] (dBm).  M_list = NULL selects the
  * reference sweep round(linspace(2, sqrt(4*tx*rx), 8)).^2 (:106-118).  Outputs H_amp, H_angle:
@@ -202,7 +203,7 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
 #define ACE_DRIVER_A2ONLY 0     /* channel_recovery_ADMM_v2_simulation_A2only.m */
 #define ACE_DRIVER_A2NUCLEAR 1  /* channel_recovery_ADMM_v2_simulation_A2nuclear.m */
 #define ACE_DRIVER_MULTIRES 2   /* channel_recovery_ADMM_v2_simulation_multiresolution.m */
-#define ACE_DRIVER_PHASELIFT 3  /* channel_recovery_ADMM_v2_simulation_phaselift.m (not implemented) */
+#define ACE_DRIVER_PHASELIFT 3  /* channel_recovery_ADMM_v2_simulation_phaselift.m (MyPhaseLift, rng(4096)) */
 int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
                        const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list,
                        double* H_amp, double* H_angle);

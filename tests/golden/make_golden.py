@@ -108,6 +108,22 @@ def reference_codebook_slice():
     print("reference codebook", cb.shape, digest[:16])
 
 
+def tfocs_tracels_kat():
+    """TFOCS's own known answer for solver_TraceLS (examples/smallscale/test_TraceLS.m):
+    the sampled entries, b, lambda and the CVX solution X_reference (data only)."""
+    mat = pathlib.Path("/root/reference/main/3rd_software_component/sparsepr/third/TFOCS/examples/smallscale/"
+                       "reference_solutions/traceLS_problem1_noisy.mat")
+    if not mat.exists():
+        print("TFOCS reference solutions not present; keeping existing fixture")
+        return
+    import scipy.io as sio
+    d = sio.loadmat(str(mat))           # plain MATLAB v5 numeric arrays
+    np.savez_compressed(HERE / "tfocs_traceLS_problem1.npz", omega=d["omega"].ravel().astype(np.int64),
+                        b=d["b"].ravel(), lam=float(d["lambda"].ravel()[0]), X_reference=d["X_reference"],
+                        obj_reference=float(d["obj_reference"].ravel()[0]))
+    print("TFOCS traceLS_problem1 KAT", d["X_reference"].shape)
+
+
 def main():
     # config 1 (SURVEY §8): 16-ant, 64 RSS meas -- single-restart inferLowRankV4 and the
     # 3-restart inferLowRankV4_multi / 1-restart inferLowRank_Nuclear
@@ -123,6 +139,7 @@ def main():
     np.savez_compressed(HERE / "synth_pin.npz", codes=synth.codebook_codes(58659179, 8, 16),
                         normals=synth.normal_pairs(58659179, 3, 4), vecH=synth.channel(58659179, 0, 4, 4))
     reference_codebook_slice()
+    tfocs_tracels_kat()
 
 
 if __name__ == "__main__":

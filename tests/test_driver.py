@@ -59,8 +59,10 @@ def test_driver_argument_errors_need_no_gpu():
         eng.channel_recovery_ADMM_v2_simulation_multiresolution(16, 16, amp, ang, rss, 1, nargout=2)
     with pytest.raises(engine.MatlabExecutionError, match="shapes"):
         eng.channel_recovery_ADMM_v2_simulation_A2only(16, 16, amp[:, :10], ang, rss, 1, nargout=2)
-    with pytest.raises(AceError, match="PhaseLift"):
+    with pytest.raises(engine.MatlabExecutionError, match="M = "):
         eng.channel_recovery_ADMM_v2_simulation_phaselift(16, 16, amp, ang, rss, 1, nargout=2)
+    with pytest.raises(AceError, match="unknown driver"):
+        engine.recover(7, 16, 16, amp, ang, rss, 1)
     with pytest.raises(engine.MatlabExecutionError, match="nargout"):
         eng.channel_recovery_ADMM_v2_simulation_A2only(16, 16, amp, ang, rss, 1, nargout=1)
 

@@ -102,3 +102,18 @@ def test_driver_nuclear_runs(gpu):
     amp, ang, rss = _trace(400, 16)
     Ha, Hp = engine.recover(engine.DRIVER_A2NUCLEAR, 16, 16, amp, ang, rss, 3, M_list=[121])
     assert Ha.shape == (1, 1, 256) and np.all(np.isfinite(Ha)) and np.all(np.isfinite(Hp))
+
+
+def test_driver_phaselift(gpu):
+    """channel_recovery_ADMM_v2_simulation_phaselift: rng(4096) rows, MyPhaseLift per sweep point
+    with Recover_Channel.m:34's scaling; equals the composition through phaselift_host."""
+    from ace_amd import engine, phaselift_host
+    tx = 8
+    amp, ang, rss = _trace(200, tx)
+    Ha, Hp = engine.recover(engine.DRIVER_PHASELIFT, tx, tx, amp, ang, rss, 5, M_list=[36])
+    H = np.squeeze(Ha * np.exp(1j * Hp))
+    idx = engine.randperm(4096, 0x100, 200, 36)
+    A = (amp * np.exp(1j * ang))[idx]
+    B = np.array([math.sqrt(math.pow(10.0, x / 10.0) / 1000.0) * RSS_FCT for x in rss[idx]])
+    sig = phaselift_host(A, ((B / 2e5) ** 2 * 1e10)[None]).sig[0] / math.sqrt(1e10) * 2e5
+    assert O.phase_aligned_rel_err(H, sig / RSS_FCT) <= 1e-12

@@ -180,3 +180,49 @@ def test_phase_equivariance():
     r2 = O.infer_admm(A[0], B[0], X0[0][:, None] * np.exp(0.7j), True, False, 8, 8, U=U)
     assert r1.iters == r2.iters
     assert np.allclose(r2.X, r1.X * np.exp(0.7j), atol=1e-10)
+
+
+# ---------------------------------------------------------------------------- TFOCS / PhaseLift
+def test_tfocs_tracels_known_answer():
+    """The TFOCS restatement reproduces TFOCS's own known answer for solver_TraceLS
+    (examples/smallscale/test_TraceLS.m: tol 1e-12, restart 100; pass = relative error to
+    the CVX solution below 1e-5)."""
+    import tfocs_oracle as T
+    g = np.load(GOLD / "tfocs_traceLS_problem1.npz")
+    om, b, lam, Xr = g["omega"] - 1, g["b"], float(g["lam"]), g["X_reference"]
+    N = Xr.shape[0]
+
+    def Aop(X):
+        return X.flatten(order="F")[om]
+
+    def Aadj(y):
+        Z = np.zeros(N * N)
+        Z[om] = y
+        return Z.reshape(N, N, order="F")
+
+    r = T.tfocs_at_tracels(Aop, Aadj, b, lam, np.zeros((N, N)), tol=1e-12, restart=100)
+    err = np.linalg.norm(r.x - Xr) / np.linalg.norm(Xr)
+    obj = 0.5 * np.linalg.norm(Aop(r.x) - b) ** 2 + lam * np.trace(r.x)
+    assert r.status.startswith("Step size") and err < 1e-5, (r.status, err)
+    assert abs(obj - float(g["obj_reference"])) < 1e-8
+
+
+def test_phaselift_reduction_is_exact():
+    """The GPU's reduced coordinates: with X0 = 0 every TFOCS iterate lies in
+    Q X Q^H, Q = range(Phi^H), so the d x d iteration with R = chol(Phi Phi^H) reproduces the
+    dense n x n oracle (here both in numpy)."""
+    import math
+    import tfocs_oracle as T
+    from ace_amd import synth
+    n, m = 64, 24
+    Phi = synth.codebook(5, m, n) * math.sqrt(n)
+    h = synth.channel(5, 0, 8, 8)
+    b = np.abs(Phi @ h) ** 2
+    dense = T.tfocs_at_tracels(*T.phaselift_ops(Phi), b, 0.05, np.zeros((n, n), complex), maxIts=30, tol=1e-10,
+                               restart=200)
+    R = np.linalg.cholesky(Phi @ Phi.conj().T).conj().T          # Phi^H = Q R
+    Q = Phi.conj().T @ np.linalg.inv(R)
+    red = T.tfocs_at_tracels(lambda X: np.einsum("ji,jk,ki->i", R.conj(), X, R),
+                             lambda g: (R * g[None, :]) @ R.conj().T, b, 0.05, np.zeros((m, m), complex),
+                             maxIts=30, tol=1e-10, restart=200)
+    assert np.linalg.norm(Q @ red.x @ Q.conj().T - dense.x) <= 1e-10 * np.linalg.norm(dense.x)

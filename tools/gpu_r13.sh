@@ -1,0 +1,6 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r13
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r13/pl -o run --output-format csv -- python3 bench.py --mode phaselift --batch 512 --iters 20 --steps 1 --warmup 0 --no-prof > gpurun_out/r13/pl.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r13/pipe -o run --output-format csv -- python3 bench.py --mode pipeline --batch 1024 --steps 1 --warmup 0 --no-prof > gpurun_out/r13/pipe.log 2>&1
+echo rc=$?

@@ -74,8 +74,21 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
 
     double vreg[8];
     d2 lreg[2];
+    // interior tiles (block-uniform) load without bounds checks
+    const bool full = (j0 + BJ <= nb) && (i0c + BI / 2 <= M) && (Kr % BK == 0);
     auto gload = [&](int ks) {
         const int kb = ks * BK;
+        if (full) {
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+                const d2 v = *reinterpret_cast<const d2*>(vptr + kb + e);
+                vreg[e] = v.x;
+                vreg[e + 1] = v.y;
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) lreg[e] = *reinterpret_cast<const d2*>(lptr + 2LL * ((kb >> 1) + e));
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
             const int kr = kb + vseg + e;
@@ -109,9 +122,9 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
     const int c_par = lane & 1;          // output real parity (re/im row)
     const int d_par = (lane >> 4) & 1;   // K real parity (re/im of the vector entry)
     const int sel = (c_par == d_par) ? 0 : 1;
-    double sgn;
-    if (!CONJ_L) sgn = (c_par == 0 && d_par == 1) ? -1.0 : 1.0;
-    else sgn = (c_par == 1 && d_par == 0) ? -1.0 : 1.0;
+    // sign of the expanded entry, applied as a sign-bit XOR (one VALU op)
+    const bool neg = !CONJ_L ? (c_par == 0 && d_par == 1) : (c_par == 1 && d_par == 0);
+    const long long smask = neg ? (long long)0x8000000000000000ULL : 0LL;
 
     gload(0);
     lstore(0);
@@ -131,7 +144,7 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii) {
                 const int ir = wi * 32 + ii * 16 + (lane & 15);
-                bf[ii] = sgn * ls[2 * ((ir >> 1) * LST + (kr >> 1)) + sel];
+                bf[ii] = __longlong_as_double(__double_as_longlong(ls[2 * ((ir >> 1) * LST + (kr >> 1)) + sel]) ^ smask);
             }
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)

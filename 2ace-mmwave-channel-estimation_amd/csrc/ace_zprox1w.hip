@@ -75,9 +75,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     d2* Z = reinterpret_cast<d2*>(a.Z) + (long long)b * n;
     d2* Qg = reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx;
     const bool warm = (!INIT) && a.warm;
-    auto evalE = [&](int k) -> d2 {  // X + N/mu (:424), true division as in the reference
+    const double imu = 1.0 / mu;
+    auto evalE = [&](int k) -> d2 {  // X + N/mu (:424), as N * (1/mu) like pre_kernel's V = Z - N/mu
         const d2 x = X[k], nn = N[k];
-        return make_double2(x.x + nn.x / mu, x.y + nn.y / mu);
+        return make_double2(fma(nn.x, imu, x.x), fma(nn.y, imu, x.y));
     };
     const d2 zero = make_double2(0.0, 0.0);
 #ifdef ACE_DEBUG_SWEEPS
@@ -401,10 +402,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     }  // !fast
     __syncthreads();
 
-    // per-element update + reductions: nX2, nZ2, nJN2, dZ2
+    // per-element update + reductions: nX2, nZ2, nJN2, dZ2.  Whether this iterate becomes
+    // opt_X (:344-351) depends only on the Y-step's objective, so it is decided here and X is
+    // copied in the same pass that reads it (iter_control below makes the same decision).
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const bool improved_pre = !INIT && sqrt(st->obj2) < st->opt_obj;
+    d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
     auto emit = [&](int k, d2 znew) {
         const d2 x = X[k];
+        if (improved_pre) oX[k] = x;
         if (!INIT) {
             const d2 zo = Z[k];
             const d2 d = csub(x, znew);
@@ -488,11 +494,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     if (lane == 0)
         improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
     improved = __shfl(improved, 0, 64);
-    if (improved) {
-        d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
+    if (improved) {  // opt_X was written by emit (improved == improved_pre)
         d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
         const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
-        for (int k = lane; k < n; k += 64) oX[k] = X[k];
         for (int i = lane; i < m; i += 64) oY[i] = Yn[i];
     }
 }

@@ -56,8 +56,15 @@ struct SpecLayout {
     }
 };
 
-__global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
-                                                    SpecLayout lay, const int* active) {
+// 1024 threads per realisation: the Hermitian matrix-vector product and the rank-2 update
+// split the trailing matrix's rows four ways (thread = column x row quarter), so each step
+// keeps four times as many independent memory streams in flight.
+constexpr int HT_THREADS = 1024;
+constexpr int HT_COLS = 256;                 // threads per row quarter
+constexpr int HT_RB = HT_THREADS / HT_COLS;  // row quarters
+
+__global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
+                                                           SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
     extern __shared__ double smem[];
@@ -65,6 +72,7 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
     d2* w = v + mt;                        // p, w (mt)
     double* dvs = reinterpret_cast<double*>(w + mt);
     __shared__ double red[16 * 2];
+    __shared__ d2 part[HT_RB][HT_COLS];
     __shared__ d2 s_tau, s_scal;
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
@@ -72,23 +80,25 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
     double* dd = base + lay.dd;
     double* ee = base + lay.ee;
     d2* taus = reinterpret_cast<d2*>(base + lay.tau);
+    const int col = t % HT_COLS, rb = t / HT_COLS;
 
     if (Kp) {
-    // D = diag(B_i / ||a_i||), ||a_i||^2 = K_ii  (SpectralInitialize :563-567; zero rows stay zero)
-    for (int i = t; i < mt; i += 256) {
-        const double kii = K[(long long)i * mt + i].x;
-        const double d = kii > 0.0 ? Bt[(long long)b * mt + i] / sqrt(kii) : 0.0;
-        dvs[i] = d;
-        base[lay.dv + i] = d;
-    }
-    __syncthreads();
-    // C = D (K + K^H)/2 D, exactly Hermitian (real diagonal)
-    for (long long e = t; e < (long long)mt * mt; e += 256) {
-        const int i = (int)(e / mt), j = (int)(e % mt);
-        const d2 kij = K[e], kji = K[(long long)j * mt + i];
-        const double s = dvs[i] * dvs[j];
-        C[e] = i == j ? make_double2(s * kij.x, 0.0) : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
-    }
+        // D = diag(B_i / ||a_i||), ||a_i||^2 = K_ii  (SpectralInitialize :563-567; zero rows stay zero)
+        for (int i = t; i < mt; i += HT_THREADS) {
+            const double kii = K[(long long)i * mt + i].x;
+            const double d = kii > 0.0 ? Bt[(long long)b * mt + i] / sqrt(kii) : 0.0;
+            dvs[i] = d;
+            base[lay.dv + i] = d;
+        }
+        __syncthreads();
+        // C = D (K + K^H)/2 D, exactly Hermitian (real diagonal)
+        for (long long e = t; e < (long long)mt * mt; e += HT_THREADS) {
+            const int i = (int)(e / mt), j = (int)(e % mt);
+            const d2 kij = K[e], kji = K[(long long)j * mt + i];
+            const double s = dvs[i] * dvs[j];
+            C[e] = i == j ? make_double2(s * kij.x, 0.0)
+                          : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
+        }
     }
     __syncthreads();
 
@@ -97,7 +107,7 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
         const long long r0 = (long long)(k + 1) * mt + (k + 1);   // C22 origin
         // x = C(k+1:m, k) = conj(C(k, k+1:m))
         double s1[1] = {0.0};
-        for (int i = t; i < L; i += 256) {
+        for (int i = t; i < L; i += HT_THREADS) {
             const d2 c = C[(long long)k * mt + k + 1 + i];
             v[i] = make_double2(c.x, -c.y);
             if (i > 0) s1[0] += cabs2(c);
@@ -125,52 +135,56 @@ __global__ __launch_bounds__(256) void hetrd_kernel(int mt, const double* Kp, co
         const d2 tau = s_tau;
         if (tau.x == 0.0 && tau.y == 0.0) continue;  // H = I (uniform branch)
         const d2 scal = s_scal;
-        for (int i = t; i < L; i += 256) {
+        for (int i = t; i < L; i += HT_THREADS) {
             const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
             v[i] = vi;
             C[(long long)k * mt + k + 1 + i] = vi;  // reflector k kept in row k (for the back transform)
         }
         __syncthreads();
-        // p = tau C22 v: p_i = tau sum_j conj(C22[j][i]) v_j (Hermitian; column reads are row-coalesced)
-        for (int i = t; i < L; i += 256) {
+        // p = tau C22 v: p_i = tau sum_j conj(C22[j][i]) v_j (Hermitian; column reads are row-coalesced);
+        // thread (col, rb) sums rows j = rb, rb + 4, ...
+        for (int i0 = 0; i0 < L; i0 += HT_COLS) {
+            const int i = i0 + col;
             double ar = 0.0, ai = 0.0;
-            const d2* col = C + r0 + i;
-            int j = 0;
-            for (; j + 4 <= L; j += 4) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const d2 c = col[(long long)(j + u) * mt], vj = v[j + u];
+            if (i < L) {
+                const d2* cc = C + r0 + i;
+#pragma unroll 4
+                for (int j = rb; j < L; j += HT_RB) {
+                    const d2 c = cc[(long long)j * mt], vj = v[j];
                     ar += c.x * vj.x + c.y * vj.y;
                     ai += c.x * vj.y - c.y * vj.x;
                 }
             }
-            for (; j < L; ++j) {
-                const d2 c = col[(long long)j * mt], vj = v[j];
-                ar += c.x * vj.x + c.y * vj.y;
-                ai += c.x * vj.y - c.y * vj.x;
+            part[rb][col] = make_double2(ar, ai);
+            __syncthreads();
+            if (rb == 0 && i < L) {
+                d2 acc = part[0][col];
+#pragma unroll
+                for (int q = 1; q < HT_RB; ++q) acc = cadd(acc, part[q][col]);
+                w[i] = cmul(tau, acc);
             }
-            w[i] = cmul(tau, make_double2(ar, ai));
+            __syncthreads();
         }
-        __syncthreads();
         double s2[2] = {0.0, 0.0};  // p^H v
-        for (int i = t; i < L; i += 256) {
+        for (int i = t; i < L; i += HT_THREADS) {
             const d2 q = cmulc(w[i], v[i]);
             s2[0] += q.x;
             s2[1] += q.y;
         }
         block_sum<2>(s2, red);
         const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
-        for (int i = t; i < L; i += 256) w[i] = cadd(w[i], cmul(alpha2, v[i]));
+        for (int i = t; i < L; i += HT_THREADS) w[i] = cadd(w[i], cmul(alpha2, v[i]));
         __syncthreads();
-        // C22 -= v w^H + w v^H  (thread per column j, rows i: coalesced row segments)
-        for (int j = t; j < L; j += 256) {
+        // C22 -= v w^H + w v^H  (thread (col, rb): column j, rows i = rb, rb + 4, ...)
+        for (int j = col; j < L; j += HT_COLS) {
             const d2 vj = v[j], wj = w[j];
             const d2 cvj = make_double2(vj.x, -vj.y), cwj = make_double2(wj.x, -wj.y);
-            d2* col = C + r0 + j;
-            for (int i = 0; i < L; ++i) {
-                d2 c = col[(long long)i * mt];
+            d2* cc = C + r0 + j;
+#pragma unroll 4
+            for (int i = rb; i < L; i += HT_RB) {
+                d2 c = cc[(long long)i * mt];
                 c = csub(c, cadd(cmul(v[i], cwj), cmul(w[i], cvj)));
-                col[(long long)i * mt] = c;
+                cc[(long long)i * mt] = c;
             }
         }
         __syncthreads();
@@ -359,46 +373,110 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
 }
 
 // u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),
-// W_k = D u_k.  Wave w owns vectors k = w, w + 4, ...
+// W_k = D u_k.  Vectors are processed in chunks held in LDS (the in-place updates of a
+// vector in global memory would put an L2 store->load round trip between consecutive
+// reflectors); within a chunk a 16-lane group owns one vector: segment dot products, a
+// 16-lane shuffle reduction and the update, with no barrier per reflector.
+constexpr int BX_SEG = 16;                 // lanes per vector
+constexpr int BX_REG = 16;                 // register-prefetched elements per lane (mt <= 256)
+
+__device__ __forceinline__ double seg_sum(double v) {  // sum over the 16-lane group
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void backxf_kernel(int mt, int ldw, const double* scratch, SpecLayout lay,
-                                                     double* Wout, int scale_d, const int* active) {
-    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+                                                     double* Wout, int scale_d, const int* active, int cv) {
+    const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
+    extern __shared__ double smem[];
+    d2* U = reinterpret_cast<d2*>(smem);   // [cv][mt]
     const double* base = scratch + b * lay.stride;
     const int r = (int)base[lay.misc];
     const d2* C = reinterpret_cast<const d2*>(base + lay.C);
     const d2* taus = reinterpret_cast<const d2*>(base + lay.tau);
+    const double* dv = base + lay.dv;
     d2* W = reinterpret_cast<d2*>(Wout) + (long long)b * ldw * mt;
-    for (int k = wv; k < r; k += 4) {
-        d2* u = W + (long long)k * mt;
-        const double* z = base + lay.z + (long long)k * mt;
-        for (int i = lane; i < mt; i += 64) u[i] = make_double2(z[i], 0.0);
-    }
-    for (int j = mt - 2; j >= 0; --j) {
-        const d2 tau = taus[j];
-        if (tau.x == 0.0 && tau.y == 0.0) continue;
-        const int L = mt - j - 1;
-        const d2* v = C + (long long)j * mt + j + 1;   // v[0] = 1
-        for (int k = wv; k < r; k += 4) {
-            d2* u = W + (long long)k * mt + j + 1;
-            double sr = 0.0, si = 0.0;
-            for (int i = lane; i < L; i += 64) {
-                const d2 q = cmulc(v[i], u[i]);
-                sr += q.x;
-                si += q.y;
+    const int grp = t / BX_SEG, sl = t % BX_SEG;
+    const bool owner = grp < cv;
+    for (int k0 = 0; k0 < r; k0 += cv) {
+        const int k = k0 + grp;
+        const bool mine = owner && k < r;
+        d2* u = U + (long long)grp * mt;
+        if (mine) {
+            const double* z = base + lay.z + (long long)k * mt;
+            for (int i = sl; i < mt; i += BX_SEG) u[i] = make_double2(z[i], 0.0);
+        }
+        // reflectors j = mt-2 .. 0 act on u[j+1 ..]; v_j[0] = 1 sits at C[j][j+1]
+        if (mine && mt <= BX_SEG * BX_REG) {  // reflector segments double-buffered in registers
+            d2 vc[BX_REG], vn[BX_REG];
+            auto fetch = [&](int j, d2 (&dst)[BX_REG]) {
+                const int L = mt - j - 1;
+                const d2* v = C + (long long)j * mt + j + 1;
+#pragma unroll
+                for (int p = 0; p < BX_REG; ++p) {
+                    const int i = sl + BX_SEG * p;
+                    dst[p] = i < L ? v[i] : make_double2(0.0, 0.0);
+                }
+            };
+            fetch(mt - 2, vn);
+            for (int j = mt - 2; j >= 0; --j) {
+#pragma unroll
+                for (int p = 0; p < BX_REG; ++p) vc[p] = vn[p];
+                if (j > 0) fetch(j - 1, vn);
+                const d2 tau = taus[j];
+                if (tau.x == 0.0 && tau.y == 0.0) continue;
+                const int L = mt - j - 1;
+                d2* uj = u + j + 1;
+                double sr = 0.0, si = 0.0;
+#pragma unroll
+                for (int p = 0; p < BX_REG; ++p) {
+                    const int i = sl + BX_SEG * p;
+                    if (i < L) {
+                        const d2 q = cmulc(vc[p], uj[i]);
+                        sr += q.x;
+                        si += q.y;
+                    }
+                }
+                sr = seg_sum(sr);
+                si = seg_sum(si);
+                const d2 f = cmul(tau, make_double2(sr, si));
+#pragma unroll
+                for (int p = 0; p < BX_REG; ++p) {
+                    const int i = sl + BX_SEG * p;
+                    if (i < L) uj[i] = csub(uj[i], cmul(f, vc[p]));
+                }
             }
-            sr = wave_sum(sr);
-            si = wave_sum(si);
-            const d2 f = cmul(tau, make_double2(sr, si));
-            for (int i = lane; i < L; i += 64) u[i] = csub(u[i], cmul(f, v[i]));
+        } else if (mine) {
+            for (int j = mt - 2; j >= 0; --j) {
+                const d2 tau = taus[j];
+                if (tau.x == 0.0 && tau.y == 0.0) continue;
+                const int L = mt - j - 1;
+                const d2* v = C + (long long)j * mt + j + 1;
+                d2* uj = u + j + 1;
+                double sr = 0.0, si = 0.0;
+                for (int i = sl; i < L; i += BX_SEG) {
+                    const d2 q = cmulc(v[i], uj[i]);
+                    sr += q.x;
+                    si += q.y;
+                }
+                sr = seg_sum(sr);
+                si = seg_sum(si);
+                const d2 f = cmul(tau, make_double2(sr, si));
+                for (int i = sl; i < L; i += BX_SEG) uj[i] = csub(uj[i], cmul(f, v[i]));
+            }
+        }
+        if (mine) {
+            d2* w = W + (long long)k * mt;
+            for (int i = sl; i < mt; i += BX_SEG) w[i] = scale_d ? cscale(u[i], dv[i]) : u[i];
         }
     }
-    if (!scale_d) return;
-    const double* dv = base + lay.dv;
-    for (int k = wv; k < r; k += 4) {
-        d2* u = W + (long long)k * mt;
-        for (int i = lane; i < mt; i += 64) u[i] = cscale(u[i], dv[i]);
-    }
+}
+// vectors per back-transform chunk: 16 (one per 16-lane group) within 64 KiB of LDS
+int backxf_chunk(int mt) {
+    int cv = (64 * 1024) / (16 * mt);
+    return cv < 1 ? 1 : (cv > 16 ? 16 : cv);
 }
 }  // namespace
 
@@ -415,11 +493,12 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
     if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
-        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(256), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay,
+        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay,
                            nullptr);
         hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr);
-        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), 0, st, mt, r, scratch, lay, W + 2LL * b0 * r * mt, 1,
-                           nullptr);
+        const int cv = backxf_chunk(mt);
+        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * mt * 16, st, mt, r, scratch, lay,
+                           W + 2LL * b0 * r * mt, 1, nullptr, cv);
     }
     return ACE_OK;
 }
@@ -436,9 +515,11 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     const SpecLayout lay(d, kmax);
     const size_t sm_h = (size_t)d * (16 + 16 + 8), sm_t = (size_t)d * 16;
     if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(256), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
+    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
     hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
-    hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), 0, st, d, kmax, scratch, lay, V, 0, active);
+    const int cv = backxf_chunk(d);
+    hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), (size_t)cv * d * 16, st, d, kmax, scratch, lay, V, 0,
+                       active, cv);
     return ACE_OK;
 }
 

@@ -11,6 +11,8 @@ from .pipeline import (inferLowRankV4_multi, inferLowRankV4, inferLowRank_Nuclea
                        infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, draw_partitions,
                        PipelineResult)
 from .phaselift import MyPhaseLift, phaselift_host, phaselift_batch, PhaseLiftResult  # noqa: F401
+from .beamformer import (svd_beamformer, svd_beamformer_compensation, codebook_beams,  # noqa: F401
+                         svd_beamformer_host, svd_beamformer_batch, BeamResult)
 from . import synth, engine  # noqa: F401
 
 __version__ = LIB.ace_version().decode()

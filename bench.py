@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
-    ap.add_argument("--mode", default="unit", choices=["unit", "pipeline", "phaselift"])
+    ap.add_argument("--mode", default="unit", choices=["unit", "pipeline", "phaselift", "beamformer"])
     return ap.parse_args()
 
 
@@ -181,6 +181,85 @@ def bench_phaselift(args, dev, rank, world):
     print(json.dumps(line), flush=True)
 
 
+BF_METRIC = "beamformer codebooks/sec (svd_beamformer: 2 zgesdd + 2-bit quantise + all-pairs search, 16x16)"
+
+
+def bench_beamformer(args, dev, rank, world):
+    """SURVEY.md §8f row 4 (separate metric): batched svd_beamformer on recovered 16 x 16
+    channels (main.py:32 num_ant = 16; codebook_library.py:57-96).  One unit = one H ->
+    (wr, wt) code pair.  Inputs: noisy synthetic channels (L = 3 paths + CN noise), resident
+    in HBM; --tx selects the array size (default 16 in this mode)."""
+    import torch
+    from ace_amd import svd_beamformer_batch, synth_problem
+    tx = args.tx if args.tx != 32 else 16
+    bsz = args.batch if args.batch != 4096 else 65536
+    _, _, X0, _ = synth_problem(args.seed, rank * bsz, bsz, 8, tx, tx, x0_noise=0.3, device=dev)
+    H = X0.reshape(bsz, tx, tx).contiguous()
+    res = None
+
+    def step():
+        nonlocal res
+        res = svd_beamformer_batch(H)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        return
+    st = res.status.cpu().numpy()
+    per_unit = 16.0 * tx * tx + 2 * tx + 8 + 8 + 4        # read H; write codes, idx, rss, status
+    achieved = per_unit * bsz / (kern_ms * 1e-3) / 1e9
+    line = {
+        "metric": BF_METRIC, "value": round(world * bsz * args.steps / elapsed, 1), "unit": "codebooks/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (L=3 paths + 0.3 relative CN noise)",
+        "config": {"workload": f"svd_beamformer on {tx}x{tx} recovered channels", "batch_per_gpu": bsz},
+        "status_clean": bool((st == 0).all()),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None,
+                     "kernel": "beamformer_kernel", "kernel_ms": round(kern_ms, 4),
+                     "note": "latency-bound scalar QR chains (dbdsqr); HBM bytes are the only algorithmic floor"},
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_beamformer(tx, H[: 2000].cpu().numpy())
+    print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_beamformer(tx, Hs):
+    """The oracle (numpy.linalg.svd = the reference's own dependency, all-pairs search
+    vectorised) on one host core, on a bounded sample of the same inputs."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import beamformer_oracle as BO
+    t0 = time.perf_counter()
+    k = 0
+    while k < len(Hs) and time.perf_counter() - t0 < 15.0:
+        BO.svd_beamformer(Hs[k])
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(k / dt, 1), "unit": "codebooks/s", "cores": 1, "kind": "port",
+            "sample": f"{k} of the same {tx}x{tx} channels through oracle/beamformer_oracle.svd_beamformer "
+                      f"(numpy zgesdd + vectorised search; the reference's per-pair Python loop is slower) "
+                      f"on {_cpu_model()}"}
+
+
 def unit_flops(m, n, tx, rx):
     """Algorithmic flops per kernel launch class per realisation per iteration (complex MAC = 8)."""
     return {
@@ -254,8 +333,9 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    if args.mode in ("pipeline", "phaselift"):
-        (bench_pipeline if args.mode == "pipeline" else bench_phaselift)(args, dev, rank, world)
+    if args.mode in ("pipeline", "phaselift", "beamformer"):
+        {"pipeline": bench_pipeline, "phaselift": bench_phaselift,
+         "beamformer": bench_beamformer}[args.mode](args, dev, rank, world)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

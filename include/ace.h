@@ -214,6 +214,27 @@ int ace_driver_m_sweep(int tx, int rx, int32_t* M_out);
  * 0-based, sampled order) from the build's counter RNG (seed, stream).  Host only. */
 int ace_driver_randperm(uint64_t seed, uint64_t stream, int P, int k, int32_t* out);
 
+/* ---- downstream beamformer ----------------------------------------
+ *   wr_out, wt_out = svd_beamformer(H)                       main/codebook_library.py:57-96
+ *   wr_out, wt_out = svd_beamformer_compensation(H, offset)  main/codebook_library.py:98-138
+ *   reached from codebook_generator (:192-213), H = reshape(H_est[i,:], [tx, rx]) (:197).
+ * H: [batch][tx][rx] c128 row-major (DEVICE for _batch).  offset: [batch][rx] radians
+ * (compensation * pi/2) or NULL for svd_beamformer.  Outputs: wr_code [batch][rx] and
+ * wt_code [batch][tx] (2-bit phase codes 0..3 = the characters of the reference's strings),
+ * beam_idx [batch][2] = (tx_idx, rx_idx) of the argmax pair, rss [batch] = its
+ * 10*log10(|wt^T H wr|^2 * 1000), status [batch] (ACE_ST_BF_*).  vh_r / vh_t (optional,
+ * may be NULL): [batch][n][n] c128 Vh of svd(H) and svd(H^T) in numpy's (zgesdd's) phase
+ * convention.  Square arrays only (tx == rx <= 32, as main.py:454 calls it). */
+#define ACE_ST_BF_NONFINITE 16u /* H has NaN/Inf: numpy raises LinAlgError; codes zeroed, beam_idx -1 */
+#define ACE_ST_BF_NOCONV 32u    /* dbdsqr iteration budget exhausted (numpy would raise) */
+#define ACE_ST_BF_DC 64u        /* n > 25: numpy's zgesdd uses divide and conquer; beams match up to sign */
+int ace_svd_beamformer_batch(int batch, int tx, int rx, const double* H, const double* offset,
+                             uint8_t* wr_code, uint8_t* wt_code, int32_t* beam_idx, double* rss,
+                             uint32_t* status, double* vh_r, double* vh_t, void* stream);
+int ace_svd_beamformer_host(int batch, int tx, int rx, const double* H, const double* offset,
+                            uint8_t* wr_code, uint8_t* wt_code, int32_t* beam_idx, double* rss,
+                            uint32_t* status, double* vh_r, double* vh_t);
+
 /* Synthetic traces (device).  Counter-based RNG (splitmix64 of seed/stream/counter),
  * identical integer streams to ace_amd.synth on the host.
  *   ace_synth_codebook: A[count][m][n] c128 with entries exp(j*pi/2*k)/sqrt(n),

@@ -27,19 +27,34 @@
 
 namespace ace {
 
-namespace {
-constexpr int BJ = 64;      // realisations per tile
-constexpr int BI = 64;      // output reals per tile (32 complex rows)
-constexpr int BK = 32;      // reals of K per step (16 complex)
-constexpr int VST = BK + 2; // V row stride (doubles): 34 = 2 mod 32 -> conflict-free ds_read_b64 A-fragments
-constexpr int LST = BK / 2 + 1; // L row stride (complex)
+// Tile configuration: BJ realisations x BI output reals per work-group, BK reals of K per
+// step, WJ x WI waves, each wave (BJ/WJ) x (BI/WI) reals = TJ x TI MFMA tiles.
+template <int BJ_, int BI_, int BK_, int WJ_, int WI_>
+struct GemmCfg {
+    static constexpr int BJ = BJ_, BI = BI_, BK = BK_, WJ = WJ_, WI = WI_;
+    static constexpr int NT = 64 * WJ * WI;
+    static constexpr int TJ = BJ / WJ / 16, TI = BI / WI / 16;
+    static constexpr int VST = BK + 2;      // V row stride (doubles): = 2 mod 32 -> conflict-free A-fragments
+    static constexpr int LST = BK / 2 + 1;  // L row stride (complex)
+    static constexpr int PV = BJ * (BK / 2) / NT;        // V complex pairs staged per thread per step
+    static constexpr int PL = (BI / 2) * (BK / 2) / NT;  // L complex entries staged per thread per step
+    static_assert(TJ >= 1 && TI >= 1 && BJ % (16 * WJ) == 0 && BI % (16 * WI) == 0, "wave tile");
+    static_assert(PV >= 1 && PL >= 1 && BJ * (BK / 2) % NT == 0 && (BI / 2) * (BK / 2) % NT == 0, "staging");
+    static_assert(BK % 4 == 0, "K step");
+    static constexpr size_t lds_bytes() { return 2 * (size_t)BJ * VST * 8 + 2 * (size_t)(BI / 2) * LST * 16; }
+};
+using GemmDefault = GemmCfg<64, 64, 32, 2, 2>;
 
-template <int MODE, bool CONJ_L>
-__global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const double* __restrict__ L, int ldl,
-                                                    long long strideL, const double* __restrict__ V, int ldv,
-                                                    long long strideV, double* __restrict__ C,
-                                                    const double* __restrict__ E, int ldc, long long strideC,
-                                                    int tilesI, int tilesJ) {
+namespace {
+
+template <int MODE, bool CONJ_L, class CF>
+__global__ __launch_bounds__(CF::NT) void zgemm_kernel(int M, int K, int nb, const double* __restrict__ L, int ldl,
+                                                       long long strideL, const double* __restrict__ V, int ldv,
+                                                       long long strideV, double* __restrict__ C,
+                                                       const double* __restrict__ E, int ldc, long long strideC,
+                                                       int tilesI, int tilesJ) {
+    constexpr int BJ = CF::BJ, BI = CF::BI, BK = CF::BK, NT = CF::NT, TJ = CF::TJ, TI = CF::TI;
+    constexpr int VST = CF::VST, LST = CF::LST, PV = CF::PV, PL = CF::PL;
     __shared__ double Vs[2][BJ * VST];
     __shared__ d2 Ls[2][(BI / 2) * LST];
 
@@ -60,63 +75,54 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
     const int j0 = tj * BJ;         // first realisation
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wj = w >> 1, wi = w & 1;
-
-    // global -> register staging indices
-    const int vj = t >> 2, vseg = (t & 3) * 8;      // V: realisation vj, reals vseg..vseg+7 of the K-step
-    const int lr = t >> 3, lkc = (t & 7) * 2;       // L: complex row lr, complex cols lkc, lkc+1
-    const int Kr = 2 * K;                           // reals of K
+    const int wj = w / CF::WI, wi = w % CF::WI;
+    const int Kr = 2 * K;  // reals of K
     const int ksteps = (Kr + BK - 1) / BK;
-    const bool vrow_ok = (j0 + vj) < nb;
-    const bool lrow_ok = (i0c + lr) < M;
-    const double* vptr = V + 2LL * (long long)(j0 + vj) * ldv + vseg;
-    const double* lptr = L + 2LL * ((long long)(i0c + lr) * ldl + lkc);
 
-    double vreg[8];
-    d2 lreg[2];
+    double vreg[PV][2];
+    d2 lreg[PL];
     // interior tiles (block-uniform) load without bounds checks
     const bool full = (j0 + BJ <= nb) && (i0c + BI / 2 <= M) && (Kr % BK == 0);
     auto gload = [&](int ks) {
         const int kb = ks * BK;
-        if (full) {
 #pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                const d2 v = *reinterpret_cast<const d2*>(vptr + kb + e);
-                vreg[e] = v.x;
-                vreg[e + 1] = v.y;
-            }
-#pragma unroll
-            for (int e = 0; e < 2; ++e) lreg[e] = *reinterpret_cast<const d2*>(lptr + 2LL * ((kb >> 1) + e));
-            return;
+        for (int u = 0; u < PV; ++u) {
+            const int p = t + NT * u, vj = p / (BK / 2), vs = 2 * (p % (BK / 2));
+            d2 v = make_double2(0.0, 0.0);
+            if (full || ((j0 + vj) < nb && kb + vs < Kr))
+                v = *reinterpret_cast<const d2*>(V + 2LL * (long long)(j0 + vj) * ldv + kb + vs);
+            vreg[u][0] = v.x;
+            vreg[u][1] = v.y;
         }
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-            const int kr = kb + vseg + e;
+        for (int u = 0; u < PL; ++u) {
+            const int p = t + NT * u, lr = p / (BK / 2), lc = p % (BK / 2);
+            const int kc = (kb >> 1) + lc;
             d2 v = make_double2(0.0, 0.0);
-            if (vrow_ok && kr < Kr) v = *reinterpret_cast<const d2*>(vptr + kb + e);
-            vreg[e] = v.x;
-            vreg[e + 1] = v.y;
-        }
-        const int kc = (kb >> 1) + lkc;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            d2 v = make_double2(0.0, 0.0);
-            if (lrow_ok && kc + e < K) v = *reinterpret_cast<const d2*>(lptr + 2LL * ((kb >> 1) + e));
-            lreg[e] = v;
+            if (full || ((i0c + lr) < M && kc < K))
+                v = *reinterpret_cast<const d2*>(L + 2LL * ((long long)(i0c + lr) * ldl + kc));
+            lreg[u] = v;
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) Vs[buf][vj * VST + vseg + e] = vreg[e];
-        Ls[buf][lr * LST + lkc] = lreg[0];
-        Ls[buf][lr * LST + lkc + 1] = lreg[1];
+        for (int u = 0; u < PV; ++u) {
+            const int p = t + NT * u, vj = p / (BK / 2), vs = 2 * (p % (BK / 2));
+            Vs[buf][vj * VST + vs] = vreg[u][0];
+            Vs[buf][vj * VST + vs + 1] = vreg[u][1];
+        }
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            const int p = t + NT * u, lr = p / (BK / 2), lc = p % (BK / 2);
+            Ls[buf][lr * LST + lc] = lreg[u];
+        }
     };
 
-    d4v acc[2][2];
+    d4v acc[TJ][TI];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TJ; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4v{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < TI; ++b) acc[a][b] = d4v{0.0, 0.0, 0.0, 0.0};
 
     // per-lane constants of the on-the-fly complex -> 2x2 real expansion
     const int c_par = lane & 1;          // output real parity (re/im row)
@@ -138,34 +144,34 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
 #pragma unroll
         for (int kk = 0; kk < BK / 4; ++kk) {
             const int kr = kk * 4 + (lane >> 4);
-            double af[2], bf[2];
+            double af[TJ], bf[TI];
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) af[jj] = vs[(wj * 32 + jj * 16 + (lane & 15)) * VST + kr];
+            for (int jj = 0; jj < TJ; ++jj) af[jj] = vs[(wj * (BJ / CF::WJ) + jj * 16 + (lane & 15)) * VST + kr];
 #pragma unroll
-            for (int ii = 0; ii < 2; ++ii) {
-                const int ir = wi * 32 + ii * 16 + (lane & 15);
+            for (int ii = 0; ii < TI; ++ii) {
+                const int ir = wi * (BI / CF::WI) + ii * 16 + (lane & 15);
                 bf[ii] = __longlong_as_double(__double_as_longlong(ls[2 * ((ir >> 1) * LST + (kr >> 1)) + sel]) ^ smask);
             }
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
+            for (int jj = 0; jj < TJ; ++jj)
 #pragma unroll
-                for (int ii = 0; ii < 2; ++ii)
+                for (int ii = 0; ii < TI; ++ii)
                     acc[jj][ii] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[jj], bf[ii], acc[jj][ii], 0, 0, 0);
         }
         if (ks + 1 < ksteps) lstore(buf ^ 1);
         __syncthreads();
     }
 
-    // epilogue: lane l, reg r -> realisation j0 + wj*32 + jj*16 + (l>>4) + 4r, real i0' + wi*32 + ii*16 + (l&15)
+    // epilogue: lane l, reg r -> realisation j0 + wj*(BJ/WJ) + jj*16 + (l>>4) + 4r, real i0' + wi*(BI/WI) + ii*16 + (l&15)
     const int Mr = 2 * M;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int jj = 0; jj < TJ; ++jj)
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
+        for (int ii = 0; ii < TI; ++ii)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int j = j0 + wj * 32 + jj * 16 + (lane >> 4) + 4 * r;
-                const int ir = 2 * i0c + wi * 32 + ii * 16 + (lane & 15);
+                const int j = j0 + wj * (BJ / CF::WJ) + jj * 16 + (lane >> 4) + 4 * r;
+                const int ir = 2 * i0c + wi * (BI / CF::WI) + ii * 16 + (lane & 15);
                 if (j < nb && ir < Mr) {
                     const long long off = 2LL * (long long)j * ldc + ir;
                     double v = acc[jj][ii][r];
@@ -177,14 +183,172 @@ __global__ __launch_bounds__(256) void zgemm_kernel(int M, int K, int nb, const 
 }
 }  // namespace
 
-void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
-                  const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
-                  long long strideC, int nz, hipStream_t st) {
-    const int tilesI = (M + BI / 2 - 1) / (BI / 2);
-    const int tilesJ = (nb + BJ - 1) / BJ;
-    dim3 grid(tilesI * tilesJ, 1, nz), block(256);
-#define ACE_GEMM_LAUNCH(MD, CJ)                                                                              \
-    hipLaunchKernelGGL((zgemm_kernel<MD, CJ>), grid, block, 0, st, M, K, nb, L, ldl, strideL, V, ldv, strideV, \
+// ---- 3M variant (Gauss): (Vr + iVi)(Lr + iLi) from three real products
+//   P1 = Vr Lr,  P2 = Vi Li,  P3 = (Vr + Vi)(Lr + Li);   Re = P1 - P2,  Im = P3 - P1 - P2
+// (Li -> -Li for a conjugated L).  6 real flops per complex MAC instead of 8: three f64
+// MFMAs per 16x16 complex block and 4 complex K instead of four.  The operands are read from
+// LDS as whole complex numbers (one 16-byte read per fragment) and the two sums are formed in
+// registers.  Tile: BJ realisations x BC complex outputs, BKC complex K per step, WJ x WI waves.
+template <int BJ_, int BC_, int BKC_, int WJ_, int WI_>
+struct Gemm3mCfg {
+    static constexpr int BJ = BJ_, BC = BC_, BKC = BKC_, WJ = WJ_, WI = WI_;
+    static constexpr int NT = 64 * WJ * WI;
+    static constexpr int TJ = BJ / WJ / 16, TC = BC / WI / 16;
+    static constexpr int VST = BKC + 1, LST = BKC + 1;  // complex row strides (odd)
+    static constexpr int PV = BJ * BKC / NT, PL = BC * BKC / NT;
+    static_assert(TJ >= 1 && TC >= 1 && BJ % (16 * WJ) == 0 && BC % (16 * WI) == 0, "wave tile");
+    static_assert(PV >= 1 && PL >= 1 && BJ * BKC % NT == 0 && BC * BKC % NT == 0, "staging");
+    static_assert(BKC % 4 == 0, "K step");
+    static constexpr size_t lds_bytes() { return 2 * (size_t)(BJ * VST + BC * LST) * 16; }
+};
+
+namespace {
+
+template <int MODE, bool CONJ_L, class CF>
+__global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, const double* __restrict__ L, int ldl,
+                                                         long long strideL, const double* __restrict__ V, int ldv,
+                                                         long long strideV, double* __restrict__ C,
+                                                         const double* __restrict__ E, int ldc, long long strideC,
+                                                         int tilesI, int tilesJ) {
+    constexpr int BJ = CF::BJ, BC = CF::BC, BKC = CF::BKC, NT = CF::NT, TJ = CF::TJ, TC = CF::TC;
+    constexpr int VST = CF::VST, LST = CF::LST, PV = CF::PV, PL = CF::PL;
+    __shared__ d2 Vs[2][BJ * VST];
+    __shared__ d2 Ls[2][BC * LST];
+
+    const int z = blockIdx.z;
+    L += 2 * strideL * z;
+    V += 2 * strideV * z;
+    C += 2 * strideC * z;
+    if (MODE != 0) E += 2 * strideC * z;
+
+    const int nblk = tilesI * tilesJ;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, local = bid >> 3;
+    const int q = nblk >> 3, rr = nblk & 7;
+    const int nid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + local;
+    const int ti = nid % tilesI, tj = nid / tilesI;
+    const int i0 = ti * BC;  // first complex output
+    const int j0 = tj * BJ;  // first realisation
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wj = w / CF::WI, wi = w % CF::WI;
+    const int ksteps = (K + BKC - 1) / BKC;
+
+    d2 vreg[PV], lreg[PL];
+    const bool full = (j0 + BJ <= nb) && (i0 + BC <= M) && (K % BKC == 0);
+    auto gload = [&](int ks) {
+        const int kb = ks * BKC;
+#pragma unroll
+        for (int u = 0; u < PV; ++u) {
+            const int p = t + NT * u, vj = p / BKC, vc = p % BKC;
+            d2 v = make_double2(0.0, 0.0);
+            if (full || ((j0 + vj) < nb && kb + vc < K))
+                v = *reinterpret_cast<const d2*>(V + 2LL * ((long long)(j0 + vj) * ldv + kb + vc));
+            vreg[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            const int p = t + NT * u, lr = p / BKC, lc = p % BKC;
+            d2 v = make_double2(0.0, 0.0);
+            if (full || ((i0 + lr) < M && kb + lc < K))
+                v = *reinterpret_cast<const d2*>(L + 2LL * ((long long)(i0 + lr) * ldl + kb + lc));
+            lreg[u] = v;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < PV; ++u) {
+            const int p = t + NT * u;
+            Vs[buf][(p / BKC) * VST + p % BKC] = vreg[u];
+        }
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            const int p = t + NT * u;
+            Ls[buf][(p / BKC) * LST + p % BKC] = lreg[u];
+        }
+    };
+
+    d4v p1[TJ][TC], p2[TJ][TC], p3[TJ][TC];
+#pragma unroll
+    for (int a = 0; a < TJ; ++a)
+#pragma unroll
+        for (int b = 0; b < TC; ++b) p1[a][b] = p2[a][b] = p3[a][b] = d4v{0.0, 0.0, 0.0, 0.0};
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+
+    for (int ks = 0; ks < ksteps; ++ks) {
+        const int buf = ks & 1;
+        if (ks + 1 < ksteps) gload(ks + 1);
+        const d2* vs = Vs[buf];
+        const d2* ls = Ls[buf];
+#pragma unroll
+        for (int kk = 0; kk < BKC / 4; ++kk) {
+            const int k = kk * 4 + (lane >> 4);
+            double ar[TJ], ai[TJ], as[TJ], br[TC], bi[TC], bs[TC];
+#pragma unroll
+            for (int jj = 0; jj < TJ; ++jj) {
+                const d2 v = vs[(wj * (BJ / CF::WJ) + jj * 16 + (lane & 15)) * VST + k];
+                ar[jj] = v.x;
+                ai[jj] = v.y;
+                as[jj] = v.x + v.y;
+            }
+#pragma unroll
+            for (int cc = 0; cc < TC; ++cc) {
+                const d2 l = ls[(wi * (BC / CF::WI) + cc * 16 + (lane & 15)) * LST + k];
+                br[cc] = l.x;
+                bi[cc] = CONJ_L ? -l.y : l.y;
+                bs[cc] = l.x + bi[cc];
+            }
+#pragma unroll
+            for (int jj = 0; jj < TJ; ++jj)
+#pragma unroll
+                for (int cc = 0; cc < TC; ++cc) {
+                    p1[jj][cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[jj], br[cc], p1[jj][cc], 0, 0, 0);
+                    p2[jj][cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[jj], bi[cc], p2[jj][cc], 0, 0, 0);
+                    p3[jj][cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[jj], bs[cc], p3[jj][cc], 0, 0, 0);
+                }
+        }
+        if (ks + 1 < ksteps) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane l, reg r -> realisation j0 + wj*(BJ/WJ) + jj*16 + (l>>4) + 4r, output i0 + wi*(BC/WI) + cc*16 + (l&15)
+#pragma unroll
+    for (int jj = 0; jj < TJ; ++jj)
+#pragma unroll
+        for (int cc = 0; cc < TC; ++cc)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int j = j0 + wj * (BJ / CF::WJ) + jj * 16 + (lane >> 4) + 4 * r;
+                const int i = i0 + wi * (BC / CF::WI) + cc * 16 + (lane & 15);
+                if (j < nb && i < M) {
+                    const long long off = 2LL * ((long long)j * ldc + i);
+                    const double a = p1[jj][cc][r], b = p2[jj][cc][r];
+                    d2 v = make_double2(a - b, p3[jj][cc][r] - a - b);
+                    if (MODE == 1) {
+                        const d2 e = *reinterpret_cast<const d2*>(E + off);
+                        v = make_double2(e.x - v.x, e.y - v.y);
+                    } else if (MODE == 2) {
+                        const d2 e = *reinterpret_cast<const d2*>(E + off);
+                        v = make_double2(e.x + v.x, e.y + v.y);
+                    }
+                    *reinterpret_cast<d2*>(C + off) = v;
+                }
+            }
+}
+}  // namespace
+
+template <class CF>
+void launch_zgemm3m_cfg(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
+                        const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
+                        long long strideC, int nz, hipStream_t st) {
+    const int tilesI = (M + CF::BC - 1) / CF::BC;
+    const int tilesJ = (nb + CF::BJ - 1) / CF::BJ;
+    dim3 grid(tilesI * tilesJ, 1, nz), block(CF::NT);
+#define ACE_GEMM_LAUNCH(MD, CJ)                                                                                    \
+    hipLaunchKernelGGL((zgemm3m_kernel<MD, CJ, CF>), grid, block, 0, st, M, K, nb, L, ldl, strideL, V, ldv, strideV, \
                        C, E, ldc, strideC, tilesI, tilesJ)
     if (conj_l) {
         if (mode == 0) ACE_GEMM_LAUNCH(0, true);
@@ -196,6 +360,44 @@ void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, 
         else ACE_GEMM_LAUNCH(2, false);
     }
 #undef ACE_GEMM_LAUNCH
+}
+
+// Launch one GEMM with tile configuration CF (also used by tools/probe_gemm.hip).
+template <class CF>
+void launch_zgemm_cfg(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
+                      const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
+                      long long strideC, int nz, hipStream_t st) {
+    const int tilesI = (M + CF::BI / 2 - 1) / (CF::BI / 2);
+    const int tilesJ = (nb + CF::BJ - 1) / CF::BJ;
+    dim3 grid(tilesI * tilesJ, 1, nz), block(CF::NT);
+#define ACE_GEMM_LAUNCH(MD, CJ)                                                                                  \
+    hipLaunchKernelGGL((zgemm_kernel<MD, CJ, CF>), grid, block, 0, st, M, K, nb, L, ldl, strideL, V, ldv, strideV, \
+                       C, E, ldc, strideC, tilesI, tilesJ)
+    if (conj_l) {
+        if (mode == 0) ACE_GEMM_LAUNCH(0, true);
+        else if (mode == 1) ACE_GEMM_LAUNCH(1, true);
+        else ACE_GEMM_LAUNCH(2, true);
+    } else {
+        if (mode == 0) ACE_GEMM_LAUNCH(0, false);
+        else if (mode == 1) ACE_GEMM_LAUNCH(1, false);
+        else ACE_GEMM_LAUNCH(2, false);
+    }
+#undef ACE_GEMM_LAUNCH
+}
+
+void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
+                  const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
+                  long long strideC, int nz, hipStream_t st) {
+    // 3M kernel (measured on MI355X, tools/probe_gemm.hip, unit shapes: apply_A 196 -> 135 us, apply_AH
+    // 194 -> 135 us, G/K 52.6 -> 38.4 us against the 4M GemmDefault).  8 waves per work-group; the
+    // 64 x 32 output tile when the 64 x 64 one would leave fewer than 512 work-groups.
+    using Big = Gemm3mCfg<64, 64, 16, 2, 4>;
+    using Small = Gemm3mCfg<64, 32, 16, 4, 2>;
+    const long long big_blocks = (long long)((M + 63) / 64) * ((nb + 63) / 64) * nz;
+    if (big_blocks >= 256 && M >= 64)
+        launch_zgemm3m_cfg<Big>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
+    else
+        launch_zgemm3m_cfg<Small>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
 }
 
 }  // namespace ace

@@ -70,7 +70,9 @@ def test_nuclear_short_horizon(gpu, tx, m, a_shared):
     A, B, X0, _ = _problem(9, 4, m, tx, a_shared)
     res = infer_admm_host(A, B, X0, tx, tx, variant="A2nuclear", maxiter=60, fixed_iters=True)
     Xo, _, _, _, _ = _oracle(A, B, X0, tx, variant=1, maxiter=60, fixed_iters=True)
-    assert _errs(res.X, Xo).max() <= 1e-9
+    # the oracle against ITSELF with B or X0 perturbed by 1e-15 moves by up to 9e-10 here
+    # (16-ant, 60 iterations); the bar sits one decade above that noise floor
+    assert _errs(res.X, Xo).max() <= 1e-8
 
 
 def test_warm_and_cold_eig_agree(gpu):

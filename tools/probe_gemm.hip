@@ -1,0 +1,115 @@
+// Probe: tile configurations of the complex f64 GEMM (csrc/ace_gemm.hip) on the unit
+// bench's shapes (batch 4096, m = 256, n = 1024).  Diagnostic only; prints avg us and TF/s
+// per (shape, config) and the max deviation from the default configuration.
+#include "../2ace-mmwave-channel-estimation_amd/csrc/ace_gemm.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+#include <random>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+using namespace ace;
+
+struct Shape { const char* name; int mode; bool conj; int M, K, nb; };
+
+static double* dev_rand(size_t ndoubles, unsigned seed) {
+    std::vector<double> h(ndoubles);
+    std::mt19937_64 g(seed);
+    std::uniform_real_distribution<double> u(-1.0, 1.0);
+    for (auto& x : h) x = u(g);
+    double* d;
+    CK(hipMalloc(&d, ndoubles * 8));
+    CK(hipMemcpy(d, h.data(), ndoubles * 8, hipMemcpyHostToDevice));
+    return d;
+}
+
+template <class CF, bool M3 = false>
+static void run(const char* cname, const Shape& s, const double* L, const double* V, const double* E, double* C,
+                const std::vector<double>& ref, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto go = [&]() {
+        if constexpr (M3) launch_zgemm3m_cfg<CF>(s.mode, s.conj, s.M, s.K, s.nb, L, s.K, 0, V, s.K, 0, C, E, s.M, 0, 1, nullptr);
+        else launch_zgemm_cfg<CF>(s.mode, s.conj, s.M, s.K, s.nb, L, s.K, 0, V, s.K, 0, C, E, s.M, 0, 1, nullptr);
+    };
+    for (int i = 0; i < 3; ++i) go();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < reps; ++i) go();
+    CK(hipEventRecord(b, nullptr));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const double us = 1e3 * ms / reps;
+    const double tf = 8.0 * s.M * (double)s.K * s.nb / (us * 1e-6) / 1e12;
+    std::vector<double> h(2 * (size_t)s.nb * s.M);
+    CK(hipMemcpy(h.data(), C, h.size() * 8, hipMemcpyDeviceToHost));
+    double dmax = 0, rmax = 0;
+    if (!ref.empty())
+        for (size_t i = 0; i < h.size(); ++i) { dmax = fmax(dmax, fabs(h[i] - ref[i])); rmax = fmax(rmax, fabs(ref[i])); }
+    printf("%-6s %-26s %9.1f us %6.2f TF/s  lds %6zu  dev %.2e\n", s.name, cname, us, tf, CF::lds_bytes(),
+           ref.empty() ? 0.0 : dmax / rmax);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
+#define CFGS(X)                                   \
+    X(GemmCfg<64, 64, 32, 2, 2>)                  \
+    X(GemmCfg<64, 64, 32, 2, 4>)                  \
+    X(GemmCfg<64, 128, 32, 2, 4>)
+
+#define CFGS3(X)                                  \
+    X(Gemm3mCfg<64, 32, 16, 2, 2>)                \
+    X(Gemm3mCfg<64, 64, 16, 2, 4>)                \
+    X(Gemm3mCfg<64, 32, 16, 4, 2>)                \
+    X(Gemm3mCfg<64, 64, 16, 2, 2>)                \
+    X(Gemm3mCfg<32, 64, 16, 2, 2>)                \
+    X(Gemm3mCfg<64, 32, 8, 2, 2>)                 \
+    X(Gemm3mCfg<128, 32, 16, 4, 2>)               \
+    X(Gemm3mCfg<64, 64, 16, 4, 4>)
+
+#define CFGS_OLD(X)                               \
+    X(GemmCfg<64, 64, 32, 2, 2>)                  \
+    X(GemmCfg<64, 64, 32, 2, 4>)                  \
+    X(GemmCfg<64, 64, 32, 4, 2>)                  \
+    X(GemmCfg<128, 64, 32, 4, 2>)                 \
+    X(GemmCfg<64, 128, 32, 2, 4>)                 \
+    X(GemmCfg<32, 64, 32, 2, 2>)                  \
+    X(GemmCfg<64, 32, 32, 2, 2>)                  \
+    X(GemmCfg<128, 64, 32, 2, 2>)                 \
+    X(GemmCfg<64, 128, 32, 2, 2>)                 \
+    X(GemmCfg<64, 64, 16, 2, 2>)                  \
+    X(GemmCfg<32, 64, 32, 1, 2>)                  \
+    X(GemmCfg<64, 32, 32, 2, 1>)
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    const Shape shapes[] = {{"A", 1, false, 256, 1024, 4096}, {"G", 0, false, 256, 256, 4096},
+                            {"AH", 2, false, 1024, 256, 4096}, {"Kcj", 0, true, 256, 1024, 256}};
+    for (const Shape& s : shapes) {
+        const double* L = dev_rand(2 * (size_t)s.M * s.K, 1);
+        const double* V = dev_rand(2 * (size_t)s.nb * s.K, 2);
+        const double* E = dev_rand(2 * (size_t)s.nb * s.M, 3);
+        double* C;
+        CK(hipMalloc(&C, 2 * (size_t)s.nb * s.M * 8));
+        std::vector<double> ref;
+        launch_zgemm_cfg<GemmDefault>(s.mode, s.conj, s.M, s.K, s.nb, L, s.K, 0, V, s.K, 0, C, E, s.M, 0, 1, nullptr);
+        CK(hipDeviceSynchronize());
+        ref.resize(2 * (size_t)s.nb * s.M);
+        CK(hipMemcpy(ref.data(), C, ref.size() * 8, hipMemcpyDeviceToHost));
+#define RUN(...) run<__VA_ARGS__>(#__VA_ARGS__ + 8, s, L, V, E, C, ref, reps);
+        CFGS(RUN)
+#undef RUN
+#define RUN(...) run<__VA_ARGS__, true>(#__VA_ARGS__ + 10, s, L, V, E, C, ref, reps);
+        CFGS3(RUN)
+#undef RUN
+        CK(hipFree((void*)L));
+        CK(hipFree((void*)V));
+        CK(hipFree((void*)E));
+        CK(hipFree(C));
+    }
+    return 0;
+}

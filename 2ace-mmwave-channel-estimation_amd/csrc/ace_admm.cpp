@@ -16,6 +16,8 @@
 //   finalize opt_X / opt_Y (:384-385)
 #include "ace_host.hpp"
 
+#include <utility>
+
 namespace ace {
 
 size_t linops_bytes(bool shared, int batch, int m, int n) {
@@ -33,6 +35,45 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->AH = shared ? cv.take(cz * n * m) : nullptr;
     L->K = cv.take(cz * mats * m * m);
     L->G = cv.take(cz * mats * m * m);
+    L->ns = shared ? cv.take(cz * 4 * m * m) : nullptr;
+}
+
+// G = (I + K)^{-1} of the shared K by Newton-Schulz on the matrix cores:
+//   X0 = 2/(1 + b) I  with b >= lambda_max(I + K) (Gershgorin) and lambda_min(I + K) >= 1,
+//   R_k = I - (I + K) X_k,   X_{k+1} = X_k + X_k R_k      (||R_{k+1}|| = ||R_k||^2).
+// Every X_k is a polynomial in I + K, hence Hermitian and commuting with it, which lets both
+// products run as the GEMM's  C = E -/+ V L^H  form.  The iteration stops one step after
+// max|R_k| < 1e-10 (the next step's error is ~1e-20, i.e. converged to rounding).  A single
+// Gauss-Jordan work-group on one CU took 5.2 ms for m = 256; this takes a few dozen small GEMMs.
+int ns_inverse(LinOps& L, hipStream_t st) {
+    const int m = L.m;
+    const long long mm = (long long)m * m;
+    double* Ap = L.ns;            // I + K
+    double* Id = L.ns + 2 * mm;   // I
+    double* R = L.ns + 4 * mm;
+    double* Xn = L.ns + 6 * mm;
+    double* X = L.G;
+    launch_ns_prep(m, L.K, Ap, Id, X, st);
+    double* flag = nullptr;
+    ACE_HIP(hipMallocAsync((void**)&flag, sizeof(double), st));
+    int it = 0;
+    bool done = false;
+    for (; it < 60 && !done; ++it) {
+        launch_zgemm(1, true, m, m, m, X, m, 0, Ap, m, 0, R, Id, m, 0, 1, st);   // R = I - (I+K) X
+        if (it >= 5) {
+            double h = 0.0;
+            launch_max_abs(2 * mm, R, flag, st);
+            ACE_HIP(hipMemcpyAsync(&h, flag, sizeof(double), hipMemcpyDeviceToHost, st));
+            ACE_HIP(hipStreamSynchronize(st));
+            done = h < 1e-10;
+        }
+        launch_zgemm(2, true, m, m, m, R, m, 0, X, m, 0, Xn, X, m, 0, 1, st);    // X' = X + X R
+        std::swap(X, Xn);
+    }
+    ACE_HIP(hipFreeAsync(flag, st));
+    if (!done) return fail(ACE_ERR_UNSUPPORTED, "setup: Newton-Schulz inverse of I + K did not converge");
+    if (X != L.G) ACE_HIP(hipMemcpyAsync(L.G, X, sizeof(double) * 2 * mm, hipMemcpyDeviceToDevice, st));
+    return ACE_OK;
 }
 
 int linops_setup(LinOps& L, int batch, hipStream_t st) {
@@ -42,8 +83,12 @@ int linops_setup(LinOps& L, int batch, hipStream_t st) {
     ProfScope ps(ACE_K_SETUP, st);
     // K[j][i] = sum_k conj(A[i][k]) A[j][k]  : GEMM with L = conj(A), V = rows of A
     launch_zgemm(0, true, m, n, m, L.A, n, mn, L.A, n, mn, L.K, nullptr, m, mm, mats, st);
-    ACE_HIP(hipMemcpyAsync(L.G, L.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
-    launch_inv_ipk(m, mats, L.G, mm, st);
+    if (L.shared) {
+        ACE_TRY(ns_inverse(L, st));
+    } else {  // one Gauss-Jordan work-group per realisation's matrix (parallel over the batch)
+        ACE_HIP(hipMemcpyAsync(L.G, L.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
+        launch_inv_ipk(m, mats, L.G, mm, st);
+    }
     if (L.shared) launch_conj_transpose(m, n, L.A, L.AH, st);
     ACE_HIP(hipGetLastError());
     return ACE_OK;

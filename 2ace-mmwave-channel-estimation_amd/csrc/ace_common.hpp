@@ -72,6 +72,10 @@ void launch_zgemv_cols(int mode, int M, int K, int nb, const double* L, long lon
 
 // (I + K)^{-1} in place for `count` m x m HPD matrices (Gauss-Jordan, no pivoting).
 void launch_inv_ipk(int m, int count, double* G, long long strideG, hipStream_t st);
+// Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
+void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
+// out[0] = max |x_i| over n doubles
+void launch_max_abs(long long n, const double* x, double* out, hipStream_t st);
 
 // Arguments of the Z-step kernel (ace_zprox.hip).
 struct ZArgs {

@@ -141,7 +141,57 @@ __global__ __launch_bounds__(1024) void inv_ipk_kernel(int m, double* __restrict
         __syncthreads();
     }
 }
+__global__ __launch_bounds__(1024) void ns_prep_kernel(int m, const d2* __restrict__ K, d2* __restrict__ Ap,
+                                                       d2* __restrict__ Id, d2* __restrict__ X0) {
+    __shared__ double part[1024];
+    double b = 0.0;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {  // Gershgorin row sums of I + K
+        double rs = 0.0;
+        for (int j = 0; j < m; ++j) {
+            d2 v = K[(long long)i * m + j];
+            if (i == j) v.x += 1.0;
+            rs += sqrt(v.x * v.x + v.y * v.y);
+        }
+        b = fmax(b, rs);
+    }
+    part[threadIdx.x] = b;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) part[threadIdx.x] = fmax(part[threadIdx.x], part[threadIdx.x + s]);
+        __syncthreads();
+    }
+    const double alpha = 2.0 / (1.0 + part[0]);
+    for (long long e = threadIdx.x; e < (long long)m * m; e += blockDim.x) {
+        const bool diag = (e / m) == (e % m);
+        d2 v = K[e];
+        if (diag) v.x += 1.0;
+        Ap[e] = v;
+        Id[e] = make_double2(diag ? 1.0 : 0.0, 0.0);
+        X0[e] = make_double2(diag ? alpha : 0.0, 0.0);
+    }
+}
+
+__global__ __launch_bounds__(1024) void max_abs_kernel(long long n, const double* __restrict__ x, double* out) {
+    __shared__ double part[1024];
+    double v = 0.0;
+    for (long long i = threadIdx.x; i < n; i += blockDim.x) v = fmax(v, fabs(x[i]));
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) part[threadIdx.x] = fmax(part[threadIdx.x], part[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = part[0];
+}
 }  // namespace
+
+void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st) {
+    hipLaunchKernelGGL(ns_prep_kernel, dim3(1), dim3(1024), 0, st, m, (const d2*)K, (d2*)Ap, (d2*)Id, (d2*)X0);
+}
+
+void launch_max_abs(long long n, const double* x, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(max_abs_kernel, dim3(1), dim3(1024), 0, st, n, x, out);
+}
 
 void launch_zgemv_rows(int mode, int M, int K, int nb, const double* L, long long strideL, const double* V,
                        int ldv, double* C, const double* E, int ldc, hipStream_t st) {

@@ -107,6 +107,7 @@ struct LinOps {
     double* AH;
     double* K;
     double* G;
+    double* ns;  // shared regime: Newton-Schulz scratch (4 m x m: I + K, I, R, X'), else null
 };
 size_t linops_bytes(bool shared, int batch, int m, int n);
 void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L);

@@ -83,18 +83,49 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     const d2 zero = make_double2(0.0, 0.0);
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long dbg_t1 = dbg_t0, dbg_t2 = dbg_t0, dbg_t3 = dbg_t0;
+    unsigned long long dbg_t1 = dbg_t0, dbg_t2 = dbg_t0, dbg_t3 = dbg_t0, dbg_fa = 0, dbg_fb = 0, dbg_fc = 0;
     int sweeps = -1;
 #else
     int sweeps = 0;
 #endif
 
-    // ---- E = reshape(X + N/mu, tx, []) (:424-426), zero padded to 32x32
-    for (int e = lane; e < ZT * ZT; e += 64) {
-        const int i = e & 31, j = e >> 5;
-        T0[i * ZHS + j] = (i < tx && j < rx) ? evalE(i + tx * j) : zero;
+    // Qprev operand fragments of the warm product F = Qprev^H E, fetched first so that their
+    // latency overlaps the E loads: qv[I][s] = Qprev[4s + (lane>>4)][16I + (lane&15)] (identity padded)
+    d2 qv[2][8];
+    if (warm) {
+#pragma unroll
+        for (int I = 0; I < 2; ++I)
+#pragma unroll
+            for (int s8 = 0; s8 < 8; ++s8) {
+                const int i = 4 * s8 + (lane >> 4), k = 16 * I + (lane & 15);
+                qv[I][s8] = (i < tx && k < tx) ? Qg[i * tx + k] : make_double2(i == k ? 1.0 : 0.0, 0.0);
+            }
+    }
+    // ---- E = reshape(X + N/mu, tx, []) (:424-426), zero padded to 32x32.  Loads are issued
+    // in chunks of 8 per lane ahead of the LDS stores (memory-level parallelism).
+#pragma unroll
+    for (int e0 = 0; e0 < ZT * ZT; e0 += 64 * 8) {
+        d2 xv[8], nv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
+            xv[u] = nv[u] = zero;
+            if (i < tx && j < rx) {
+                xv[u] = X[i + tx * j];
+                nv[u] = N[i + tx * j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
+            T0[i * ZHS + j] = (i < tx && j < rx) ? make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y))
+                                                 : zero;
+        }
     }
     __syncthreads();
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_fa = __builtin_amdgcn_s_memrealtime();
+#endif
     // Qprev with identity padding
     auto qprev = [&](int i, int k) -> d2 {
         if (i < tx && k < tx) return Qg[i * tx + k];
@@ -106,8 +137,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         for (int I = 0; I < 2; ++I)
 #pragma unroll
             for (int J = 0; J < 2; ++J)
-                mm16([&](int r, int k) { const d2 q = qprev(k, 16 * I + r); return make_double2(q.x, -q.y); },
-                     [&](int, int k, int c) { return T0[k * ZHS + 16 * J + c]; }, cr[I][J], ci[I][J], lane);
+            {
+                cr[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
+                ci[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8) {
+                    const d2 q = qv[I][s8];
+                    mfma_c(make_double2(q.x, -q.y), T0[(4 * s8 + (lane >> 4)) * ZHS + 16 * J + (lane & 15)], cr[I][J],
+                           ci[I][J]);
+                }
+            }
         __syncthreads();
 #pragma unroll
         for (int I = 0; I < 2; ++I)
@@ -119,6 +158,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
                         make_double2(cr[I][J][r], ci[I][J][r]);
         __syncthreads();
     }
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_fb = __builtin_amdgcn_s_memrealtime();
+#endif
     // ---- Spectral certificate.  The tail rescaling (:469-480) fires only when some
     // profile entry has  sum(top-r eigenvalues) < f * trace.  By Ky Fan, the sum of the r
     // largest diagonal entries of Qprev^H H Qprev (= squared row norms of F) is a lower
@@ -157,6 +199,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     }
     __syncthreads();
     const bool fast = flag_fast;
+#ifdef ACE_DEBUG_SWEEPS
+    dbg_fc = __builtin_amdgcn_s_memrealtime();
+#endif
     if (lane == 0) flag_any = 0;
     if (!fast) {
     // H = F F^H (:428), upper blocks (0,0), (0,1), (1,1) -> packed buffer 0
@@ -408,13 +453,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     const bool improved_pre = !INIT && sqrt(st->obj2) < st->opt_obj;
     d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
-    auto emit = [&](int k, d2 znew) {
-        const d2 x = X[k];
+    // emit_v: element k with its X, N, Z_old already loaded
+    auto emit_v = [&](int k, d2 x, d2 nn, d2 zo, d2 znew) {
         if (improved_pre) oX[k] = x;
         if (!INIT) {
-            const d2 zo = Z[k];
             const d2 d = csub(x, znew);
-            N[k] = cadd(N[k], cscale(d, mu));
+            N[k] = cadd(nn, cscale(d, mu));
             acc[0] += cabs2(x);
             acc[1] += cabs2(znew);
             acc[2] += cabs2(d);
@@ -422,6 +466,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         }
         Z[k] = znew;
     };
+    auto emit = [&](int k, d2 znew) { emit_v(k, X[k], INIT ? zero : N[k], INIT ? zero : Z[k], znew); };
     if (flag_any) {
         // per column block J of E: T(:, J) = diag(sqrt(scl)) Qnew^H E(:, J) (rows = eigen indices),
         // then Z^T(J, :) = T(:, J)^T Qnew^T with A = T^T straight from the accumulators and
@@ -464,13 +509,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
             }
         }
     } else {
-        for (int k = lane; k < n; k += 64) emit(k, evalE(k));
+        // Z = E: all loads of a chunk are issued before any of its stores (the stores to N, Z and
+        // opt_X would otherwise serialise every element behind a full memory round trip)
+        constexpr int CH = 8;
+        for (int k0 = 0; k0 < n; k0 += 64 * CH) {
+            d2 xv[CH], nv[CH], zv[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int k = k0 + lane + 64 * u;
+                xv[u] = nv[u] = zv[u] = zero;
+                if (k < n) {
+                    xv[u] = X[k];
+                    nv[u] = N[k];
+                    if (!INIT) zv[u] = Z[k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int k = k0 + lane + 64 * u;
+                if (k < n)
+                    emit_v(k, xv[u], nv[u], zv[u], make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y)));
+            }
+        }
     }
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t4 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && (b == 0 || b == 2000) && (a.it < 4 || a.it % 20 == 0))
+    if (lane == 0 && (b == 0 || b == 2000) && (a.it < 30 || a.it % 20 == 0))
         printf("1w b %d it %d sweeps %d pre %llu jac %llu order+Q %llu emit %llu (x10ns)\n", b, a.it, sweeps,
                dbg_t1 - dbg_t0, dbg_t2 - dbg_t1, dbg_t3 - dbg_t2, dbg_t4 - dbg_t3);
+    if (lane == 0 && (b == 0 || b == 2000) && (a.it % 20 == 0))
+        printf("1w b %d it %d fast: E %llu F %llu cert %llu rest %llu\n", b, a.it, dbg_fa - dbg_t0, dbg_fb - dbg_fa,
+               dbg_fc - dbg_fb, dbg_t4 - dbg_fc);
 #endif
     if (INIT) return;
 
@@ -499,6 +568,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
         for (int i = lane; i < m; i += 64) oY[i] = Yn[i];
     }
+#ifdef ACE_DEBUG_SWEEPS
+    if (lane == 0 && a.it == 100) {
+        const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        printf("wave %d %llu %llu %u\n", b, dbg_t0, te, hw);
+    }
+#endif
 }
 }  // namespace
 

@@ -57,18 +57,16 @@ static void run(const char* cname, const Shape& s, const double* L, const double
 }
 
 #define CFGS(X)                                   \
-    X(GemmCfg<64, 64, 32, 2, 2>)                  \
-    X(GemmCfg<64, 64, 32, 2, 4>)                  \
-    X(GemmCfg<64, 128, 32, 2, 4>)
+    X(GemmCfg<64, 64, 32, 2, 2>)
 
 #define CFGS3(X)                                  \
-    X(Gemm3mCfg<64, 32, 16, 2, 2>)                \
     X(Gemm3mCfg<64, 64, 16, 2, 4>)                \
-    X(Gemm3mCfg<64, 32, 16, 4, 2>)                \
-    X(Gemm3mCfg<64, 64, 16, 2, 2>)                \
-    X(Gemm3mCfg<32, 64, 16, 2, 2>)                \
-    X(Gemm3mCfg<64, 32, 8, 2, 2>)                 \
-    X(Gemm3mCfg<128, 32, 16, 4, 2>)               \
+    X(Gemm3mCfg<128, 64, 16, 4, 2>)               \
+    X(Gemm3mCfg<64, 128, 16, 2, 4>)               \
+    X(Gemm3mCfg<64, 64, 16, 1, 4>)                \
+    X(Gemm3mCfg<64, 64, 32, 2, 4>)                \
+    X(Gemm3mCfg<64, 64, 8, 2, 4>)                 \
+    X(Gemm3mCfg<32, 64, 16, 2, 4>)                \
     X(Gemm3mCfg<64, 64, 16, 4, 4>)
 
 #define CFGS_OLD(X)                               \

@@ -122,6 +122,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const int nv = batch * r;                         // vectors per apply
     const long long mm = (long long)m * m, mn = (long long)m * n;
     const bool fast = (r == 1);                       // r = 1 kernels (ystep, one-wave zstep)
+    const bool fused = fast && L.shared;              // pre_kernel folded into the shared-A GEMMs
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -174,16 +175,25 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     int q = 0;
     const int poll = 8;
     for (int it = 1; it <= p.maxiter; ++it) {
-        { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
-        { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }          // T = S - A V
+        if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
+            ProfScope ps(ACE_K_APPLY_A, st);
+            launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
+        } else {
+            { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
+            { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }      // T = S - A V
+        }
         { ProfScope ps(ACE_K_APPLY_G, st); applyMM(L.G, w.T, w.g); }            // g = G T
         {
             ProfScope ps(ACE_K_YSTEP, st);
-            if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+            if (fast) launch_ystep(m, batch, fused ? nullptr : w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
             else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
         }
         { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
-        { ProfScope ps(ACE_K_APPLY_AH, st); applyAH(w.g, w.X, w.V); }           // X = V + A^H g
+        {
+            ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
+            if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
+            else applyAH(w.g, w.X, w.V);
+        }
         za.it = it;
         za.Ynew = w.Y[1 - q];
         za.Yold = w.Y[q];

@@ -72,6 +72,10 @@ void launch_zgemv_cols(int mode, int M, int K, int nb, const double* L, long lon
 
 // (I + K)^{-1} in place for `count` m x m HPD matrices (Gauss-Jordan, no pivoting).
 void launch_inv_ipk(int m, int count, double* G, long long strideG, hipStream_t st);
+struct RealState;
+void launch_zgemm_fused(bool fv, int M, int K, int nb, const double* L, int ldl, const double* V, const double* V2,
+                        int ldv, double* C, const double* E, const double* E2, int ldc, const RealState* rs,
+                        hipStream_t st);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
 // out[0] = max |x_i| over n doubles

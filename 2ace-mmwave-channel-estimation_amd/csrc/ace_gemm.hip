@@ -204,12 +204,17 @@ struct Gemm3mCfg {
 
 namespace {
 
-template <int MODE, bool CONJ_L, class CF>
+// FV: the V operand is formed while staging as V - V2 / mu_j (pre_kernel's V = Z - N/mu);
+// FE: the epilogue operand is E - E2 / mu_j (S = Y - M/mu, or V = Z - N/mu), and rows of
+// realisations already marked done are left untouched (as the unfused path leaves them).
+// mu_j and done come from the per-realisation RealState array rs.
+template <int MODE, bool CONJ_L, class CF, bool FV = false, bool FE = false>
 __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, const double* __restrict__ L, int ldl,
                                                          long long strideL, const double* __restrict__ V, int ldv,
                                                          long long strideV, double* __restrict__ C,
                                                          const double* __restrict__ E, int ldc, long long strideC,
-                                                         int tilesI, int tilesJ) {
+                                                         int tilesI, int tilesJ, const double* __restrict__ V2,
+                                                         const double* __restrict__ E2, const RealState* __restrict__ rs) {
     constexpr int BJ = CF::BJ, BC = CF::BC, BKC = CF::BKC, NT = CF::NT, TJ = CF::TJ, TC = CF::TC;
     constexpr int VST = CF::VST, LST = CF::LST, PV = CF::PV, PL = CF::PL;
     __shared__ d2 Vs[2][BJ * VST];
@@ -235,16 +240,28 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
     const int ksteps = (K + BKC - 1) / BKC;
 
     d2 vreg[PV], lreg[PL];
+    d2 v2reg[FV ? PV : 1];
+    double vimu[FV ? PV : 1];
+    if constexpr (FV) {
+#pragma unroll
+        for (int u = 0; u < PV; ++u) {
+            const int j = j0 + (t + NT * u) / BKC;
+            vimu[u] = j < nb ? 1.0 / rs[j].mu : 0.0;
+        }
+    }
     const bool full = (j0 + BJ <= nb) && (i0 + BC <= M) && (K % BKC == 0);
     auto gload = [&](int ks) {
         const int kb = ks * BKC;
 #pragma unroll
         for (int u = 0; u < PV; ++u) {
             const int p = t + NT * u, vj = p / BKC, vc = p % BKC;
-            d2 v = make_double2(0.0, 0.0);
-            if (full || ((j0 + vj) < nb && kb + vc < K))
+            d2 v = make_double2(0.0, 0.0), v2 = v;
+            if (full || ((j0 + vj) < nb && kb + vc < K)) {
                 v = *reinterpret_cast<const d2*>(V + 2LL * ((long long)(j0 + vj) * ldv + kb + vc));
+                if constexpr (FV) v2 = *reinterpret_cast<const d2*>(V2 + 2LL * ((long long)(j0 + vj) * ldv + kb + vc));
+            }
             vreg[u] = v;
+            if constexpr (FV) v2reg[u] = v2;
         }
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
@@ -259,7 +276,9 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
 #pragma unroll
         for (int u = 0; u < PV; ++u) {
             const int p = t + NT * u;
-            Vs[buf][(p / BKC) * VST + p % BKC] = vreg[u];
+            d2 v = vreg[u];
+            if constexpr (FV) v = csub(v, cscale(v2reg[u], vimu[u]));
+            Vs[buf][(p / BKC) * VST + p % BKC] = v;
         }
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
@@ -324,15 +343,16 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
                 const int j = j0 + wj * (BJ / CF::WJ) + jj * 16 + (lane >> 4) + 4 * r;
                 const int i = i0 + wi * (BC / CF::WI) + cc * 16 + (lane & 15);
                 if (j < nb && i < M) {
+                    if constexpr (FE) {
+                        if (rs[j].done) continue;
+                    }
                     const long long off = 2LL * ((long long)j * ldc + i);
                     const double a = p1[jj][cc][r], b = p2[jj][cc][r];
                     d2 v = make_double2(a - b, p3[jj][cc][r] - a - b);
-                    if (MODE == 1) {
-                        const d2 e = *reinterpret_cast<const d2*>(E + off);
-                        v = make_double2(e.x - v.x, e.y - v.y);
-                    } else if (MODE == 2) {
-                        const d2 e = *reinterpret_cast<const d2*>(E + off);
-                        v = make_double2(e.x + v.x, e.y + v.y);
+                    if (MODE != 0) {
+                        d2 e = *reinterpret_cast<const d2*>(E + off);
+                        if constexpr (FE) e = csub(e, cscale(*reinterpret_cast<const d2*>(E2 + off), 1.0 / rs[j].mu));
+                        v = MODE == 1 ? make_double2(e.x - v.x, e.y - v.y) : make_double2(e.x + v.x, e.y + v.y);
                     }
                     *reinterpret_cast<d2*>(C + off) = v;
                 }
@@ -349,7 +369,7 @@ void launch_zgemm3m_cfg(int mode, bool conj_l, int M, int K, int nb, const doubl
     dim3 grid(tilesI * tilesJ, 1, nz), block(CF::NT);
 #define ACE_GEMM_LAUNCH(MD, CJ)                                                                                    \
     hipLaunchKernelGGL((zgemm3m_kernel<MD, CJ, CF>), grid, block, 0, st, M, K, nb, L, ldl, strideL, V, ldv, strideV, \
-                       C, E, ldc, strideC, tilesI, tilesJ)
+                       C, E, ldc, strideC, tilesI, tilesJ, nullptr, nullptr, nullptr)
     if (conj_l) {
         if (mode == 0) ACE_GEMM_LAUNCH(0, true);
         else if (mode == 1) ACE_GEMM_LAUNCH(1, true);
@@ -398,6 +418,24 @@ void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, 
         launch_zgemm3m_cfg<Big>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
     else
         launch_zgemm3m_cfg<Small>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
+}
+
+// Shared-A products of the r = 1 iteration with pre_kernel folded in (Big tile configuration):
+//   apply_A  (fv):  C = (E - E2/mu) - A (V - V2/mu)       T = S - A V  with S = Y - M/mu, V = Z - N/mu
+//   apply_AH (!fv): C = (E - E2/mu) + A^H V               X = V + A^H g with V = Z - N/mu
+void launch_zgemm_fused(bool fv, int M, int K, int nb, const double* L, int ldl, const double* V, const double* V2,
+                        int ldv, double* C, const double* E, const double* E2, int ldc, const RealState* rs,
+                        hipStream_t st) {
+    using CF = Gemm3mCfg<64, 64, 16, 2, 4>;
+    const int tilesI = (M + CF::BC - 1) / CF::BC;
+    const int tilesJ = (nb + CF::BJ - 1) / CF::BJ;
+    dim3 grid(tilesI * tilesJ, 1, 1), block(CF::NT);
+    if (fv)
+        hipLaunchKernelGGL((zgemm3m_kernel<1, false, CF, true, true>), grid, block, 0, st, M, K, nb, L, ldl, 0LL, V,
+                           ldv, 0LL, C, E, ldc, 0LL, tilesI, tilesJ, V2, E2, rs);
+    else
+        hipLaunchKernelGGL((zgemm3m_kernel<2, false, CF, false, true>), grid, block, 0, st, M, K, nb, L, ldl, 0LL, V,
+                           ldv, 0LL, C, E, ldc, 0LL, tilesI, tilesJ, V2, E2, rs);
 }
 
 }  // namespace ace

@@ -316,8 +316,10 @@ __global__ __launch_bounds__(256) void ystep_kernel(int m, const double* Sp, con
     d2* Yn = reinterpret_cast<d2*>(Ynew) + (long long)b * m;
     double v[5] = {0, 0, 0, 0, 0};  // obj2, nAX2, nY2, nJM2, dY2
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        const d2 ax = csub(S[i], g[i]);
         const d2 mi = M[i];
+        // S == null: S = Y - M/mu is formed here (pre_kernel folded into the GEMMs)
+        const d2 si = Sp ? S[i] : csub(Yo[i], cscale(mi, imu));
+        const d2 ax = csub(si, g[i]);
         d2 c = cadd(ax, cscale(mi, imu));
         double d = sqrt(cabs2(c));
         if (d == 0.0) {  // ArgMinY zero guard (:516-520 / :524-528)

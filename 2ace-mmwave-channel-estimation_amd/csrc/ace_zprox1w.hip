@@ -90,19 +90,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
 #endif
 
     // Qprev operand fragments of the warm product F = Qprev^H E, fetched first so that their
-    // latency overlaps the E loads: qv[I][s] = Qprev[4s + (lane>>4)][16I + (lane&15)] (identity padded)
+    // latency overlaps the E loads: qv[I][s] = Qprev[4s + (lane>>4)][16I + (lane&15)] (identity
+    // padded).  Qprev's columns are stored in descending eigenvalue order (below), so when every
+    // profile rank is <= 16 the certificate needs only F's first 16 rows (I = 0); the second
+    // half is fetched only if the certificate fails.
+    int maxr = 0;
+    for (int pi = 0; pi < pf.np; ++pi) maxr = max(maxr, pf.rl[pi]);
+    const bool top16 = warm && maxr <= 16;
     d2 qv[2][8];
+    auto load_q = [&](int I) {
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+            const int i = 4 * s8 + (lane >> 4), k = 16 * I + (lane & 15);
+            qv[I][s8] = (i < tx && k < tx) ? Qg[i * tx + k] : make_double2(i == k ? 1.0 : 0.0, 0.0);
+        }
+    };
     if (warm) {
-#pragma unroll
-        for (int I = 0; I < 2; ++I)
-#pragma unroll
-            for (int s8 = 0; s8 < 8; ++s8) {
-                const int i = 4 * s8 + (lane >> 4), k = 16 * I + (lane & 15);
-                qv[I][s8] = (i < tx && k < tx) ? Qg[i * tx + k] : make_double2(i == k ? 1.0 : 0.0, 0.0);
-            }
+        load_q(0);
+        if (!top16) load_q(1);
     }
     // ---- E = reshape(X + N/mu, tx, []) (:424-426), zero padded to 32x32.  Loads are issued
     // in chunks of 8 per lane ahead of the LDS stores (memory-level parallelism).
+    double etr = 0.0;  // ||E||_F^2 = trace(E E^H)
 #pragma unroll
     for (int e0 = 0; e0 < ZT * ZT; e0 += 64 * 8) {
         d2 xv[8], nv[8];
@@ -118,8 +127,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
-            T0[i * ZHS + j] = (i < tx && j < rx) ? make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y))
-                                                 : zero;
+            const d2 ev = (i < tx && j < rx) ? make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y)) : zero;
+            etr += cabs2(ev);
+            T0[i * ZHS + j] = ev;
         }
     }
     __syncthreads();
@@ -132,21 +142,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         return make_double2(i == k ? 1.0 : 0.0, 0.0);
     };
     d4v cr[2][2], ci[2][2];
-    if (warm) {  // F = Qprev^H E -> T0
+    auto warm_half = [&](int I) {  // rows 16I..16I+15 of F = Qprev^H E (T0 = E)
 #pragma unroll
-        for (int I = 0; I < 2; ++I)
+        for (int J = 0; J < 2; ++J) {
+            cr[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
+            ci[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int J = 0; J < 2; ++J)
-            {
-                cr[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
-                ci[I][J] = d4v{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s8 = 0; s8 < 8; ++s8) {
-                    const d2 q = qv[I][s8];
-                    mfma_c(make_double2(q.x, -q.y), T0[(4 * s8 + (lane >> 4)) * ZHS + 16 * J + (lane & 15)], cr[I][J],
-                           ci[I][J]);
-                }
+            for (int s8 = 0; s8 < 8; ++s8) {
+                const d2 q = qv[I][s8];
+                mfma_c(make_double2(q.x, -q.y), T0[(4 * s8 + (lane >> 4)) * ZHS + 16 * J + (lane & 15)], cr[I][J],
+                       ci[I][J]);
             }
+        }
+    };
+    auto store_f = [&]() {  // T0 = F (after every wave has finished reading E)
         __syncthreads();
 #pragma unroll
         for (int I = 0; I < 2; ++I)
@@ -157,45 +166,102 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
                     T0[(16 * I + (lane >> 4) + 4 * r) * ZHS + 16 * J + (lane & 15)] =
                         make_double2(cr[I][J][r], ci[I][J][r]);
         __syncthreads();
+    };
+    if (warm) {
+        warm_half(0);
+        if (!top16) warm_half(1);
     }
 #ifdef ACE_DEBUG_SWEEPS
     dbg_fb = __builtin_amdgcn_s_memrealtime();
 #endif
     // ---- Spectral certificate.  The tail rescaling (:469-480) fires only when some
     // profile entry has  sum(top-r eigenvalues) < f * trace.  By Ky Fan, the sum of the r
-    // largest diagonal entries of Qprev^H H Qprev (= squared row norms of F) is a lower
-    // bound on sum(top-r eigenvalues) for any unitary Qprev, and the diagonal sums to the
-    // trace.  When every entry clears its threshold by a relative margin far above the
-    // rounding of the reference's eig, no rescaling happens there either and Z = E
-    // exactly: the eigendecomposition is skipped (Q keeps its warm start).
-    if (!INIT) {
-        if (lane < ZT) {
-            double d = 0.0;
-            for (int j = 0; j < ZT; ++j) d += cabs2(T0[lane * ZHS + j]);
-            wv[lane] = d;
-        }
-        __syncthreads();
-        if (lane < ZT) {
-            const double dk = wv[lane];
-            int rank = 0;
-            for (int j = 0; j < ZT; ++j) rank += (wv[j] > dk) || (wv[j] == dk && j < lane);
-            rs2[rank] = dk;
-        }
-        __syncthreads();
-        if (lane == 0) {
+    // largest diagonal entries of Q^H H Q (= squared row norms of F = Q^H E) is a lower bound
+    // on sum(top-r eigenvalues) for any Q with orthonormal columns, and trace(H) = ||E||_F^2.
+    // When every entry clears its threshold by a relative margin far above the rounding of
+    // the reference's eig, no rescaling happens there either and Z = E exactly: the
+    // eigendecomposition is skipped (Q keeps its warm start).
+    bool fast_reg = false;
+    if (!INIT && top16) {
+        // row norms of F's first 16 rows straight from the accumulators: lane l holds rows
+        // (l>>4) + 4r, columns l&15 (+16J); reduce over the 16 column lanes
+        double rn[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
             double v = 0.0;
-            for (int k = 0; k < ZT; ++k) v += rs2[k];
-            int ok = v > 0.0;
-            for (int pi = 0; pi < pf.np; ++pi) {
-                double vr = 0.0;
-                for (int k = 0; k < pf.rl[pi]; ++k) vr += rs2[k];
-                ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
-            }
-            flag_fast = ok;
+#pragma unroll
+            for (int J = 0; J < 2; ++J) v += cr[0][J][r] * cr[0][J][r] + ci[0][J][r] * ci[0][J][r];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+            rn[r] = v;
         }
+        // lane L (of each 16-lane group) takes row L = (L&3) + 4(L>>2)
+        const int L16 = lane & 15;
+        double t0 = __shfl(rn[0], 16 * (L16 & 3), 64), t1 = __shfl(rn[1], 16 * (L16 & 3), 64);
+        double t2 = __shfl(rn[2], 16 * (L16 & 3), 64), t3 = __shfl(rn[3], 16 * (L16 & 3), 64);
+        const int rsel = L16 >> 2;
+        double val = rsel == 0 ? t0 : (rsel == 1 ? t1 : (rsel == 2 ? t2 : t3));
+        // bitonic sort, descending, within the 16-lane group
+#pragma unroll
+        for (int k = 2; k <= 16; k <<= 1)
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const double o = __shfl_xor(val, j, 64);
+                const bool asc = (L16 & k) == 0;
+                const bool keep_max = ((L16 & j) == 0) == asc;
+                val = keep_max ? fmax(val, o) : fmin(val, o);
+            }
+        // inclusive prefix sums of the sorted norms
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const double u = __shfl_up(val, o, 16);
+            if (L16 >= o) val += u;
+        }
+        const double v = wave_sum(etr);
+        bool ok = v > 0.0;
+        for (int pi = 0; pi < pf.np; ++pi) {
+            const double vr = __shfl(val, pf.rl[pi] - 1, 64);
+            ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
+        }
+        fast_reg = ok;
+        if (!fast_reg) {  // the eigendecomposition needs all of F
+            load_q(1);
+            warm_half(1);
+            store_f();
+        }
+        if (lane == 0) flag_fast = fast_reg;
         __syncthreads();
-    } else if (lane == 0) {
-        flag_fast = 0;
+    } else {
+        if (warm) store_f();
+        if (!INIT) {
+            if (lane < ZT) {
+                double d = 0.0;
+                for (int j = 0; j < ZT; ++j) d += cabs2(T0[lane * ZHS + j]);
+                wv[lane] = d;
+            }
+            __syncthreads();
+            if (lane < ZT) {
+                const double dk = wv[lane];
+                int rank = 0;
+                for (int j = 0; j < ZT; ++j) rank += (wv[j] > dk) || (wv[j] == dk && j < lane);
+                rs2[rank] = dk;
+            }
+            __syncthreads();
+            if (lane == 0) {
+                double v = 0.0;
+                for (int k = 0; k < ZT; ++k) v += rs2[k];
+                int ok = v > 0.0;
+                for (int pi = 0; pi < pf.np; ++pi) {
+                    double vr = 0.0;
+                    for (int k = 0; k < pf.rl[pi]; ++k) vr += rs2[k];
+                    ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
+                }
+                flag_fast = ok;
+            }
+            __syncthreads();
+        } else if (lane == 0) {
+            flag_fast = 0;
+        }
     }
     __syncthreads();
     const bool fast = flag_fast;
@@ -439,7 +505,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         __syncthreads();
     }
     if (a.Q) {
-        for (int e = lane; e < tx * tx; e += 64) Qg[e] = T0[(e / tx) * ZHS + (e % tx)];
+        // columns in descending eigenvalue order (ord), for the top-16 certificate above
+        for (int e = lane; e < tx * tx; e += 64) Qg[e] = T0[(e / tx) * ZHS + ord[e % tx]];
     }
 #ifdef ACE_DEBUG_SWEEPS
     dbg_t3 = __builtin_amdgcn_s_memrealtime();

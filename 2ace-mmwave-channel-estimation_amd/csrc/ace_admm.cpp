@@ -109,6 +109,7 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->T = cv.take(cz * bm);
     s->g = cv.take(cz * bm);
     s->optY = cv.take(cz * bm);
+    s->ypart = cv.take(sizeof(double) * 5 * (size_t)batch * r * ((m + 63) / 64));
     s->st = cv.take<RealState>(sizeof(RealState) * (size_t)batch);
     s->done = cv.take<int>(256);
 }
@@ -182,11 +183,17 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
             { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }      // T = S - A V
         }
-        { ProfScope ps(ACE_K_APPLY_G, st); applyMM(L.G, w.T, w.g); }            // g = G T
-        {
-            ProfScope ps(ACE_K_YSTEP, st);
-            if (fast) launch_ystep(m, batch, fused ? nullptr : w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
-            else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+        if (fused) {  // g = G T with the Y-step in its epilogue
+            ProfScope ps(ACE_K_APPLY_G, st);
+            const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
+            launch_zgemm_ystep(m, batch, L.G, w.T, w.g, ys, w.st, st);
+        } else {
+            { ProfScope ps(ACE_K_APPLY_G, st); applyMM(L.G, w.T, w.g); }        // g = G T
+            {
+                ProfScope ps(ACE_K_YSTEP, st);
+                if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+                else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+            }
         }
         { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
         {
@@ -195,6 +202,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             else applyAH(w.g, w.X, w.V);
         }
         za.it = it;
+        za.ypart = fused ? w.ypart : nullptr;
+        za.ytiles = (m + 63) / 64;
         za.Ynew = w.Y[1 - q];
         za.Yold = w.Y[q];
         za.KYnew = w.KY[1 - q];

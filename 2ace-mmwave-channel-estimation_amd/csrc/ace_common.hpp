@@ -104,7 +104,23 @@ struct ZArgs {
     const unsigned char* rank_one;  // per-realisation use_rank_one (null: all 0); profile [1], [0.95]
     double tol_rel, tol_abs, rho;
     int it, fixed_iters, warm, ld_state;
+    // Y-step reductions left as per-tile partials by the fused apply_G epilogue (null: the
+    // ystep kernel wrote them to RealState): ypart[(b * ytiles + t) * 5 + k], k = obj2, nAX2,
+    // nY2, nJM2, dY2
+    const double* ypart;
+    int ytiles;
 };
+// Y-step fused into the g = G T epilogue (r = 1, shared G): ArgMinY, M update, Y_new and the
+// five reductions as per-(realisation, 64-output tile) partials.
+struct YsArgs {
+    const double* B;   // [b][m]
+    const double* Yo;  // [b][m] c128 (Y of the previous iterate: S = Yo - M/mu)
+    double* M;         // [b][m] c128 in/out
+    double* Yn;        // [b][m] c128 out
+    double* part;      // [b][tilesI][5]
+};
+void launch_zgemm_ystep(int m, int nb, const double* G, const double* T, double* g, const YsArgs& ys,
+                        const RealState* rs, hipStream_t st);
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st);
 

@@ -208,13 +208,17 @@ namespace {
 // FE: the epilogue operand is E - E2 / mu_j (S = Y - M/mu, or V = Z - N/mu), and rows of
 // realisations already marked done are left untouched (as the unfused path leaves them).
 // mu_j and done come from the per-realisation RealState array rs.
-template <int MODE, bool CONJ_L, class CF, bool FV = false, bool FE = false>
+// YS (MODE 0, r = 1): the Y-step of ystep_kernel runs on the g tile in the epilogue; its five
+// reductions are summed over the tile's outputs (16 lanes, then the WI waves, fixed order)
+// and stored as the partial of (realisation, output tile).
+template <int MODE, bool CONJ_L, class CF, bool FV = false, bool FE = false, bool YS = false>
 __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, const double* __restrict__ L, int ldl,
                                                          long long strideL, const double* __restrict__ V, int ldv,
                                                          long long strideV, double* __restrict__ C,
                                                          const double* __restrict__ E, int ldc, long long strideC,
                                                          int tilesI, int tilesJ, const double* __restrict__ V2,
-                                                         const double* __restrict__ E2, const RealState* __restrict__ rs) {
+                                                         const double* __restrict__ E2, const RealState* __restrict__ rs,
+                                                         YsArgs ys = YsArgs{}) {
     constexpr int BJ = CF::BJ, BC = CF::BC, BKC = CF::BKC, NT = CF::NT, TJ = CF::TJ, TC = CF::TC;
     constexpr int VST = CF::VST, LST = CF::LST, PV = CF::PV, PL = CF::PL;
     __shared__ d2 Vs[2][BJ * VST];
@@ -334,6 +338,72 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
     }
 
     // epilogue: lane l, reg r -> realisation j0 + wj*(BJ/WJ) + jj*16 + (l>>4) + 4r, output i0 + wi*(BC/WI) + cc*16 + (l&15)
+    if constexpr (YS) {
+        static_assert(MODE == 0 && TC == 1, "fused Y-step: g = G T with one 16-output block per wave");
+        double* red = reinterpret_cast<double*>(Vs[0]);  // [BJ rows][WI][5], free after the main loop
+#pragma unroll
+        for (int jj = 0; jj < TJ; ++jj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jl = wj * (BJ / CF::WJ) + jj * 16 + (lane >> 4) + 4 * r;
+                const int j = j0 + jl;
+                const int i = i0 + wi * (BC / CF::WI) + (lane & 15);
+                const double a = p1[jj][0][r], b = p2[jj][0][r];
+                const d2 gv = make_double2(a - b, p3[jj][0][r] - a - b);
+                double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+                if (j < nb && i < M) {
+                    const long long off = (long long)j * ldc + i;
+                    reinterpret_cast<d2*>(C)[off] = gv;
+                    if (!rs[j].done) {  // ystep_kernel, element i
+                        const double mu = rs[j].mu, imu = 1.0 / mu;
+                        const d2 mi = reinterpret_cast<const d2*>(ys.M)[off];
+                        const d2 yo = reinterpret_cast<const d2*>(ys.Yo)[off];
+                        const double Bi = ys.B[off];
+                        const d2 ax = csub(csub(yo, cscale(mi, imu)), gv);
+                        d2 c = cadd(ax, cscale(mi, imu));
+                        double d = sqrt(cabs2(c));
+                        if (d == 0.0) {  // ArgMinY zero guard (:516-520 / :524-528)
+                            c = make_double2(1.0, 0.0);
+                            d = 1.0;
+                        }
+                        const double f = (Bi / d + mu) / (1.0 + mu);
+                        const d2 y = cscale(c, f);
+                        const d2 jv = csub(ax, y);
+                        reinterpret_cast<d2*>(ys.M)[off] = cadd(mi, cscale(jv, mu));
+                        reinterpret_cast<d2*>(ys.Yn)[off] = y;
+                        const double aax = sqrt(cabs2(ax)) - Bi;
+                        v[0] = aax * aax;
+                        v[1] = cabs2(ax);
+                        v[2] = cabs2(y);
+                        v[3] = cabs2(jv);
+                        v[4] = cabs2(csub(y, yo));
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) v[k] += __shfl_xor(v[k], o, 64);
+                }
+                if ((lane & 15) == 0) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) red[(jl * CF::WI + wi) * 5 + k] = v[k];
+                }
+            }
+        __syncthreads();
+        if (t < BJ) {
+            const int j = j0 + t;
+            if (j < nb && !rs[j].done) {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int q = 0; q < CF::WI; ++q) s += red[(t * CF::WI + q) * 5 + k];
+                    ys.part[((long long)j * tilesI + ti) * 5 + k] = s;
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int jj = 0; jj < TJ; ++jj)
 #pragma unroll
@@ -418,6 +488,17 @@ void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, 
         launch_zgemm3m_cfg<Big>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
     else
         launch_zgemm3m_cfg<Small>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
+}
+
+// g = G T with the Y-step in the epilogue (r = 1, shared G).  ys.part: [nb][ceil(m/64)][5].
+void launch_zgemm_ystep(int m, int nb, const double* G, const double* T, double* g, const YsArgs& ys,
+                        const RealState* rs, hipStream_t st) {
+    using CF = Gemm3mCfg<64, 64, 16, 2, 4>;
+    const int tilesI = (m + CF::BC - 1) / CF::BC;
+    const int tilesJ = (nb + CF::BJ - 1) / CF::BJ;
+    dim3 grid(tilesI * tilesJ, 1, 1), block(CF::NT);
+    hipLaunchKernelGGL((zgemm3m_kernel<0, false, CF, false, false, true>), grid, block, 0, st, m, m, nb, G, m, 0LL, T,
+                       m, 0LL, g, nullptr, m, 0LL, tilesI, tilesJ, nullptr, nullptr, rs, ys);
 }
 
 // Shared-A products of the r = 1 iteration with pre_kernel folded in (Big tile configuration):

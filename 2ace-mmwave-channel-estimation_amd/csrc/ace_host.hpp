@@ -124,6 +124,7 @@ struct AdmmParams {
 struct AdmmState {
     double *X, *Z, *N, *V, *optX, *Q;
     double *Y[2], *KY[2], *M, *S, *T, *g, *optY;
+    double* ypart;  // fused Y-step partials [batch][ceil(m/64)][5] (r = 1 iterations)
     RealState* st;
     int* done;
 };

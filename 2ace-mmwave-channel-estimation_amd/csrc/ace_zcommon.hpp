@@ -79,8 +79,24 @@ __device__ __forceinline__ int circ_next(int n, int p) {
 // residuals (:364-366), thresholds (:368-370), stop test (:372), mu update (:379-381).
 // Sums: nX2 = ||X||^2, nZ2 = ||Z||^2, jn2 = ||X - Z||^2, dZ2 = ||Z - Z0||^2,
 // dAtY = ||A^H (Y - Y0)||^2, nAtY = ||A^H Y||^2.  Returns 1 when the objective improved.
+// Sum the fused Y-step partials of realisation b (fixed tile order) into v[5].
+__device__ __forceinline__ void ystep_sums(const ZArgs& a, int b, double* v) {
+    for (int k = 0; k < 5; ++k) v[k] = 0.0;
+    for (int t = 0; t < a.ytiles; ++t)
+        for (int k = 0; k < 5; ++k) v[k] += a.ypart[((long long)b * a.ytiles + t) * 5 + k];
+}
+
 __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, double mu, double nX2, double nZ2,
                                             double jn2, double dZ2, double dAtY, double nAtY) {
+    if (a.ypart) {
+        double v[5];
+        ystep_sums(a, (int)(st - a.st), v);
+        st->obj2 = v[0];
+        st->nAX2 = v[1];
+        st->nY2 = v[2];
+        st->nJM2 = v[3];
+        st->dY2 = v[4];
+    }
     const int m = a.m, n = a.n;
     const double nX = sqrt(nX2), nZ = sqrt(nZ2);
     const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);

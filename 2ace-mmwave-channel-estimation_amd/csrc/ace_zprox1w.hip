@@ -518,7 +518,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     // opt_X (:344-351) depends only on the Y-step's objective, so it is decided here and X is
     // copied in the same pass that reads it (iter_control below makes the same decision).
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    const bool improved_pre = !INIT && sqrt(st->obj2) < st->opt_obj;
+    double obj2_now = 0.0;
+    if (!INIT) {
+        if (a.ypart) {
+            double v[5];
+            ystep_sums(a, b, v);
+            obj2_now = v[0];
+        } else {
+            obj2_now = st->obj2;
+        }
+    }
+    const bool improved_pre = !INIT && sqrt(obj2_now) < st->opt_obj;
     d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
     // emit_v: element k with its X, N, Z_old already loaded
     auto emit_v = [&](int k, d2 x, d2 nn, d2 zo, d2 znew) {

@@ -107,6 +107,8 @@ def _load():
     lib.ace_synth_channels.restype = C.c_int
     lib.ace_prof_start.argtypes = [C.c_int]
     lib.ace_prof_start.restype = C.c_int
+    lib.ace_prof_sample.argtypes = [C.c_int]
+    lib.ace_prof_sample.restype = C.c_int
     lib.ace_prof_stop.argtypes = [dp, ip]
     lib.ace_prof_stop.restype = C.c_int
     lib.ace_last_error.argtypes = []

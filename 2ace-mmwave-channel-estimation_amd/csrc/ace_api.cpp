@@ -29,6 +29,13 @@ extern "C" {
 const char* ace_last_error(void) { return g_err.c_str(); }
 const char* ace_version(void) { return "ace-mi355x 0.1.0 (gfx950)"; }
 
+int ace_prof_sample(int stride) {
+    g_err.clear();
+    if (stride < 1) return fail(ACE_ERR_ARG, "stride must be >= 1");
+    g_prof.stride = stride;
+    return ACE_OK;
+}
+
 int ace_prof_start(int max_launches) {
     g_err.clear();
     if (max_launches < 1) return fail(ACE_ERR_ARG, "max_launches must be >= 1");
@@ -37,6 +44,7 @@ int ace_prof_start(int max_launches) {
     for (auto& e : g_prof.ev) ACE_HIP(hipEventCreate(&e));
     g_prof.cls.assign(max_launches, 0);
     g_prof.used = 0;
+    for (int& c : g_prof.seen) c = 0;
     g_prof.on = true;
     return ACE_OK;
 }

@@ -37,6 +37,7 @@ sys.path.insert(0, str(ROOT / "2ace-mmwave-channel-estimation_amd"))
 METRIC = "channel recoveries/sec (32-ant, 256 RSS meas, 200 ADMM iters) @1/2/4/8 GPU"
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= FP64 vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
+PROF_STRIDE = 8           # unit mode: kernel events on every 8th launch per class
 
 
 def parse():
@@ -367,7 +368,8 @@ def main():
     if world > 1:
         dist.barrier()
     prof = not args.no_prof
-    if prof:
+    if prof:   # HIP event pairs on every 8th launch of each kernel class (the pairs cost ~7% if on all)
+        check(LIB.ace_prof_sample(PROF_STRIDE))
         check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
     torch.cuda.synchronize()
     if world > 1:
@@ -421,7 +423,8 @@ def main():
             timed = [k for k in kernels if k in uf or k in ub]
             dom = max(timed, key=lambda k: kernels[k]["total_ms"])
             roof = roofline(dom)
-            roof["note"] = ("dominant kernel by total device time (HIP events on the launch stream); FP64 dense peak "
+            roof["note"] = (f"dominant kernel by total device time (HIP event pairs on the launch stream around every "
+                            f"{PROF_STRIDE}th launch of each kernel class inside the timed region); FP64 dense peak "
                             "(matrix = vector on MI355X) / HBM3E 8 TB/s; traffic: PMC summary in profiles/")
             gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["total_ms"])
             roof_gemm = roofline(gemm)

@@ -107,7 +107,7 @@ def _load():
     lib.ace_synth_channels.restype = C.c_int
     lib.ace_prof_start.argtypes = [C.c_int]
     lib.ace_prof_start.restype = C.c_int
-    lib.ace_prof_sample.argtypes = [C.c_int]
+    lib.ace_prof_sample.argtypes = [C.c_int, C.c_uint32]
     lib.ace_prof_sample.restype = C.c_int
     lib.ace_prof_stop.argtypes = [dp, ip]
     lib.ace_prof_stop.restype = C.c_int

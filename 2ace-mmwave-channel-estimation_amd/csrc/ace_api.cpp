@@ -29,10 +29,11 @@ extern "C" {
 const char* ace_last_error(void) { return g_err.c_str(); }
 const char* ace_version(void) { return "ace-mi355x 0.1.0 (gfx950)"; }
 
-int ace_prof_sample(int stride) {
+int ace_prof_sample(int stride, uint32_t full_mask) {
     g_err.clear();
     if (stride < 1) return fail(ACE_ERR_ARG, "stride must be >= 1");
     g_prof.stride = stride;
+    g_prof.full = full_mask;
     return ACE_OK;
 }
 

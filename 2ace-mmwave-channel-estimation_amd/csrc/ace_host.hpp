@@ -45,7 +45,8 @@ struct Prof {
     std::vector<hipEvent_t> ev;   // 2 per record
     std::vector<int> cls;
     size_t used = 0;
-    int stride = 1;               // record every stride-th launch of each class (ace_prof_sample)
+    int stride = 1;               // record every stride-th launch of each class (ace_prof_sample) ...
+    unsigned full = 0;            // ... except the classes in this mask, recorded on every launch
     int seen[ACE_NKCLASS] = {};
 };
 inline Prof g_prof;
@@ -54,7 +55,9 @@ struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on
     hipStream_t st;
     int idx = -1;
     ProfScope(int c, hipStream_t s) : st(s) {
-        if (g_prof.on && (g_prof.seen[c]++ % g_prof.stride) == 0 && g_prof.used < g_prof.cls.size()) {
+        const bool pick = ((g_prof.full >> c) & 1u) || (g_prof.seen[c] % g_prof.stride) == 0;
+        if (g_prof.on) ++g_prof.seen[c];
+        if (g_prof.on && pick && g_prof.used < g_prof.cls.size()) {
             idx = (int)g_prof.used++;
             g_prof.cls[idx] = c;
             (void)hipEventRecord(g_prof.ev[2 * idx], st);

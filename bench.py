@@ -37,7 +37,7 @@ sys.path.insert(0, str(ROOT / "2ace-mmwave-channel-estimation_amd"))
 METRIC = "channel recoveries/sec (32-ant, 256 RSS meas, 200 ADMM iters) @1/2/4/8 GPU"
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= FP64 vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
-PROF_STRIDE = 8           # unit mode: kernel events on every 8th launch per class
+PROF_STRIDE = 8           # unit mode: kernel events on every 8th launch of the non-roofline classes
 
 
 def parse():
@@ -368,8 +368,10 @@ def main():
     if world > 1:
         dist.barrier()
     prof = not args.no_prof
-    if prof:   # HIP event pairs on every 8th launch of each kernel class (the pairs cost ~7% if on all)
-        check(LIB.ace_prof_sample(PROF_STRIDE))
+    if prof:   # HIP event pairs on every launch of the roofline kernels, every 8th of the rest
+        full = (1 << KERNEL_CLASSES.index("zstep")) | (1 << KERNEL_CLASSES.index("apply_A")) | \
+               (1 << KERNEL_CLASSES.index("apply_AH"))
+        check(LIB.ace_prof_sample(PROF_STRIDE, full))
         check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
     torch.cuda.synchronize()
     if world > 1:
@@ -421,12 +423,14 @@ def main():
                         "kernel": k, "bytes_per_launch": per}
 
             timed = [k for k in kernels if k in uf or k in ub]
-            dom = max(timed, key=lambda k: kernels[k]["total_ms"])
+            # every timed class launches once per iteration: dominant = largest average launch
+            dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
             roof = roofline(dom)
-            roof["note"] = (f"dominant kernel by total device time (HIP event pairs on the launch stream around every "
-                            f"{PROF_STRIDE}th launch of each kernel class inside the timed region); FP64 dense peak "
+            roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
+                            f"region: every launch of zstep/apply_A/apply_AH, every {PROF_STRIDE}th of the other "
+                            f"classes); FP64 dense peak "
                             "(matrix = vector on MI355X) / HBM3E 8 TB/s; traffic: PMC summary in profiles/")
-            gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["total_ms"])
+            gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
             roof_gemm = roofline(gemm)
         cpu = None
         if not args.no_cpu_baseline and world == 1:

@@ -266,9 +266,10 @@ int ace_synth_channels(uint64_t seed, int64_t first, int count, int m, int tx, i
 #define ACE_K_FINAL 9
 #define ACE_NKCLASS 10
 int ace_prof_start(int max_launches);
-/* Record only every stride-th launch of each kernel class (default 1) from the next
- * ace_prof_start on: keeps the event overhead out of a throughput measurement. */
-int ace_prof_sample(int stride);
+/* From the next ace_prof_start on, record only every stride-th launch of each kernel class
+ * (default 1) except the classes whose bit (1 << ACE_K_*) is set in full_mask, which are
+ * recorded on every launch: keeps the event overhead out of a throughput measurement. */
+int ace_prof_sample(int stride, uint32_t full_mask);
 int ace_prof_stop(double* total_ms, int32_t* launches);
 
 /* Last error text for this thread ("" if none). */

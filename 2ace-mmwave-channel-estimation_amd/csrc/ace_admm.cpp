@@ -16,6 +16,8 @@
 //   finalize opt_X / opt_Y (:384-385)
 #include "ace_host.hpp"
 
+#include <cmath>
+#include <cstdlib>
 #include <utility>
 
 namespace ace {
@@ -36,6 +38,39 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->K = cv.take(cz * mats * m * m);
     L->G = cv.take(cz * mats * m * m);
     L->ns = shared ? cv.take(cz * 4 * m * m) : nullptr;
+    L->LA8 = shared ? cv.take<int8_t>(i8_frag_bytes(m, n)) : nullptr;
+    L->LAH8 = shared ? cv.take<int8_t>(i8_frag_bytes(n, m)) : nullptr;
+    L->c8 = shared ? cv.take(sizeof(double)) : nullptr;
+    L->i8flag = shared ? cv.take<int>(sizeof(int)) : nullptr;
+    L->i8ok = false;
+}
+
+// ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
+static bool i8_disabled() {
+    static const bool v = [] {
+        const char* e = getenv("ACE_NO_I8");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// Phase-code check and int8 fragment images of A and A^H (ace_i8gemm.hip).
+static int i8_setup(LinOps& L, hipStream_t st) {
+    const int m = L.m, n = L.n;
+    L.i8ok = false;
+    if (i8_disabled()) return ACE_OK;
+    ACE_HIP(hipMemsetAsync(L.LA8, 0, i8_frag_bytes(m, n), st));
+    ACE_HIP(hipMemsetAsync(L.LAH8, 0, i8_frag_bytes(n, m), st));
+    ACE_HIP(hipMemsetAsync(L.i8flag, 0, sizeof(int), st));
+    launch_max_abs(2LL * m * n, L.A, L.c8, st);
+    launch_i8_expand(m, n, L.A, L.c8, L.LA8, L.LAH8, L.i8flag, st);
+    int flag = 1;
+    double c = 0.0;
+    ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    ACE_HIP(hipMemcpyAsync(&c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
+    ACE_HIP(hipStreamSynchronize(st));
+    L.i8ok = flag == 0 && c > 0.0 && std::isfinite(c);
+    return ACE_OK;
 }
 
 // G = (I + K)^{-1} of the shared K by Newton-Schulz on the matrix cores:
@@ -89,7 +124,10 @@ int linops_setup(LinOps& L, int batch, hipStream_t st) {
         ACE_HIP(hipMemcpyAsync(L.G, L.K, sizeof(double) * 2 * mm * mats, hipMemcpyDeviceToDevice, st));
         launch_inv_ipk(m, mats, L.G, mm, st);
     }
-    if (L.shared) launch_conj_transpose(m, n, L.A, L.AH, st);
+    if (L.shared) {
+        launch_conj_transpose(m, n, L.A, L.AH, st);
+        ACE_TRY(i8_setup(L, st));
+    }
     ACE_HIP(hipGetLastError());
     return ACE_OK;
 }
@@ -102,6 +140,8 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->V = cv.take(cz * bn);
     s->optX = cv.take(cz * bn);
     s->Q = cv.take(cz * (size_t)batch * 32 * 32);
+    s->Z2 = cv.take(cz * (size_t)batch * n);
+    s->N2 = cv.take(cz * (size_t)batch * n);
     for (int i = 0; i < 2; ++i) s->Y[i] = cv.take(cz * bm);
     for (int i = 0; i < 2; ++i) s->KY[i] = cv.take(cz * bm);
     s->M = cv.take(cz * bm);
@@ -124,6 +164,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const long long mm = (long long)m * m, mn = (long long)m * n;
     const bool fast = (r == 1);                       // r = 1 kernels (ystep, one-wave zstep)
     const bool fused = fast && L.shared;              // pre_kernel folded into the shared-A GEMMs
+    const bool i8 = fused && L.i8ok;                  // phase-code A: int8 digit-plane applies
+    const bool wmode = i8 && zstep_takes_w(p.variant, r);   // apply_AH writes W = A^H g, the Z-step forms X
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -160,6 +202,10 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.rho = p.rho;
     za.fixed_iters = p.fixed_iters;
     za.warm = p.eig_warm;
+    za.wmode = 0;
+    za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
+    za.Zn = nullptr;   // in place (init, and every kernel outside wmode)
+    za.Nn = nullptr;
 
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
@@ -175,8 +221,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
 
     int q = 0;
     const int poll = 8;
+    // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
+    double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
-        if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
+        if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
+            ProfScope ps(ACE_K_APPLY_A, st);
+            launch_i8_apply(1, batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, st);
+        } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
         } else {
@@ -198,10 +249,19 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
         {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
-            if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
+            if (wmode) launch_i8_apply(2, batch, m, n, L.LAH8, w.g, nullptr, nullptr, nullptr, w.X, L.c8, w.st, st);
+            else if (i8) launch_i8_apply(2, batch, m, n, L.LAH8, w.g, nullptr, w.Z, w.N, w.X, L.c8, w.st, st);
+            else if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
             else applyAH(w.g, w.X, w.V);
         }
         za.it = it;
+        za.wmode = wmode;
+        if (wmode) {
+            za.Z = Zc;
+            za.N = Nc;
+            za.Zn = Zo;
+            za.Nn = No;
+        }
         za.ypart = fused ? w.ypart : nullptr;
         za.ytiles = (m + 63) / 64;
         za.Ynew = w.Y[1 - q];
@@ -210,6 +270,10 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.KYold = w.KY[q];
         { ProfScope ps(ACE_K_ZSTEP, st); launch_zstep(p.variant, false, za, batch, st); }
         q = 1 - q;
+        if (wmode) {
+            std::swap(Zc, Zo);
+            std::swap(Nc, No);
+        }
         if (!p.fixed_iters && (it % poll == 0) && it < p.maxiter) {
             int h_done = 0;
             ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -220,7 +284,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     ACE_HIP(hipGetLastError());
     {
         ProfScope ps(ACE_K_FINAL, st);
-        launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, w.X, w.Y[q], Xo, Yo, iters, status,
+        launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, wmode ? w.V : w.X, w.Y[q], Xo, Yo, iters, status,
                           mu_out, w.st, st);
     }
     ACE_HIP(hipGetLastError());

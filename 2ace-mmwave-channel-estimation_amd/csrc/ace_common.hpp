@@ -22,7 +22,10 @@ struct RealState {
     double mu, last_res, opt_obj, nB;
     // written by the Y-step kernel each iteration
     double obj2, nAX2, nY2, nJM2, dY2;
-    double pad0, pad1, pad2;
+    // written by the Z-step: upper bound on max|Re|,|Im| of V = Z - N/mu for the next iteration's
+    // apply (the exponent of the int8 digit planes, ace_i8gemm.hip); NaN when Z or N is not finite
+    double vbound;
+    double pad1, pad2;
     int32_t iters, done, status, objcol;  // objcol: argmin column of the per-column objective
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
@@ -33,6 +36,23 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// running max |component| of the entries passed to add(), with a sticky NaN term for
+// non-finite entries (fmax alone would drop a NaN)
+struct VMax {
+    double m = 0.0, s = 0.0;
+    __device__ __forceinline__ void add(double2 v) {
+        const double ax = fabs(v.x), ay = fabs(v.y);
+        m = fmax(m, fmax(ax, ay));
+        s += 0.0 * (ax + ay);
+    }
+};
 
 // block reduction of up to NV doubles; all threads get the result. `sh` >= 16*NV doubles.
 template <int NV>
@@ -76,6 +96,17 @@ struct RealState;
 void launch_zgemm_fused(bool fv, int M, int K, int nb, const double* L, int ldl, const double* V, const double* V2,
                         int ldv, double* C, const double* E, const double* E2, int ldc, const RealState* rs,
                         hipStream_t st);
+// int8 digit-plane applies of a phase-code A (ace_i8gemm.hip)
+int i8_nks(int kc);
+int i8_ncols(int mc);
+size_t i8_frag_bytes(int mc, int kc);
+void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t* LA, int8_t* LH, int* flag,
+                      hipStream_t st);
+// mode 1: C = E1 - E2/mu - c A (V1 - V2/mu)  (Kc = n, Mc = m);  mode 2: C = E1 - E2/mu + c A^H V1  (Kc = m, Mc = n),
+// or C = c A^H V1 alone when E1 is null (the Z-step's wmode)
+void launch_i8_apply(int mode, int nb, int Kc, int Mc, const int8_t* Bfrag, const double* V1, const double* V2,
+                     const double* E1, const double* E2, double* C, const double* cmax, const RealState* rs,
+                     hipStream_t st);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
 // out[0] = max |x_i| over n doubles
@@ -109,7 +140,20 @@ struct ZArgs {
     // nY2, nJM2, dY2
     const double* ypart;
     int ytiles;
+    // wmode (A2only r = 1, non-init): the X buffer holds W = A^H g, and the Z-step forms
+    // X = (Z - N/mu) + W itself (xw below); X of realisations that never improved goes to Xcur
+    int wmode;
+    double* Xcur;
+    // outputs Z', N' (null: in place).  When distinct from Z, N (ping-pong, r = 1) the one-wave
+    // kernel writes the common-case outputs Z' = E, N' = N + mu (X - E) as it forms E, and only
+    // rewrites them when the tail rescaling fires.
+    double* Zn;
+    double* Nn;
 };
+// X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
+__device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {
+    return make_double2(fma(-n.x, imu, z.x) + w.x, fma(-n.y, imu, z.y) + w.y);
+}
 // Y-step fused into the g = G T epilogue (r = 1, shared G): ArgMinY, M update, Y_new and the
 // five reductions as per-(realisation, 64-output tile) partials.
 struct YsArgs {
@@ -123,6 +167,7 @@ void launch_zgemm_ystep(int m, int nb, const double* G, const double* T, double*
                         const RealState* rs, hipStream_t st);
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st);
+bool zstep_takes_w(int variant, int r);
 
 // ArgMinZ rank profile of realisation b (inferLowRankV4_multi.m:437-464; use_rank_one -> :448-450).
 struct ZProfile {

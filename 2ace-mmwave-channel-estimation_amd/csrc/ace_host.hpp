@@ -113,6 +113,13 @@ struct LinOps {
     double* K;
     double* G;
     double* ns;  // shared regime: Newton-Schulz scratch (4 m x m: I + K, I, R, X'), else null
+    // shared regime, phase-code A (every real component in {0, +-c}): the int8 fragment images of
+    // A and A^H for the exact digit-plane applies (ace_i8gemm.hip); i8ok is set by linops_setup
+    int8_t* LA8;
+    int8_t* LAH8;
+    double* c8;   // device: c
+    int* i8flag;  // device: set when some component is not in {0, +-c}
+    bool i8ok;
 };
 size_t linops_bytes(bool shared, int batch, int m, int n);
 void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L);
@@ -128,6 +135,7 @@ struct AdmmParams {
 // Per-iteration state of a batch of `batch` realisations with r columns each.
 struct AdmmState {
     double *X, *Z, *N, *V, *optX, *Q;
+    double *Z2, *N2;  // ping-pong partners of Z, N for the r = 1 wmode iteration ([batch][n])
     double *Y[2], *KY[2], *M, *S, *T, *g, *optY;
     double* ypart;  // fused Y-step partials [batch][ceil(m/64)][5] (r = 1 iterations)
     RealState* st;

@@ -44,12 +44,16 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
 
     // accumulators: nX2, nZ2, nJN2, dZ2
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    VMax vz, vn;   // max |Z|, |N| of the outputs: the next apply's bound on |Z - N/mu|
     auto emit = [&](int k, d2 znew) {  // per-element update + reductions
         const d2 x = X[k];
+        vz.add(znew);
         if (!INIT) {
             const d2 zo = Z[k];
             const d2 d = csub(x, znew);
-            N[k] = cadd(N[k], cscale(d, mu));
+            const d2 nnew = cadd(N[k], cscale(d, mu));
+            N[k] = nnew;
+            vn.add(nnew);
             acc[0] += cabs2(x);
             acc[1] += cabs2(znew);
             acc[2] += cabs2(d);
@@ -254,7 +258,28 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
     }
 #undef ACE_ZSTEP_LDS
-    if (INIT) return;
+    // bound for the next iteration's V = Z - N/mu (written after iter_control's mu update)
+    double vb[3] = {wave_max(vz.m), wave_max(vn.m), wave_sum(vz.s + vn.s)};
+    __syncthreads();
+    if (lane == 0) {
+        red[64 + 3 * w] = vb[0];
+        red[64 + 3 * w + 1] = vb[1];
+        red[64 + 3 * w + 2] = vb[2];
+    }
+    __syncthreads();
+    if (t == 0)
+        for (int k = 1; k < nt / 64; ++k) {
+            vb[0] = fmax(vb[0], red[64 + 3 * k]);
+            vb[1] = fmax(vb[1], red[64 + 3 * k + 1]);
+            vb[2] += red[64 + 3 * k + 2];
+        }
+    auto write_vbound = [&]() {
+        if (t == 0) st->vbound = (vb[0] + vb[1] * (1.0 / st->mu)) * (1.0 + 0x1p-40) + vb[2];
+    };
+    if (INIT) {
+        write_vbound();
+        return;
+    }
 
     // m-space dual terms: ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0),  ||A^H Y||^2 = Y^H K Y
     const int rm = r * m;
@@ -273,6 +298,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
     }
     block_sum<6>(v6, red);
     if (t == 0) flag_improved = iter_control(a, st, mu, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]);
+    write_vbound();
     __syncthreads();
     if (flag_improved) {  // best-objective iterate (:344-361): all columns, or the argmin column
         const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * rm;
@@ -378,6 +404,9 @@ static bool use_4wave_zstep() {
     }();
     return v;
 }
+
+// the one-wave A2only kernel forms X from W = A^H g itself (ZArgs::wmode)
+bool zstep_takes_w(int variant, int r) { return variant != ACE_VARIANT_NUCLEAR && r == 1 && !use_4wave_zstep(); }
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st) {
 #define ACE_ZL(V, I, G) hipLaunchKernelGGL((zstep_kernel<V, I, G>), dim3(batch), dim3(256), 0, st, a)

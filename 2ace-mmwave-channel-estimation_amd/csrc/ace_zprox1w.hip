@@ -71,16 +71,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
 
     const double mu = INIT ? 1.0 : st->mu;
     const d2* X = reinterpret_cast<const d2*>(a.X) + (long long)b * n;
-    d2* N = reinterpret_cast<d2*>(a.N) + (long long)b * n;
-    d2* Z = reinterpret_cast<d2*>(a.Z) + (long long)b * n;
+    const d2* N = reinterpret_cast<const d2*>(a.N) + (long long)b * n;
+    const d2* Z = reinterpret_cast<const d2*>(a.Z) + (long long)b * n;
+    d2* Nn = reinterpret_cast<d2*>(a.Nn ? a.Nn : a.N) + (long long)b * n;
+    d2* Zn = reinterpret_cast<d2*>(a.Zn ? a.Zn : a.Z) + (long long)b * n;
+    const bool pp = !INIT && a.Zn && a.Zn != a.Z && a.Nn != a.N;   // ping-pong outputs
     d2* Qg = reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx;
     const bool warm = (!INIT) && a.warm;
     const double imu = 1.0 / mu;
+    // wmode: the X buffer holds W = A^H g and X = (Z - N/mu) + W is formed here
+    const bool wm = !INIT && a.wmode;
+    auto loadx = [&](int k, d2 nn, d2 zo) -> d2 {
+        const d2 v = X[k];
+        return wm ? xw(zo, nn, v, imu) : v;
+    };
     auto evalE = [&](int k) -> d2 {  // X + N/mu (:424), as N * (1/mu) like pre_kernel's V = Z - N/mu
-        const d2 x = X[k], nn = N[k];
+        const d2 nn = N[k];
+        const d2 x = loadx(k, nn, wm ? Z[k] : nn);
         return make_double2(fma(nn.x, imu, x.x), fma(nn.y, imu, x.y));
     };
     const d2 zero = make_double2(0.0, 0.0);
+    // Whether this iterate becomes opt_X (:344-351) depends only on the Y-step's objective, so
+    // it is decided up front and X is copied as it is formed (iter_control makes the same decision).
+    double obj2_now = 0.0;
+    if (!INIT) {
+        if (a.ypart) {
+            double v[5];
+            ystep_sums(a, b, v);
+            obj2_now = v[0];
+        } else {
+            obj2_now = st->obj2;
+        }
+    }
+    const bool improved_pre = !INIT && sqrt(obj2_now) < st->opt_obj;
+    const bool keep_cur = wm && !improved_pre && !(st->opt_obj < INFINITY);   // finalize's fallback X
+    d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
+    d2* Xc = reinterpret_cast<d2*>(a.Xcur) + (long long)b * n;
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long dbg_t1 = dbg_t0, dbg_t2 = dbg_t0, dbg_t3 = dbg_t0, dbg_fa = 0, dbg_fb = 0, dbg_fc = 0;
@@ -111,25 +137,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     }
     // ---- E = reshape(X + N/mu, tx, []) (:424-426), zero padded to 32x32.  Loads are issued
     // in chunks of 8 per lane ahead of the LDS stores (memory-level parallelism).
+    // Speculative outputs of the common case Z = E (no tail rescaling): N' = N + mu (X - E) and
+    // the four sums, kept in registers until the certificate decides (element e = lane + 64 u).
     double etr = 0.0;  // ||E||_F^2 = trace(E E^H)
+    double sacc[4] = {0.0, 0.0, 0.0, 0.0};
+    VMax svz, svn;
 #pragma unroll
     for (int e0 = 0; e0 < ZT * ZT; e0 += 64 * 8) {
-        d2 xv[8], nv[8];
+        d2 xv[8], nv[8], zv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
-            xv[u] = nv[u] = zero;
+            xv[u] = nv[u] = zv[u] = zero;
             if (i < tx && j < rx) {
                 xv[u] = X[i + tx * j];
                 nv[u] = N[i + tx * j];
+                if (!INIT) zv[u] = Z[i + tx * j];
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
-            const d2 ev = (i < tx && j < rx) ? make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y)) : zero;
+            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5, k = i + tx * j;
+            const bool in = i < tx && j < rx;
+            const d2 x = wm ? xw(zv[u], nv[u], xv[u], imu) : xv[u];
+            const d2 ev = in ? make_double2(fma(nv[u].x, imu, x.x), fma(nv[u].y, imu, x.y)) : zero;
             etr += cabs2(ev);
             T0[i * ZHS + j] = ev;
+            if (in && !INIT) {
+                if (improved_pre) oX[k] = x;
+                else if (keep_cur) Xc[k] = x;
+                const d2 d = csub(x, ev);
+                const d2 nn = cadd(nv[u], cscale(d, mu));
+                if (pp) {
+                    Zn[k] = ev;
+                    Nn[k] = nn;
+                }
+                sacc[0] += cabs2(x);
+                sacc[1] += cabs2(ev);
+                sacc[2] += cabs2(d);
+                sacc[3] += cabs2(csub(ev, zv[u]));
+                svz.add(ev);
+                svn.add(nn);
+            }
         }
     }
     __syncthreads();
@@ -269,6 +318,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     dbg_fc = __builtin_amdgcn_s_memrealtime();
 #endif
     if (lane == 0) flag_any = 0;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    VMax vz, vn;   // max |Z|, |N| of the outputs: the next apply's bound on |Z - N/mu|
+    if (pp && fast) {   // Z = E: the outputs written in phase 1 stand
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = sacc[q];
+        vz = svz;
+        vn = svn;
+    } else {
     if (!fast) {
     // H = F F^H (:428), upper blocks (0,0), (0,1), (1,1) -> packed buffer 0
     {
@@ -517,33 +574,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     // per-element update + reductions: nX2, nZ2, nJN2, dZ2.  Whether this iterate becomes
     // opt_X (:344-351) depends only on the Y-step's objective, so it is decided here and X is
     // copied in the same pass that reads it (iter_control below makes the same decision).
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    double obj2_now = 0.0;
-    if (!INIT) {
-        if (a.ypart) {
-            double v[5];
-            ystep_sums(a, b, v);
-            obj2_now = v[0];
-        } else {
-            obj2_now = st->obj2;
-        }
-    }
-    const bool improved_pre = !INIT && sqrt(obj2_now) < st->opt_obj;
-    d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
-    // emit_v: element k with its X, N, Z_old already loaded
+    // emit_v: element k with its X, N, Z_old already loaded (opt_X was copied in phase 1)
     auto emit_v = [&](int k, d2 x, d2 nn, d2 zo, d2 znew) {
-        if (improved_pre) oX[k] = x;
+        vz.add(znew);
         if (!INIT) {
             const d2 d = csub(x, znew);
-            N[k] = cadd(nn, cscale(d, mu));
+            const d2 nnew = cadd(nn, cscale(d, mu));
+            Nn[k] = nnew;
+            vn.add(nnew);
             acc[0] += cabs2(x);
             acc[1] += cabs2(znew);
             acc[2] += cabs2(d);
             acc[3] += cabs2(csub(znew, zo));
         }
-        Z[k] = znew;
+        Zn[k] = znew;
     };
-    auto emit = [&](int k, d2 znew) { emit_v(k, X[k], INIT ? zero : N[k], INIT ? zero : Z[k], znew); };
+    auto emit = [&](int k, d2 znew) {
+        const d2 nn = INIT ? zero : N[k], zo = INIT ? zero : Z[k];
+        emit_v(k, loadx(k, nn, zo), nn, zo, znew);
+    };
     if (flag_any) {
         // per column block J of E: T(:, J) = diag(sqrt(scl)) Qnew^H E(:, J) (rows = eigen indices),
         // then Z^T(J, :) = T(:, J)^T Qnew^T with A = T^T straight from the accumulators and
@@ -604,11 +653,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int k = k0 + lane + 64 * u;
-                if (k < n)
-                    emit_v(k, xv[u], nv[u], zv[u], make_double2(fma(nv[u].x, imu, xv[u].x), fma(nv[u].y, imu, xv[u].y)));
+                const d2 x = wm ? xw(zv[u], nv[u], xv[u], imu) : xv[u];
+                if (k < n) emit_v(k, x, nv[u], zv[u], make_double2(fma(nv[u].x, imu, x.x), fma(nv[u].y, imu, x.y)));
             }
         }
     }
+    }  // !(fast)
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t4 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0 && (b == 0 || b == 2000) && (a.it < 30 || a.it % 20 == 0))
@@ -618,7 +668,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         printf("1w b %d it %d fast: E %llu F %llu cert %llu rest %llu\n", b, a.it, dbg_fa - dbg_t0, dbg_fb - dbg_fa,
                dbg_fc - dbg_fb, dbg_t4 - dbg_fc);
 #endif
-    if (INIT) return;
+    // bound for the next iteration's V = Z - N/mu (after iter_control's mu update)
+    auto write_vbound = [&]() {
+        const double zm = wave_max(vz.m), nm = wave_max(vn.m), sn = wave_sum(vz.s + vn.s);
+        if (lane == 0) st->vbound = (zm + nm * (1.0 / st->mu)) * (1.0 + 0x1p-40) + sn;
+    };
+    if (INIT) {
+        write_vbound();   // N = 0 after init (init_r_kernel)
+        return;
+    }
 
     // m-space dual terms: ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0),  ||A^H Y||^2 = Y^H K Y
     double dAtY = 0.0, nAtY = 0.0;
@@ -640,6 +698,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     if (lane == 0)
         improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
     improved = __shfl(improved, 0, 64);
+    write_vbound();
     if (improved) {  // opt_X was written by emit (improved == improved_pre)
         d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
         const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;

@@ -69,7 +69,7 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipMemcpyAsync(&c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipStreamSynchronize(st));
-    L.i8ok = flag == 0 && c > 0.0 && std::isfinite(c);
+    L.i8ok = flag == 0 && c > 0.0 && std::isfinite(c) && i8ah_lds_bytes(m) <= 160 * 1024 - 256;
     return ACE_OK;
 }
 
@@ -164,8 +164,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const long long mm = (long long)m * m, mn = (long long)m * n;
     const bool fast = (r == 1);                       // r = 1 kernels (ystep, one-wave zstep)
     const bool fused = fast && L.shared;              // pre_kernel folded into the shared-A GEMMs
-    const bool i8 = fused && L.i8ok;                  // phase-code A: int8 digit-plane applies
-    const bool wmode = i8 && zstep_takes_w(p.variant, r);   // apply_AH writes W = A^H g, the Z-step forms X
+    // phase-code A: int8 digit-plane applies; apply_AH writes W = A^H g and the Z-step forms X
+    const bool i8 = fused && L.i8ok && zstep_takes_w(p.variant, r);
+    const bool wmode = i8;
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -226,7 +227,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     for (int it = 1; it <= p.maxiter; ++it) {
         if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
-            launch_i8_apply(1, batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, st);
+            launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
@@ -249,8 +250,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
         {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
-            if (wmode) launch_i8_apply(2, batch, m, n, L.LAH8, w.g, nullptr, nullptr, nullptr, w.X, L.c8, w.st, st);
-            else if (i8) launch_i8_apply(2, batch, m, n, L.LAH8, w.g, nullptr, w.Z, w.N, w.X, L.c8, w.st, st);
+            if (wmode) launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st);
             else if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
             else applyAH(w.g, w.X, w.V);
         }

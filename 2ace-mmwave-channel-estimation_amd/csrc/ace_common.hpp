@@ -102,11 +102,13 @@ int i8_ncols(int mc);
 size_t i8_frag_bytes(int mc, int kc);
 void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t* LA, int8_t* LH, int* flag,
                       hipStream_t st);
-// mode 1: C = E1 - E2/mu - c A (V1 - V2/mu)  (Kc = n, Mc = m);  mode 2: C = E1 - E2/mu + c A^H V1  (Kc = m, Mc = n),
-// or C = c A^H V1 alone when E1 is null (the Z-step's wmode)
-void launch_i8_apply(int mode, int nb, int Kc, int Mc, const int8_t* Bfrag, const double* V1, const double* V2,
-                     const double* E1, const double* E2, double* C, const double* cmax, const RealState* rs,
-                     hipStream_t st);
+// T = (Y - M/mu) - c A (Z - N/mu)   (A: m x n phase code, c = *cmax)
+void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
+                       const double* M, double* T, const double* cmax, const RealState* rs, hipStream_t st);
+// W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
+void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
+                        const RealState* rs, hipStream_t st);
+size_t i8ah_lds_bytes(int kc);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
 // out[0] = max |x_i| over n doubles

@@ -45,11 +45,10 @@ typedef int i16v __attribute__((ext_vector_type(16)));
 
 constexpr int RB = 16;           // realisations per work-group
 constexpr int ROWS = RB * 8;     // MFMA rows per work-group (realisation, digit)
-constexpr int KC = 128;          // K reals per stage
-constexpr int RS = KC + 16;      // LDS row stride (bytes): 16-byte slots of 8 consecutive rows distinct
+constexpr int KC = 128;          // K padding granule (reals) and apply_AH's staging block
 constexpr int NCB = 512;         // output reals per work-group
 constexpr int NT = 512;          // threads (8 waves)
-constexpr int KSC = KC / 32;     // MFMA K-steps per stage
+constexpr int KSC = KC / 32;     // MFMA K-steps per granule
 
 // LDS row of (realisation bl in 0..15, digit t in 0..7): inverse of the accumulator map
 // row = (g & 3) + 8 (g >> 2) + 4 h  ->  realisation 4R + 2 (g >> 3) + h, digit (g & 3) + 4 ((g >> 2) & 1)
@@ -90,161 +89,316 @@ __device__ __forceinline__ int exp_of(double bound) {
     return e < -960 ? -960 : (e > 1000 ? 1000 : e);
 }
 
-// MODE 1: C = E1 - E2/mu - c (A V),  V = V1 - V2/mu   (K = n, outputs m)
-// MODE 2: C = E1 - E2/mu + c (A^H V), V = V1           (K = m, outputs n)
-template <int MODE>
-__global__ __launch_bounds__(NT, 1) void i8apply_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
-                                                        const double* __restrict__ V1, const double* __restrict__ V2,
-                                                        const double* __restrict__ E1, const double* __restrict__ E2,
-                                                        double* __restrict__ C, const double* __restrict__ cptr,
-                                                        const RealState* __restrict__ rs) {
-    __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RS];
+// A fragments of one K-step from the LDS digit image: rows 32R + (lane & 31), k bytes
+// 16 (lane >> 5) .. +15 of the step.
+__device__ __forceinline__ void aload(const int8_t* arow, int rstride, i4v (&af)[4]) {
+#ifdef ACE_I8_PROBE_NO_LDS
+    for (int R = 0; R < 4; ++R) af[R] = i4v{R, 1, 2, 3};
+#else
+#pragma unroll
+    for (int R = 0; R < 4; ++R) af[R] = *reinterpret_cast<const i4v*>(arow + 32 * R * rstride);
+#endif
+}
+// The 4 x 2 MFMA tiles of a wave for one K-step (codebook fragments b0, b1).
+__device__ __forceinline__ void kstep(const i4v (&af)[4], i4v b0, i4v b1, i16v (&acc)[4][2]) {
+#pragma unroll
+    for (int R = 0; R < 4; ++R) {
+        acc[R][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], b0, acc[R][0], 0, 0, 0);
+        acc[R][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], b1, acc[R][1], 0, 0, 0);
+    }
+}
+
+// Recombined digit planes of output column col for realisation 4R + 2q + (lane >> 5):
+// sum_t acc[8q + t] 128^t (Horner from the signed top digit).
+__device__ __forceinline__ double recombine(const i16v& a, int q) {
+    double v = (double)a[8 * q + 7];
+#pragma unroll
+    for (int tt = 6; tt >= 0; --tt) v = fma(v, 128.0, (double)a[8 * q + tt]);
+    return v;
+}
+
+// Exponent and scale of one realisation's digit planes from a bound on max|component|.
+__device__ __forceinline__ void plane_scale(double bound, double c, double& p2, double& sc) {
+    const bool finite = bound <= DBL_MAX;
+    const int e = finite ? exp_of(bound) : 0;
+    p2 = ldexp(1.0, 54 - e);
+    sc = finite ? c * ldexp(1.0, e - 54) : __builtin_nan("");
+}
+
+// ---- software pipeline shared by both applies.  A "stage" is SK = 2 MFMA K-steps (64 K
+// reals).  Global loads are issued only at stage starts, in a fixed order, into register
+// sets whose roles alternate between even and odd stages (the stage loop is unrolled by 2),
+// so no register that a load is still filling is ever copied and the compiler's vmcnt
+// waits are exact: a stage's codebook fragments are loaded one stage ahead, apply_A's f64
+// inputs two stages ahead.  (vmcnt retires in order on CDNA; a copy of an in-flight
+// register, or a load under a branch, turns every wait into vmcnt(0).)
+constexpr int SK = 2;
+struct BSet {
+    i4v f[SK][2];
+};
+// codebook fragments of K-steps ks0, ks0 + 1 for this wave's two column tiles (clamped to
+// the last step past the end: the loads stay unconditional)
+__device__ __forceinline__ void bload(BSet& b, const i4v* bp0, const i4v* bp1, int ks0, int kmax) {
+#pragma unroll
+    for (int kk = 0; kk < SK; ++kk) {
+        const long long ks = min(ks0 + kk, kmax);
+        b.f[kk][0] = bp0[ks * 64];
+        b.f[kk][1] = bp1[ks * 64];
+    }
+}
+// SK K-steps on the digit image at arow (A fragments double-buffered one step ahead)
+__device__ __forceinline__ void stage_mma(const int8_t* arow, int rstride, const BSet& b, i16v (&acc)[4][2]) {
+    i4v a0[4], a1[4];
+    aload(arow, rstride, a0);
+    aload(arow + 32, rstride, a1);
+    kstep(a0, b.f[0][0], b.f[0][1], acc);
+    kstep(a1, b.f[1][0], b.f[1][1], acc);
+}
+
+// apply_A:  T = (Y - M/mu) - c A V,  V = Z - N/mu  (K = n complex, outputs m complex).
+constexpr int SKR = SK * 32;       // K reals per stage
+constexpr int RSA = SKR + 16;      // LDS row stride of a stage image (bytes): conflict-free b128 reads
+__global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                                    const double* __restrict__ Zp, const double* __restrict__ Np,
+                                                    const double* __restrict__ Yp, const double* __restrict__ Mp,
+                                                    double* __restrict__ Tp, const double* __restrict__ cptr,
+                                                    const RealState* __restrict__ rs) {
+    __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
     __shared__ double sc_s[RB], imu_s[RB];
     __shared__ int live_s[RB];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int j0 = blockIdx.x * RB, cb = blockIdx.y;
-    // staging role: realisation bl, complex pair cp (entries 64 kc + 2 cp, +1 of chunk kc)
-    const int bl = t >> 5, cp = t & 31, jb = j0 + bl;
+    const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: realisation bl, entry 32 s + cq
     const bool live = jb < nb && !rs[jb].done;
     const double imu = live ? 1.0 / rs[jb].mu : 0.0;
-    const d2* v1 = reinterpret_cast<const d2*>(V1) + (long long)jb * Kc;
-    const d2* v2 = reinterpret_cast<const d2*>(V2) + (long long)jb * Kc;
-
-    double bound = 0.0;
-    if (MODE == 1) {
-        bound = live ? rs[jb].vbound : 0.0;
-    } else {   // max |g| over the realisation (32 lanes of this half-wave)
-        double mx = 0.0, sn = 0.0;
-        if (live)
-            for (int k = cp; k < Kc; k += 32) {
-                const d2 v = v1[k];
-                const double ax = fabs(v.x), ay = fabs(v.y);
-                mx = fmax(mx, fmax(ax, ay));
-                sn += 0.0 * (ax + ay);   // NaN / Inf sticky
-            }
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            mx = fmax(mx, __shfl_xor(mx, o, 64));
-            sn += __shfl_xor(sn, o, 64);
-        }
-        bound = mx + sn;
-    }
-    const bool finite = bound <= DBL_MAX;
-    const int e = finite ? exp_of(bound) : 0;
-    const double p2 = ldexp(1.0, 54 - e);
-    if (cp == 0) {
-        sc_s[bl] = finite ? (*cptr) * ldexp(1.0, e - 54) : __builtin_nan("");
+    const d2* z = reinterpret_cast<const d2*>(Zp) + (long long)(live ? jb : 0) * Kc;
+    const d2* nn = reinterpret_cast<const d2*>(Np) + (long long)(live ? jb : 0) * Kc;
+    double p2, sc;
+    plane_scale(live ? rs[jb].vbound : 0.0, *cptr, p2, sc);
+    if (cq == 0) {
+        sc_s[bl] = sc;
         imu_s[bl] = imu;
         live_s[bl] = live;
     }
-
-    // ---- staging: 2 complex entries of realisation bl per thread per stage
-    d2 g1[2], g2[2];
-    auto gload = [&](int kc) {
+    const int nstage = nks / SK, kmax = nks - 1;
+    struct Raw {
+        d2 z, n;
+    };
+    auto gload = [&](int s, Raw& r) {   // unconditional (clamped) loads; masked at the digit step
+        const int k = min(32 * s + cq, Kc - 1);
+        r.z = z[k];
+        r.n = nn[k];
+    };
+    auto lstore = [&](const Raw& r, int s, int buf) {
+        const bool in = live && 32 * s + cq < Kc;
+        const double v[2] = {in ? fma(-r.n.x, imu, r.z.x) : 0.0, in ? fma(-r.n.y, imu, r.z.y) : 0.0};
+        uint32_t lo[2];
+        int32_t hi[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int k = KC / 2 * kc + 2 * cp + u;
-            g1[u] = g2[u] = make_double2(0.0, 0.0);
-            if (live && k < Kc) {
-                g1[u] = v1[k];
-                if (MODE == 1) g2[u] = v2[k];
+        for (int i = 0; i < 2; ++i) {
+            const double x = rint(v[i] * p2);
+            const double h = floor(x * 0x1p-32);
+            hi[i] = (int32_t)h;
+            lo[i] = (uint32_t)fma(-h, 0x1p32, x);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            uint32_t d[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (tt < 4) d[i] = (lo[i] >> (7 * tt)) & 127u;
+                else if (tt == 4) d[i] = __builtin_amdgcn_alignbit((uint32_t)hi[i], lo[i], 28) & 127u;
+                else if (tt == 5) d[i] = ((uint32_t)hi[i] >> 3) & 127u;
+                else if (tt == 6) d[i] = ((uint32_t)hi[i] >> 10) & 127u;
+                else d[i] = (uint32_t)(hi[i] >> 17) & 255u;
             }
+            *reinterpret_cast<uint16_t*>(&As[buf][lds_row(bl, tt) * RSA + 2 * cq]) = (uint16_t)(d[0] | (d[1] << 8));
         }
-    };
-    auto lstore = [&](int buf) {
-        double v[4];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            d2 x = g1[u];
-            if (MODE == 1) x = make_double2(fma(-g2[u].x, imu, x.x), fma(-g2[u].y, imu, x.y));   // V = Z - N/mu (xw)
-            v[2 * u] = x.x;
-            v[2 * u + 1] = x.y;
-        }
-        uint32_t d[8];
-        digits4(v, p2, d);
-#pragma unroll
-        for (int tt = 0; tt < 8; ++tt)
-            *reinterpret_cast<uint32_t*>(&As[buf][lds_row(bl, tt) * RS + 4 * cp]) = d[tt];
     };
 
-    // ---- codebook fragments: wave w owns column tiles ct0, ct0 + 1 of the 32-column tiles
-    const int ct0 = cb * (NCB / 32) + 2 * w;
+    const int ct0 = cb * (NCB / 32) + 2 * w;   // this wave's two 32-column tiles
     const i4v* bp0 = Bf + (long long)ct0 * nks * 64 + lane;
     const i4v* bp1 = bp0 + (long long)nks * 64;
-    // three-deep register ring (current, +1, +2 K-steps), rotated by value
-    i4v bc0, bc1, bn0, bn1, bm0, bm1;
 
     i16v acc[4][2];
 #pragma unroll
-    for (int R = 0; R < 4; ++R)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[R][c] = i16v{};
+    for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
 
-    const int nstage = nks / KSC;
-    bc0 = bp0[0];
-    bc1 = bp1[0];
-    bn0 = bp0[64];
-    bn1 = bp1[64];
-    gload(0);
-    lstore(0);
+    Raw r0, r1;
+    BSet bA, bB;
+    bload(bA, bp0, bp1, 0, kmax);
+    gload(0, r0);
+    gload(1, r1);
+    lstore(r0, 0, 0);
     __syncthreads();
-    const int8_t* arow = nullptr;
-    for (int s = 0; s < nstage; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < nstage) gload(s + 1);
-        arow = &As[buf][(lane & 31) * RS + 16 * (lane >> 5)];
-#pragma unroll
-        for (int kk = 0; kk < KSC; ++kk) {
-            const int ks = s * KSC + kk;
-            if (ks + 2 < nks) {
-                bm0 = bp0[(long long)(ks + 2) * 64];
-                bm1 = bp1[(long long)(ks + 2) * 64];
-            }
-            i4v af[4];
-#pragma unroll
-            for (int R = 0; R < 4; ++R) af[R] = *reinterpret_cast<const i4v*>(arow + 32 * R * RS + 32 * kk);
-#pragma unroll
-            for (int R = 0; R < 4; ++R) {
-                acc[R][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], bc0, acc[R][0], 0, 0, 0);
-                acc[R][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], bc1, acc[R][1], 0, 0, 0);
-            }
-            bc0 = bn0;
-            bc1 = bn1;
-            bn0 = bm0;
-            bn1 = bm1;
-        }
-        if (s + 1 < nstage) lstore(buf ^ 1);
+    const int8_t* arow0 = &As[0][(lane & 31) * RSA + 16 * (lane >> 5)];
+    const int8_t* arow1 = arow0 + ROWS * RSA;
+    for (int s = 0; s < nstage; s += 2) {
+        // even stage s: digits in buffer 0, codebook bA, raw(s + 1) in r1
+        bload(bB, bp0, bp1, (s + 1) * SK, kmax);
+        gload(min(s + 2, nstage - 1), r0);
+        __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
+        stage_mma(arow0, RSA, bA, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        lstore(r1, s + 1, 1);
+        __syncthreads();
+        // odd stage s + 1: buffer 1, bB, raw(s + 2) in r0
+        bload(bA, bp0, bp1, (s + 2) * SK, kmax);
+        gload(min(s + 3, nstage - 1), r1);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_mma(arow1, RSA, bB, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        lstore(r0, s + 2, 0);
         __syncthreads();
     }
 
-    // ---- epilogue: lane (col = lane & 31, h = lane >> 5), registers 8q..8q+7 = digits of
+    // epilogue: lane (col = lane & 31, h = lane >> 5), registers 8q..8q+7 = digit planes of
     // realisation 4R + 2q + h
-    const int h = lane >> 5;
-    const int ldo = 2 * Mc;   // reals per output row
+    const int h = lane >> 5, ldo = 2 * Mc;
 #pragma unroll
     for (int R = 0; R < 4; ++R)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int blo = 4 * R + 2 * q + h, j = j0 + blo;
             if (j >= nb || !live_s[blo]) continue;
-            const double sc = sc_s[blo], im = imu_s[blo];
+            const double scb = sc_s[blo], im = imu_s[blo];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const int col = (ct0 + c) * 32 + (lane & 31);
                 if (col >= ldo) continue;
-                double a = (double)acc[R][c][8 * q + 7];
-#pragma unroll
-                for (int tt = 6; tt >= 0; --tt) a = fma(a, 128.0, (double)acc[R][c][8 * q + tt]);
                 const long long off = (long long)j * ldo + col;
-                if (MODE == 2 && !E1) {   // raw product W for the Z-step's wmode
-                    C[off] = sc * a;
-                    continue;
-                }
-                const double ev = fma(-E2[off], im, E1[off]);
-                C[off] = MODE == 1 ? ev - sc * a : ev + sc * a;
+                Tp[off] = fma(-Mp[off], im, Yp[off]) - scb * recombine(acc[R][c], q);
             }
         }
+}
+
+// apply_AH in the Z-step's wmode:  W = c A^H g  (K = m complex, outputs n complex).
+// The digit planes of all of K stay in LDS (dynamic, ROWS x (32 nks + 16) bytes) and the
+// work-group sweeps every 512-column block of the output as one flat sequence of K-steps,
+// so the exponent pre-pass and the staging run once per 16 realisations and the codebook
+// pipeline runs across block boundaries.
+__global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                                     const double* __restrict__ Gp, double* __restrict__ Wp,
+                                                     const double* __restrict__ cptr,
+                                                     const RealState* __restrict__ rs) {
+    extern __shared__ __attribute__((aligned(16))) int8_t Ad[];
+    __shared__ double sc_s[RB];
+    __shared__ int live_s[RB];
+    const int rst = 32 * nks + 16;   // LDS row stride (bytes)
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int j0 = blockIdx.x * RB;
+    const int bl = t >> 5, cp = t & 31, jb = j0 + bl;
+    const bool live = jb < nb && !rs[jb].done;
+    const d2* g = reinterpret_cast<const d2*>(Gp) + (long long)jb * Kc;
+
+    // g of this realisation: 2 complex entries per 128-real block per thread, one batch of
+    // loads (up to GR blocks held in registers; longer K re-reads the rest from L2)
+    constexpr int GR = 4;
+    const int nst = nks / 4;
+    d2 gv[GR][2];
+    double mx = 0.0, sn = 0.0;   // max |g| of the realisation over this half-wave
+    auto gat = [&](int s, int u) -> d2 {
+        const int k = 64 * s + 2 * cp + u;
+        return (live && k < Kc) ? g[k] : make_double2(0.0, 0.0);
+    };
+#pragma unroll
+    for (int s = 0; s < GR; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) gv[s][u] = s < nst ? gat(s, u) : make_double2(0.0, 0.0);
+    auto acc_max = [&](d2 v) {
+        const double ax = fabs(v.x), ay = fabs(v.y);
+        mx = fmax(mx, fmax(ax, ay));
+        sn += 0.0 * (ax + ay);   // NaN / Inf sticky
+    };
+#pragma unroll
+    for (int s = 0; s < GR; ++s) {
+        acc_max(gv[s][0]);
+        acc_max(gv[s][1]);
+    }
+    for (int s = GR; s < nst; ++s) {
+        acc_max(gat(s, 0));
+        acc_max(gat(s, 1));
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+        sn += __shfl_xor(sn, o, 64);
+    }
+    double p2, sc;
+    plane_scale(mx + sn, *cptr, p2, sc);
+    if (cp == 0) {
+        sc_s[bl] = sc;
+        live_s[bl] = live;
+    }
+    for (int s = 0; s < nst; ++s) {
+        d2 x0, x1;
+        if (s < GR) {
+#pragma unroll
+            for (int q = 0; q < GR; ++q)
+                if (q == s) {
+                    x0 = gv[q][0];
+                    x1 = gv[q][1];
+                }
+        } else {
+            x0 = gat(s, 0);
+            x1 = gat(s, 1);
+        }
+        const double v[4] = {x0.x, x0.y, x1.x, x1.y};
+        uint32_t d[8];
+        digits4(v, p2, d);
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) *reinterpret_cast<uint32_t*>(&Ad[lds_row(bl, tt) * rst + KC * s + 4 * cp]) = d[tt];
+    }
+    __syncthreads();
+
+    const int h = lane >> 5, ldo = 2 * Mc, ncb = (ldo + NCB - 1) / NCB;
+    const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
+    const int total = ncb * nks;   // flat (column block, K-step) sequence, a multiple of 2 SK
+    auto bfl = [&](BSet& b, int f0) {   // codebook fragments of flat steps f0, f0 + 1 (clamped)
+#pragma unroll
+        for (int kk = 0; kk < SK; ++kk) {
+            const int f = min(f0 + kk, total - 1), cb = f / nks, ks = f - cb * nks;
+            const i4v* p = Bf + ((long long)(cb * (NCB / 32) + 2 * w) * nks + ks) * 64 + lane;
+            b.f[kk][0] = p[0];
+            b.f[kk][1] = p[(long long)nks * 64];
+        }
+    };
+    auto epilogue = [&](int cbk, i16v (&acc)[4][2]) {
+        const int ct0 = cbk * (NCB / 32) + 2 * w;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                if (j >= nb || !live_s[blo]) continue;
+                const double scb = sc_s[blo];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int col = (ct0 + c) * 32 + (lane & 31);
+                    if (col < ldo) Wp[(long long)j * ldo + col] = scb * recombine(acc[R][c], q);
+                }
+            }
+#pragma unroll
+        for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+    };
+    i16v acc[4][2];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+    BSet bA, bB;
+    bfl(bA, 0);
+    for (int f = 0; f < total; f += 2 * SK) {
+        bfl(bB, f + SK);
+        __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
+        stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        bfl(bA, f + 2 * SK);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc);
+    }
 }
 
 // Codebook check and expansion.  cmax = max |component| of A (device scalar).  Each
@@ -298,17 +452,24 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
                        i8_nks(n), LH, i8_nks(m), flag);
 }
 
-void launch_i8_apply(int mode, int nb, int Kc, int Mc, const int8_t* Bfrag, const double* V1, const double* V2,
-                     const double* E1, const double* E2, double* C, const double* cmax, const RealState* rs,
-                     hipStream_t st) {
-    dim3 grid((nb + RB - 1) / RB, i8_ncols(Mc) / NCB, 1), block(NT);
-    const i4v* B = reinterpret_cast<const i4v*>(Bfrag);
-    if (mode == 1)
-        hipLaunchKernelGGL(i8apply_kernel<1>, grid, block, 0, st, nb, Kc, Mc, i8_nks(Kc), B, V1, V2, E1, E2, C, cmax,
-                           rs);
-    else
-        hipLaunchKernelGGL(i8apply_kernel<2>, grid, block, 0, st, nb, Kc, Mc, i8_nks(Kc), B, V1, V2, E1, E2, C, cmax,
-                           rs);
+size_t i8ah_lds_bytes(int kc) { return (size_t)ROWS * (32 * i8_nks(kc) + 16); }
+
+void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
+                       const double* M, double* T, const double* cmax, const RealState* rs, hipStream_t st) {
+    dim3 grid((nb + RB - 1) / RB, i8_ncols(m) / NCB, 1), block(NT);
+    hipLaunchKernelGGL(i8a_kernel, grid, block, 0, st, nb, n, m, i8_nks(n), reinterpret_cast<const i4v*>(LA), Z, N,
+                       Y, M, T, cmax, rs);
+}
+void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
+                        const RealState* rs, hipStream_t st) {
+    static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
+    }();
+    (void)attr;
+    dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
+    hipLaunchKernelGGL(i8ah_kernel, grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+                       reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs);
 }
 
 }  // namespace ace

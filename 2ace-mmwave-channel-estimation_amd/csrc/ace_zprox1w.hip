@@ -57,8 +57,8 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
 }
 
 template <bool INIT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zstep1w_kernel(ZArgs a) {
-    const int b = blockIdx.x, lane = threadIdx.x;
+__device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
+    const int lane = threadIdx.x;
     const ZProfile pf = z_profile(a, b);
     const int n = a.n, m = a.m, tx = a.tx, rx = a.rx;
     RealState* st = a.st + b;
@@ -107,6 +107,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     const bool keep_cur = wm && !improved_pre && !(st->opt_obj < INFINITY);   // finalize's fallback X
     d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
     d2* Xc = reinterpret_cast<d2*>(a.Xcur) + (long long)b * n;
+    // m-space dual terms ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0), ||A^H Y||^2 = Y^H K Y, and opt_Y:
+    // they depend only on the Y-step and K Y, so they run first (their loads then do not queue
+    // behind this kernel's stores)
+    double dAtY = 0.0, nAtY = 0.0;
+    if (!INIT) {
+        const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
+        const d2* Yo = reinterpret_cast<const d2*>(a.Yold) + (long long)b * m;
+        const d2* Kn = reinterpret_cast<const d2*>(a.KYnew) + (long long)b * m;
+        const d2* Ko = reinterpret_cast<const d2*>(a.KYold) + (long long)b * m;
+        d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
+        for (int i = lane; i < m; i += 64) {
+            const d2 yn = Yn[i], kn = Kn[i];
+            const d2 dy = csub(yn, Yo[i]), dk = csub(kn, Ko[i]);
+            dAtY += dy.x * dk.x + dy.y * dk.y;
+            nAtY += yn.x * kn.x + yn.y * kn.y;
+            if (improved_pre) oY[i] = yn;   // best-objective iterate (:344-351; iter_control agrees)
+        }
+    }
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long dbg_t1 = dbg_t0, dbg_t2 = dbg_t0, dbg_t3 = dbg_t0, dbg_fa = 0, dbg_fb = 0, dbg_fc = 0;
@@ -678,20 +696,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         return;
     }
 
-    // m-space dual terms: ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0),  ||A^H Y||^2 = Y^H K Y
-    double dAtY = 0.0, nAtY = 0.0;
-    {
-        const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
-        const d2* Yo = reinterpret_cast<const d2*>(a.Yold) + (long long)b * m;
-        const d2* Kn = reinterpret_cast<const d2*>(a.KYnew) + (long long)b * m;
-        const d2* Ko = reinterpret_cast<const d2*>(a.KYold) + (long long)b * m;
-        for (int i = lane; i < m; i += 64) {
-            const d2 yn = Yn[i], kn = Kn[i];
-            const d2 dy = csub(yn, Yo[i]), dk = csub(kn, Ko[i]);
-            dAtY += dy.x * dk.x + dy.y * dk.y;
-            nAtY += yn.x * kn.x + yn.y * kn.y;
-        }
-    }
     const double s_nX2 = wave_sum(acc[0]), s_nZ2 = wave_sum(acc[1]), s_jn2 = wave_sum(acc[2]),
                  s_dZ2 = wave_sum(acc[3]), s_dAtY = wave_sum(dAtY), s_nAtY = wave_sum(nAtY);
     int improved = 0;
@@ -699,11 +703,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
         improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
     improved = __shfl(improved, 0, 64);
     write_vbound();
-    if (improved) {  // opt_X was written by emit (improved == improved_pre)
-        d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
-        const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
-        for (int i = lane; i < m; i += 64) oY[i] = Yn[i];
-    }
 #ifdef ACE_DEBUG_SWEEPS
     if (lane == 0 && a.it == 100) {
         const unsigned long long te = __builtin_amdgcn_s_memrealtime();
@@ -713,6 +712,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     }
 #endif
 }
+
+template <bool INIT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zstep1w_kernel(ZArgs a) {
+    zstep1w_body<INIT>(a, blockIdx.x);
+}
+
 }  // namespace
 
 void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st) {

@@ -40,7 +40,8 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->ns = shared ? cv.take(cz * 4 * m * m) : nullptr;
     L->LA8 = shared ? cv.take<int8_t>(i8_frag_bytes(m, n)) : nullptr;
     L->LAH8 = shared ? cv.take<int8_t>(i8_frag_bytes(n, m)) : nullptr;
-    L->c8 = shared ? cv.take(sizeof(double)) : nullptr;
+    L->LK8 = shared ? cv.take<int8_t>(i8k_frag_bytes(m)) : nullptr;
+    L->c8 = shared ? cv.take(2 * sizeof(double)) : nullptr;
     L->i8flag = shared ? cv.take<int>(sizeof(int)) : nullptr;
     L->i8ok = false;
 }
@@ -65,11 +66,19 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     launch_max_abs(2LL * m * n, L.A, L.c8, st);
     launch_i8_expand(m, n, L.A, L.c8, L.LA8, L.LAH8, L.i8flag, st);
     int flag = 1;
-    double c = 0.0;
+    double c[2] = {0.0, 0.0};
     ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipMemcpyAsync(&c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
+    ACE_HIP(hipMemcpyAsync(c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipStreamSynchronize(st));
-    L.i8ok = flag == 0 && c > 0.0 && std::isfinite(c) && i8ah_lds_bytes(m) <= 160 * 1024 - 256;
+    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= 160 * 1024 - 256;
+    if (!L.i8ok) return ACE_OK;
+    c[1] = c[0] * c[0];
+    ACE_HIP(hipMemcpyAsync(L.c8 + 1, c + 1, sizeof(double), hipMemcpyHostToDevice, st));
+    ACE_HIP(hipMemsetAsync(L.LK8, 0, i8k_frag_bytes(m), st));
+    launch_i8k_expand(m, L.K, L.c8, L.LK8, L.i8flag, st);
+    ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    ACE_HIP(hipStreamSynchronize(st));
+    L.i8ok = flag == 0;
     return ACE_OK;
 }
 
@@ -247,7 +256,11 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
             }
         }
-        { ProfScope ps(ACE_K_APPLY_K, st); applyMM(L.K, w.Y[1 - q], w.KY[1 - q]); }  // K Y
+        {   // K Y
+            ProfScope ps(ACE_K_APPLY_K, st);
+            if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
+            else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
+        }
         {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
             if (wmode) launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st);

@@ -109,6 +109,11 @@ void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, 
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st);
 size_t i8ah_lds_bytes(int kc);
+// KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
+size_t i8k_frag_bytes(int m);
+void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);
+void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
+                       const RealState* rs, hipStream_t st);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
 // out[0] = max |x_i| over n doubles

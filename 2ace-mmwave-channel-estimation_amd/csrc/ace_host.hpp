@@ -117,7 +117,8 @@ struct LinOps {
     // A and A^H for the exact digit-plane applies (ace_i8gemm.hip); i8ok is set by linops_setup
     int8_t* LA8;
     int8_t* LAH8;
-    double* c8;   // device: c
+    int8_t* LK8;  // the two base-128 digit planes of K / c^2
+    double* c8;   // device: c, c^2
     int* i8flag;  // device: set when some component is not in {0, +-c}
     bool i8ok;
 };

@@ -278,6 +278,14 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
 // work-group sweeps every 512-column block of the output as one flat sequence of K-steps,
 // so the exponent pre-pass and the staging run once per 16 realisations and the codebook
 // pipeline runs across block boundaries.
+//
+// KY (apply_K, KY = K Y with K = A A^H = c^2 K_int, K_int a Gaussian-integer matrix with
+// |entries| <= 2n): the codebook operand holds the two base-128 digit planes of the real
+// expansion of K_int, interleaved by 32-column tile (low digit, high digit) so that a wave's
+// two accumulator tiles are the two planes of the same 32 output columns; they are combined
+// exactly in int32 (acc_lo + 128 acc_hi) before the recombination.  A work-group then covers
+// 256 output columns per block.
+template <bool KY>
 __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
                                                      const double* __restrict__ Gp, double* __restrict__ Wp,
                                                      const double* __restrict__ cptr,
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     }
     __syncthreads();
 
-    const int h = lane >> 5, ldo = 2 * Mc, ncb = (ldo + NCB - 1) / NCB;
+    const int h = lane >> 5, ldo = 2 * Mc, ocb = KY ? NCB / 2 : NCB, ncb = (ldo + ocb - 1) / ocb;
     const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
     const int total = ncb * nks;   // flat (column block, K-step) sequence, a multiple of 2 SK
     auto bfl = [&](BSet& b, int f0) {   // codebook fragments of flat steps f0, f0 + 1 (clamped)
@@ -366,6 +374,23 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
         }
     };
     auto epilogue = [&](int cbk, i16v (&acc)[4][2]) {
+        if constexpr (KY) {   // one 32-column output tile per wave: low + 128 x high digit plane
+            const int col = (cbk * (NCB / 64) + w) * 32 + (lane & 31);
+#pragma unroll
+            for (int R = 0; R < 4; ++R)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                    if (j >= nb || !live_s[blo] || col >= ldo) continue;
+                    i16v cmb;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) cmb[e] = acc[R][0][e] + 128 * acc[R][1][e];
+                    Wp[(long long)j * ldo + col] = sc_s[blo] * recombine(cmb, q);
+                }
+#pragma unroll
+            for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+            return;
+        }
         const int ct0 = cbk * (NCB / 32) + 2 * w;
 #pragma unroll
         for (int R = 0; R < 4; ++R)
@@ -437,6 +462,31 @@ __global__ __launch_bounds__(256) void i8_expand_kernel(int m, int n, const doub
     LH[frag_off(2 * k + 1, 2 * i, nksH)] = (int8_t)(-q);
     LH[frag_off(2 * k + 1, 2 * i + 1, nksH)] = (int8_t)p;
 }
+// K_int = rint(K / c^2) (exact: K = A A^H of a phase code is c^2 times a Gaussian-integer
+// matrix, and its f64 rounding error is far below c^2 / 2).  Real expansion entry (oc, kk)
+// of K_int as base-128 digits lo in [0, 127], hi = floor(v / 128); plane p of output tile
+// oc / 32 is codebook tile 2 (oc / 32) + p.
+__global__ __launch_bounds__(256) void i8k_expand_kernel(int m, const double* __restrict__ Kp,
+                                                          const double* __restrict__ cmax, int8_t* __restrict__ LK,
+                                                          int nks, int* flag) {
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= (long long)m * m) return;
+    const int i = (int)(e / m), k = (int)(e % m);
+    const d2 kv = reinterpret_cast<const d2*>(Kp)[e];
+    const double c2 = cmax[1];
+    const double kr = rint(kv.x / c2), ki = rint(kv.y / c2);
+    if (fabs(kr) > 8192.0 || fabs(ki) > 8192.0) atomicOr(flag, 2);
+    auto put = [&](int oc, int kk, double v) {
+        const int iv = (int)v, hi = iv >> 7, lo = iv & 127;   // iv = 128 hi + lo
+        const int t = oc >> 5, cc = oc & 31;
+        LK[frag_off(32 * (2 * t) + cc, kk, nks)] = (int8_t)lo;
+        LK[frag_off(32 * (2 * t + 1) + cc, kk, nks)] = (int8_t)hi;
+    };
+    put(2 * i, 2 * k, kr);
+    put(2 * i, 2 * k + 1, -ki);
+    put(2 * i + 1, 2 * k, ki);
+    put(2 * i + 1, 2 * k + 1, kr);
+}
 }  // namespace
 
 // padded K-steps (of 32 reals) for a complex inner dimension kc: multiple of one stage
@@ -460,15 +510,32 @@ void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, 
     hipLaunchKernelGGL(i8a_kernel, grid, block, 0, st, nb, n, m, i8_nks(n), reinterpret_cast<const i4v*>(LA), Z, N,
                        Y, M, T, cmax, rs);
 }
-void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
-                        const RealState* rs, hipStream_t st) {
-    static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel),
+size_t i8k_frag_bytes(int m) { return (size_t)2 * ((2 * m + NCB / 2 - 1) / (NCB / 2)) * (NCB / 2) * i8_nks(m) * 32; }
+void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st) {
+    const long long tot = (long long)m * m;
+    hipLaunchKernelGGL(i8k_expand_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, K, cmax, LK,
+                       i8_nks(m), flag);
+}
+void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
+                       const RealState* rs, hipStream_t st) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<true>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
     }();
     (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
-    hipLaunchKernelGGL(i8ah_kernel, grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+    hipLaunchKernelGGL(i8ah_kernel<true>, grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
+                       reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs);
+}
+void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
+                        const RealState* rs, hipStream_t st) {
+    static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
+    }();
+    (void)attr;
+    dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
+    hipLaunchKernelGGL(i8ah_kernel<false>, grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
                        reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs);
 }
 

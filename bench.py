@@ -37,7 +37,9 @@ sys.path.insert(0, str(ROOT / "2ace-mmwave-channel-estimation_amd"))
 METRIC = "channel recoveries/sec (32-ant, 256 RSS meas, 200 ADMM iters) @1/2/4/8 GPU"
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= FP64 vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
-PROF_STRIDE = 8           # unit mode: kernel events on every 8th launch of the non-roofline classes
+PEAK_I8_TOPS = 5000.0     # MI355X int8 matrix dense peak, spec (2x the BF16 rate per clock)
+PROF_STRIDE = 3           # unit mode: kernel events on every 3rd launch of each class (200 iterations per
+                          # step, 200 mod 3 != 0: over 3 steps every iteration index is sampled equally)
 
 
 def parse():
@@ -271,17 +273,27 @@ def unit_flops(m, n, tx, rx):
     }
 
 
+def unit_i8_ops(m, n):
+    """int8 matrix-core ops executed per realisation per launch by the digit-plane applies
+    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC."""
+    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m)}
+
+
 def unit_bytes(m, n, tx, rx):
-    """Algorithmic HBM bytes per realisation per iteration of the memory-bound kernel classes
-    (complex128 = 16 B; each array read / written once):
-      zstep: read X, N, Z_old, Q (tx x tx), Y_new, Y_old, KY_new, KY_old; write N, Z
-      pre:   read Z, N, Y, M; write V, S
-      ystep: read S, g, M, B (8 B), Y_old; write M, Y_new"""
+    """Algorithmic HBM bytes per realisation per iteration (complex128 = 16 B, each array read or
+    written once):
+      zstep (wmode):  read W = A^H g, N, Z, the top-16 columns of Q (tx x 16), Y, Y_old, KY, KY_old;
+                      write Z', N', opt_X, opt_Y (the best-objective copies fire on almost every
+                      iteration of a fixed-length solve)
+      apply_A (i8):   read Z, N, Y, M; write T
+      apply_AH (i8):  read g; write W"""
     return {
-        "zstep": 16.0 * (5 * n + tx * tx + 4 * m),
-        "pre": 16.0 * (3 * n + 3 * m),
-        "ystep": 16.0 * 6 * m + 8.0 * m,
+        "zstep": 16.0 * (6 * n + 5 * m) + 16.0 * 16 * tx,
+        "apply_A": 16.0 * (2 * n + 3 * m),
+        "apply_AH": 16.0 * (m + n),
     }
+
+
 def cpu_baseline(args, n_samples):
     """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
     timed on the host cores on a bounded sample of the same workload."""
@@ -307,6 +319,33 @@ def cpu_baseline(args, n_samples):
                        f"n={n}, shared codebook) on {cores} threads of "
                        f"{_cpu_model()}; U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}; "
                        f"solve {t_solve:.2f}s")}
+
+
+PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel"}
+
+
+def _pmc_traffic(cls):
+    """HBM bytes per launch (PMC FETCH_SIZE, gfx950-corrected, + WRITE_SIZE) of a kernel class from
+    the newest committed profiles/*_pmc_hbm.json (written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc passes of this benchmark), or None."""
+    name = PMC_KERNEL.get(cls)
+    def version(f):   # r<round>_v<version>_pmc_hbm.json
+        parts = f.name.split("_")
+        try:
+            return int(parts[0][1:]), int(parts[1][1:])
+        except (IndexError, ValueError):
+            return -1, -1
+    files = sorted((ROOT / "profiles").glob("r*_pmc_hbm.json"), key=version)
+    if not name or not files:
+        return None
+    try:
+        d = json.loads(files[-1].read_text())
+    except (OSError, ValueError):
+        return None
+    for k, v in d.items():
+        if k.split(" grid=")[0].strip().startswith(name):
+            return round(v["hbm_bytes"]), f"profiles/{files[-1].name}"
+    return None
 
 
 def _cpu_model():
@@ -368,10 +407,8 @@ def main():
     if world > 1:
         dist.barrier()
     prof = not args.no_prof
-    if prof:   # HIP event pairs on every launch of the roofline kernels, every 8th of the rest
-        full = (1 << KERNEL_CLASSES.index("zstep")) | (1 << KERNEL_CLASSES.index("apply_A")) | \
-               (1 << KERNEL_CLASSES.index("apply_AH"))
-        check(LIB.ace_prof_sample(PROF_STRIDE, full))
+    if prof:   # HIP event pairs on every PROF_STRIDE-th launch of each kernel class
+        check(LIB.ace_prof_sample(PROF_STRIDE, 0))
         check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
     torch.cuda.synchronize()
     if world > 1:
@@ -406,8 +443,23 @@ def main():
                 if kn[i]:
                     kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
 
+            # the int8 digit-plane applies run for a phase-code codebook in the A2only r = 1 iteration
+            i8 = (not args.private) and args.variant == "A2only" and os.environ.get("ACE_NO_I8") != "1"
+            io = unit_i8_ops(m, n)
+
             def roofline(k):
                 avg_s = kernels[k]["avg_ms"] * 1e-3
+                if k in io and i8:   # exact int8 digit planes on the matrix cores
+                    per, pb = io[k] * bsz, ub[k] * bsz
+                    return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
+                            "unit": "TOP/s", "frac": round(per / avg_s / 1e12 / PEAK_I8_TOPS, 4), "traffic": None,
+                            "kernel": k, "ops_per_launch": per,
+                            "hbm": {"achieved": round(pb / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                    "frac": round(pb / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": pb},
+                            "f64_equiv_tflops": round(uf[k] * bsz / avg_s / 1e12, 1),
+                            "op_note": "int8 x int8 -> int32 ops of the 8 digit planes x the 2x2 real expansion "
+                                       "(exact: the codebook is a phase code); f64_equiv_tflops counts the same "
+                                       "product as 8 flops per complex MAC"}
                 if k in uf:   # MFMA-bound complex f64 GEMM
                     per = uf[k] * bsz
                     # algorithmic = conventional 8 flops per complex MAC; the 3M kernel executes 6
@@ -427,9 +479,11 @@ def main():
             dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
             roof = roofline(dom)
             roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
-                            f"region: every launch of zstep/apply_A/apply_AH, every {PROF_STRIDE}th of the other "
-                            f"classes); FP64 dense peak "
-                            "(matrix = vector on MI355X) / HBM3E 8 TB/s; traffic: PMC summary in profiles/")
+                            f"region, on every {PROF_STRIDE}rd launch of each kernel class); peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); "
+                            "traffic: PMC FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source")
+            tr = _pmc_traffic(dom)
+            if tr:
+                roof["traffic"], roof["traffic_source"] = tr
             gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
             roof_gemm = roofline(gemm)
         cpu = None

@@ -45,7 +45,7 @@ class AdmmCfg(C.Structure):
         ("fixed_iters", C.c_int),
         ("a_shared", C.c_int),
         ("eig_warm", C.c_int),
-        ("reserved", C.c_int),
+        ("f64_applies", C.c_int),
         ("mu0", C.c_double),
         ("rho", C.c_double),
         ("tol_rel", C.c_double),

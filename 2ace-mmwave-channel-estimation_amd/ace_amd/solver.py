@@ -46,12 +46,12 @@ class BatchResult:
 
 
 def _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-         eig_warm):
+         eig_warm, f64_applies=False):
     return default_cfg(variant=VARIANTS[variant], scale_by_row=int(bool(scale_by_row)),
                        use_rank_one=int(bool(use_rank_one)), mu0=float(mu0), rho=float(rho),
                        tol_rel=float(tol_rel), tol_abs=float(tol_abs), maxiter=int(maxiter),
                        fixed_iters=int(bool(fixed_iters)), a_shared=int(bool(a_shared)),
-                       eig_warm=int(bool(eig_warm)))
+                       eig_warm=int(bool(eig_warm)), f64_applies=int(bool(f64_applies)))
 
 
 def _dp(a):
@@ -84,8 +84,10 @@ def InferADMM(A, B, X0, scale_by_row, use_rank_one, tx, rx, lambda_=0.0, mu0=1e-
 
 
 def infer_admm_host(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, use_rank_one=False, mu0=1e-3,
-                    rho=1.03, tol_rel=1e-4, tol_abs=1e-8, maxiter=500, fixed_iters=False, eig_warm=True):
-    """Batch solve on host numpy arrays: A [1|batch][m][n], B [batch][m], X0 [batch][n]."""
+                    rho=1.03, tol_rel=1e-4, tol_abs=1e-8, maxiter=500, fixed_iters=False, eig_warm=True,
+                    f64_applies=False):
+    """Batch solve on host numpy arrays: A [1|batch][m][n], B [batch][m], X0 [batch][n].
+    ``f64_applies`` keeps the f64 matrix-core applies for phase-code codebooks too."""
     A = np.ascontiguousarray(A, dtype=np.complex128)
     B = np.ascontiguousarray(B, dtype=np.float64)
     X0 = np.ascontiguousarray(X0, dtype=np.complex128)
@@ -95,7 +97,7 @@ def infer_admm_host(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, us
         raise ValueError(f"shape mismatch: A{A.shape} B{B.shape} X0{X0.shape}")
     a_shared = A.shape[0] == 1
     cfg = _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-               eig_warm)
+               eig_warm, f64_applies)
     X = np.empty((batch, n), np.complex128)
     Y = np.empty((batch, m), np.complex128)
     it = np.empty(batch, np.int32)
@@ -126,7 +128,7 @@ _DEFAULT_WS = Workspace()
 
 def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, use_rank_one=False, mu0=1e-3,
                      rho=1.03, tol_rel=1e-4, tol_abs=1e-8, maxiter=500, fixed_iters=False, eig_warm=True,
-                     out=None, workspace=None, stream=None):
+                     f64_applies=False, out=None, workspace=None, stream=None):
     """Batched InferADMM on device tensors (torch, complex128 / float64, contiguous).
 
     A: [1|batch][m][n] (1 = shared codebook), B: [batch][m], X0: [batch][n].
@@ -145,7 +147,7 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
         raise ValueError(f"shape mismatch: A{tuple(A.shape)} B{tuple(B.shape)} X0{tuple(X0.shape)}")
     a_shared = A.shape[0] == 1
     cfg = _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-               eig_warm)
+               eig_warm, f64_applies)
     dev = A.device
     if out is None:
         out = BatchResult(torch.empty((batch, n), dtype=torch.complex128, device=dev),

@@ -44,6 +44,7 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->c8 = shared ? cv.take(2 * sizeof(double)) : nullptr;
     L->i8flag = shared ? cv.take<int>(sizeof(int)) : nullptr;
     L->i8ok = false;
+    L->allow_i8 = true;
 }
 
 // ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
@@ -59,7 +60,7 @@ static bool i8_disabled() {
 static int i8_setup(LinOps& L, hipStream_t st) {
     const int m = L.m, n = L.n;
     L.i8ok = false;
-    if (i8_disabled()) return ACE_OK;
+    if (!L.allow_i8 || i8_disabled()) return ACE_OK;
     ACE_HIP(hipMemsetAsync(L.LA8, 0, i8_frag_bytes(m, n), st));
     ACE_HIP(hipMemsetAsync(L.LAH8, 0, i8_frag_bytes(n, m), st));
     ACE_HIP(hipMemsetAsync(L.i8flag, 0, sizeof(int), st));

@@ -114,6 +114,7 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     linops_carve(cv, cfg->a_shared != 0, batch, m, n, &L);
     admm_state_carve(cv, batch, m, n, 1, &w);
     L.A = A;
+    L.allow_i8 = cfg->f64_applies == 0;
     ACE_TRY(linops_setup(L, batch, st));
     AdmmParams p{};
     p.variant = cfg->variant;

@@ -121,6 +121,7 @@ struct LinOps {
     double* c8;   // device: c, c^2
     int* i8flag;  // device: set when some component is not in {0, +-c}
     bool i8ok;
+    bool allow_i8;  // caller's choice (ace_admm_cfg::f64_applies == 0), set before linops_setup
 };
 size_t linops_bytes(bool shared, int batch, int m, int n);
 void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L);

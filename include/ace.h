@@ -83,7 +83,8 @@ typedef struct ace_admm_cfg {
     int fixed_iters;   /* 1: throughput mode -- run exactly maxiter iterations (no early exit) */
     int a_shared;      /* 1: one A for the whole batch (shared codebook); 0: private A per realisation */
     int eig_warm;      /* 1: warm-start the Z-prox Jacobi from the previous iteration's eigenvectors */
-    int reserved;
+    int f64_applies;   /* 0: a shared phase-code A (every component in {0, +-c}) runs A v, A^H g and K Y
+                          as exact int8 digit-plane products (f64 accuracy); 1: f64 matrix cores always */
     double mu0;        /* 1e-3   (:7) */
     double rho;        /* 1.03   (:8) */
     double tol_rel;    /* 1e-4   (:10) */

@@ -180,3 +180,52 @@ def test_error_paths(gpu):
     A3, B3, X03, _ = _problem(1, 1, 16, 3)
     with pytest.raises(AceError):
         infer_admm_host(A3, B3, X03, 3, 3)         # odd tx unsupported for the Jacobi Z-prox
+
+
+@pytest.mark.parametrize("fixed", [True, False])
+def test_int8_applies_match_f64(gpu, fixed):
+    """The exact int8 digit-plane applies (phase-code codebook, ace_i8gemm.hip) against the f64
+    matrix-core applies and the C oracle at the unit's size (32 antennas, m = 256)."""
+    from ace_amd import infer_admm_host
+    A, B, X0, _ = _problem(17, 6, 256, 32)
+    kw = dict(variant="A2only", maxiter=200, fixed_iters=fixed)
+    r8 = infer_admm_host(A, B, X0, 32, 32, **kw)
+    r64 = infer_admm_host(A, B, X0, 32, 32, f64_applies=True, **kw)
+    e = _errs(r8.X, r64.X)
+    assert e.max() <= 1e-9, e
+    assert np.array_equal(r8.iters, r64.iters)
+    Xo, _, ito, _, _ = _oracle(A, B, X0, 32, variant=0, maxiter=200, fixed_iters=fixed)
+    assert _errs(r8.X, Xo).max() <= TOL
+    assert np.array_equal(r8.iters, ito)
+
+
+def test_generic_codebook_runs_f64_path(gpu):
+    """A shared codebook that is not a phase code (complex Gaussian) takes the f64 applies."""
+    from ace_amd import infer_admm_host
+    rng = np.random.default_rng(5)
+    A, B, X0, _ = _problem(19, 4, 64, 16)
+    A = (rng.standard_normal(A.shape) + 1j * rng.standard_normal(A.shape)) / np.sqrt(2 * 256)
+    H = (rng.standard_normal((4, 256)) + 1j * rng.standard_normal((4, 256)))
+    B = np.abs(np.einsum("mn,bn->bm", A[0], H))
+    res = infer_admm_host(A, B, X0, 16, 16, variant="A2only")
+    Xo, _, ito, _, _ = _oracle(A, B, X0, 16, variant=0)
+    assert _errs(res.X, Xo).max() <= TOL
+    assert np.array_equal(res.iters, ito)
+
+
+def test_phase_code_with_switched_off_antennas(gpu):
+    """Multiresolution-style codebook: phase codes with switched-off antennas (0 entries) stay
+    on the int8 path ({0, +-c} components) and match the oracle."""
+    from ace_amd import infer_admm_host
+    A, B, X0, _ = _problem(23, 4, 128, 16)
+    A = A.copy()
+    A[0, :, ::3] = 0.0          # every third antenna off on every probe
+    A[0, ::5, 1::3] = 0.0       # and a second group off on every fifth probe
+    rng = np.random.default_rng(2)
+    H = (rng.standard_normal((4, 256)) + 1j * rng.standard_normal((4, 256)))
+    B = np.abs(np.einsum("mn,bn->bm", A[0], H))
+    res = infer_admm_host(A, B, X0, 16, 16, variant="A2only", maxiter=200, fixed_iters=True)
+    r64 = infer_admm_host(A, B, X0, 16, 16, variant="A2only", maxiter=200, fixed_iters=True, f64_applies=True)
+    assert _errs(res.X, r64.X).max() <= 1e-9
+    Xo, _, ito, _, _ = _oracle(A, B, X0, 16, variant=0, maxiter=200, fixed_iters=True)
+    assert _errs(res.X, Xo).max() <= TOL

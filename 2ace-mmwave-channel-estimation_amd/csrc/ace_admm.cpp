@@ -43,7 +43,9 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->LK8 = shared ? cv.take<int8_t>(i8k_frag_bytes(m)) : nullptr;
     L->c8 = shared ? cv.take(2 * sizeof(double)) : nullptr;
     L->i8flag = shared ? cv.take<int>(sizeof(int)) : nullptr;
+    L->Gf = shared && m <= GYK_MAXM ? cv.take(gyk_gfrag_bytes(m)) : nullptr;
     L->i8ok = false;
+    L->gyk_ok = false;
     L->allow_i8 = true;
 }
 
@@ -80,6 +82,8 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipStreamSynchronize(st));
     L.i8ok = flag == 0;
+    L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= (size_t)GYK_MAXDYN;
+    if (L.gyk_ok) launch_gyk_gfrag(m, L.G, L.Gf, st);
     return ACE_OK;
 }
 
@@ -177,6 +181,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // phase-code A: int8 digit-plane applies; apply_AH writes W = A^H g and the Z-step forms X
     const bool i8 = fused && L.i8ok && zstep_takes_w(p.variant, r);
     const bool wmode = i8;
+    const bool gyk = wmode && L.gyk_ok;               // g, Y-step, K Y and the dual terms in one kernel
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -245,7 +250,11 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
             { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }      // T = S - A V
         }
-        if (fused) {  // g = G T with the Y-step in its epilogue
+        if (gyk) {
+            ProfScope ps(ACE_K_APPLY_G, st);
+            const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st};
+            launch_gyk(batch, m, ga, st);
+        } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st);
             const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
             launch_zgemm_ystep(m, batch, L.G, w.T, w.g, ys, w.st, st);
@@ -257,7 +266,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
             }
         }
-        {   // K Y
+        if (!gyk) {   // K Y
             ProfScope ps(ACE_K_APPLY_K, st);
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
@@ -276,7 +285,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             za.Zn = Zo;
             za.Nn = No;
         }
-        za.ypart = fused ? w.ypart : nullptr;
+        za.ypart = fused && !gyk ? w.ypart : nullptr;
+        za.yfused = gyk;
         za.ytiles = (m + 63) / 64;
         za.Ynew = w.Y[1 - q];
         za.Yold = w.Y[q];

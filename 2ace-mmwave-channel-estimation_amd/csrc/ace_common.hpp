@@ -25,7 +25,9 @@ struct RealState {
     // written by the Z-step: upper bound on max|Re|,|Im| of V = Z - N/mu for the next iteration's
     // apply (the exponent of the int8 digit planes, ace_i8gemm.hip); NaN when Z or N is not finite
     double vbound;
-    double pad1, pad2;
+    // written by the fused g / Y-step / K Y kernel (ace_i8gemm.hip::gyk_kernel):
+    // ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0) and ||A^H Y||^2 = Y^H K Y
+    double dAtY, nAtY;
     int32_t iters, done, status, objcol;  // objcol: argmin column of the per-column objective
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
@@ -109,6 +111,30 @@ void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, 
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st);
 size_t i8ah_lds_bytes(int kc);
+// Fused g = G T (3M f64 MFMA), Y-step, K Y (int8 digit planes), dual terms and opt_Y for
+// 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
+// fragment order (launch_gyk_gfrag at setup).
+constexpr int GYK_MAXM = 256;
+constexpr int GYK_MAXDYN = 160 * 1024 - 8192;   // dynamic LDS limit of gyk_kernel
+size_t gyk_gfrag_bytes(int m);
+size_t gyk_lds_bytes(int m);
+void launch_gyk_gfrag(int m, const double* G, double* Gf, hipStream_t st);
+struct GykArgs {
+    const double* Gf;
+    const double* T;
+    const double* B;
+    const double* Yo;
+    double* M;
+    double* Yn;
+    double* g;
+    const double* KYo;
+    double* KYn;
+    double* optY;
+    const int8_t* LK;   // K digit planes (launch_i8k_expand)
+    const double* c8;   // c, c^2
+    RealState* rs;
+};
+void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);
@@ -156,6 +182,8 @@ struct ZArgs {
     // rewrites them when the tail rescaling fires.
     double* Zn;
     double* Nn;
+    // the Y-step sums, the dual terms (RealState::dAtY, nAtY) and opt_Y come from gyk_kernel
+    int yfused;
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

@@ -121,6 +121,8 @@ struct LinOps {
     double* c8;   // device: c, c^2
     int* i8flag;  // device: set when some component is not in {0, +-c}
     bool i8ok;
+    double* Gf;     // G in f64 MFMA fragment order for gyk_kernel (m <= GYK_MAXM), set when gyk_ok
+    bool gyk_ok;
     bool allow_i8;  // caller's choice (ace_admm_cfg::f64_applies == 0), set before linops_setup
 };
 size_t linops_bytes(bool shared, int batch, int m, int n);

@@ -50,6 +50,8 @@ constexpr int NCB = 512;         // output reals per work-group
 constexpr int NT = 512;          // threads (8 waves)
 constexpr int KSC = KC / 32;     // MFMA K-steps per granule
 
+__device__ __forceinline__ int i8_nks_dev(int kc) { return (2 * kc + KC - 1) / KC * KSC; }
+
 // LDS row of (realisation bl in 0..15, digit t in 0..7): inverse of the accumulator map
 // row = (g & 3) + 8 (g >> 2) + 4 h  ->  realisation 4R + 2 (g >> 3) + h, digit (g & 3) + 4 ((g >> 2) & 1)
 __device__ __forceinline__ int lds_row(int bl, int t) {
@@ -462,6 +464,355 @@ __global__ __launch_bounds__(256) void i8_expand_kernel(int m, int n, const doub
     LH[frag_off(2 * k + 1, 2 * i, nksH)] = (int8_t)(-q);
     LH[frag_off(2 * k + 1, 2 * i + 1, nksH)] = (int8_t)p;
 }
+// ---- fused r = 1 middle of the iteration for 16-realisation blocks (m <= GYK_MAXM):
+//   g = G T on the f64 matrix cores (3M form; G streamed from L2 in fragment order, T from LDS)
+//   Y-step (ArgMinY, M update, :326-337) with the five sums completed in the work-group
+//   K Y_new on the int8 matrix cores (digit planes of Y_new from LDS, as i8ah_kernel<true>)
+//   the dual terms dY^H (K Y - K Y0), Y^H K Y and the opt_Y copy
+// so that neither the Z-step nor a separate K Y launch touches Y or K Y again.
+constexpr int GSK = 4;          // f64 K-steps (4 complex each) per pipeline stage
+constexpr int GRB = 16;         // realisations per work-group (one f64 MFMA row tile)
+__host__ __device__ __forceinline__ int gyk_mp(int m) { return (m + 31) & ~31; }
+struct GSet {
+    d2 f[GSK][2];
+};
+
+__global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ double red[8][GRB][7];
+    __shared__ double sc_s[GRB], p2_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB];
+    const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
+    const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
+    d2* Ts = reinterpret_cast<d2*>(smem);               // [16][tst]: T, then Y_new
+    int8_t* Ad = reinterpret_cast<int8_t*>(smem) + ((GRB * tst * 16 + 255) & ~255);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB;
+    if (t < GRB) {
+        const int j = j0 + t;
+        live_s[t] = j < nb && !a.rs[j].done;
+    }
+    __syncthreads();
+    for (int idx = t; idx < GRB * mp; idx += NT) {
+        const int jl = idx / mp, k = idx - jl * mp, j = j0 + jl;
+        Ts[jl * tst + k] = (live_s[jl] && k < m) ? reinterpret_cast<const d2*>(a.T)[(long long)j * m + k]
+                                                 : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+
+    // the Y-step inputs of the lane's 8 elements, loaded before the G T loop so that they land
+    // while it runs (unconditional, clamped addresses; per-element branches would serialise
+    // 8 memory round trips)
+    d2 mi[2][4], yov[2][4];
+    double biv[2][4], muv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int jl = (lane >> 4) + 4 * r;
+        muv[r] = a.rs[live_s[jl] ? j0 + jl : j0].mu;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int i = min(16 * (2 * w + c) + (lane & 15), m - 1);
+            const long long off = (long long)(live_s[jl] ? j0 + jl : j0) * m + i;
+            mi[c][r] = reinterpret_cast<const d2*>(a.M)[off];
+            yov[c][r] = reinterpret_cast<const d2*>(a.Yo)[off];
+            biv[c][r] = a.B[off];
+        }
+    }
+    // ---- g = G T: wave w owns output tiles 2w, 2w + 1 (16 complex each)
+    const int nct = mp / 16, nks = mp / 4, nstage = nks / GSK;
+    const int ct0 = min(2 * w, nct - 1), ct1 = min(2 * w + 1, nct - 1);
+    const d2* gp0 = reinterpret_cast<const d2*>(a.Gf) + (long long)ct0 * 64 + lane;
+    const d2* gp1 = reinterpret_cast<const d2*>(a.Gf) + (long long)ct1 * 64 + lane;
+    auto gload = [&](GSet& gs, int s) {
+#pragma unroll
+        for (int kk = 0; kk < GSK; ++kk) {
+            const long long ks = min(GSK * s + kk, nks - 1);
+#ifdef ACE_GYK_PROBE_NO_G
+            gs.f[kk][0] = make_double2(1.0 + ks, 0.5);
+            gs.f[kk][1] = make_double2(0.5, 1.0 + ks);
+#else
+            gs.f[kk][0] = gp0[ks * nct * 64];
+            gs.f[kk][1] = gp1[ks * nct * 64];
+#endif
+        }
+    };
+    d4v p1[2], p2[2], p3[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) p1[c] = p2[c] = p3[c] = d4v{0.0, 0.0, 0.0, 0.0};
+    const d2* trow = Ts + (lane & 15) * tst + (lane >> 4);
+    struct TSet {
+        d2 v[GSK];
+    };
+    auto tload = [&](TSet& ts, int s) {   // T fragments of a stage, one stage ahead of their use
+        const int s2 = min(s, nstage - 1);
+#pragma unroll
+        for (int kk = 0; kk < GSK; ++kk) ts.v[kk] = trow[4 * (GSK * s2 + kk)];
+    };
+    auto gcomp = [&](const GSet& gs, const TSet& ts) {
+#pragma unroll
+        for (int kk = 0; kk < GSK; ++kk) {
+            const d2 v = ts.v[kk];
+            const double ar = v.x, ai = v.y, as = v.x + v.y;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const d2 l = gs.f[kk][c];
+                p1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, l.x, p1[c], 0, 0, 0);
+                p2[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, l.y, p2[c], 0, 0, 0);
+                p3[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(as, l.x + l.y, p3[c], 0, 0, 0);
+            }
+        }
+    };
+    {
+        GSet gA, gB;
+        TSet tA, tB;
+        gload(gA, 0);
+        tload(tA, 0);
+        for (int s = 0; s < nstage; s += 2) {   // nstage is even (mp multiple of 32)
+            gload(gB, s + 1);
+            tload(tB, s + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            gcomp(gA, tA);
+            __builtin_amdgcn_sched_barrier(0);
+            gload(gA, s + 2);
+            tload(tA, s + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            gcomp(gB, tB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __syncthreads();   // every wave is done with T: Ts becomes Y_new
+#ifdef ACE_GYK_PROBE_ONLY_A
+    {
+        double sacc = 0.0;
+        for (int c = 0; c < 2; ++c)
+            for (int r = 0; r < 4; ++r) sacc += p1[c][r] + p2[c][r] + p3[c][r];
+        if (sacc == 12345.678) a.g[0] = sacc;
+    }
+    return;
+#endif
+
+    // ---- Y-step on this lane's 2 x 4 outputs: realisation (lane >> 4) + 4 r, output 16 ct + (lane & 15)
+    double v7[4][7];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v7[r][k] = 0.0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int ct = 2 * w + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int jl = (lane >> 4) + 4 * r, j = j0 + jl, i = 16 * ct + (lane & 15);
+            if (ct >= nct || i >= m || !live_s[jl]) continue;
+            const long long off = (long long)j * m + i;
+            const double e1 = p1[c][r], e2 = p2[c][r];
+            const d2 gv = make_double2(e1 - e2, p3[c][r] - e1 - e2);
+            const double mu = muv[r], imu = 1.0 / mu;
+            const d2 mii = mi[c][r], yo = yov[c][r];
+            const double Bi = biv[c][r];
+            const d2 ax = csub(csub(yo, cscale(mii, imu)), gv);
+            d2 cc = cadd(ax, cscale(mii, imu));
+            double d = sqrt(cabs2(cc));
+            if (d == 0.0) {   // ArgMinY zero guard (:516-520 / :524-528)
+                cc = make_double2(1.0, 0.0);
+                d = 1.0;
+            }
+            const double f = (Bi / d + mu) / (1.0 + mu);
+            const d2 y = cscale(cc, f);
+            const d2 jv = csub(ax, y);
+            reinterpret_cast<d2*>(a.g)[off] = gv;
+            reinterpret_cast<d2*>(a.M)[off] = cadd(mii, cscale(jv, mu));
+            reinterpret_cast<d2*>(a.Yn)[off] = y;
+            Ts[jl * tst + i] = y;
+            const double aax = sqrt(cabs2(ax)) - Bi;
+            v7[r][0] += aax * aax;
+            v7[r][1] += cabs2(ax);
+            v7[r][2] += cabs2(y);
+            v7[r][3] += cabs2(jv);
+            v7[r][4] += cabs2(csub(y, yo));
+            const double ay = fmax(fabs(y.x), fabs(y.y));
+            v7[r][5] = fmax(v7[r][5], ay);
+            v7[r][6] += 0.0 * (fabs(y.x) + fabs(y.y));   // NaN / Inf sticky
+        }
+    }
+#ifdef ACE_GYK_PROBE_P1
+    return;
+#endif
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) v7[r][k] += __shfl_xor(v7[r][k], o, 64);
+            v7[r][5] = fmax(v7[r][5], __shfl_xor(v7[r][5], o, 64));
+            v7[r][6] += __shfl_xor(v7[r][6], o, 64);
+        }
+        if ((lane & 15) == 0)
+#pragma unroll
+            for (int k = 0; k < 7; ++k) red[w][(lane >> 4) + 4 * r][k] = v7[r][k];
+    }
+    __syncthreads();
+    if (t < GRB) {
+        double v[7] = {0, 0, 0, 0, 0, 0, 0};
+        for (int q = 0; q < 8; ++q) {   // fixed order over the waves
+#pragma unroll
+            for (int k = 0; k < 5; ++k) v[k] += red[q][t][k];
+            v[5] = fmax(v[5], red[q][t][5]);
+            v[6] += red[q][t][6];
+        }
+        int imp = 0;
+        double p2 = 1.0, sc = 0.0;
+        if (live_s[t]) {
+            RealState& rs = a.rs[j0 + t];
+            rs.obj2 = v[0];
+            rs.nAX2 = v[1];
+            rs.nY2 = v[2];
+            rs.nJM2 = v[3];
+            rs.dY2 = v[4];
+            imp = sqrt(v[0]) < rs.opt_obj;   // iter_control makes the same decision (opt_Y here)
+            plane_scale(v[5] + v[6], a.c8[1], p2, sc);
+        }
+        imp_s[t] = imp;
+        p2_s[t] = p2;
+        sc_s[t] = sc;
+    }
+    __syncthreads();
+#ifdef ACE_GYK_PROBE_P2
+    return;
+#endif
+    for (int idx = t; idx < GRB * m; idx += NT) {   // opt_Y (:344-351)
+        const int jl = idx / m, i = idx - jl * m;
+        if (live_s[jl] && imp_s[jl]) reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
+    }
+#ifdef ACE_GYK_PROBE_P3
+    return;
+#endif
+    // ---- K Y_new: digit planes of Y_new (thread: realisation bl, entries 64 s + 2 cp + {0, 1})
+    {
+        const int bl = t >> 5, cp = t & 31;
+        const double p2 = p2_s[bl];
+        for (int s = 0; s < nksK / KSC; ++s) {
+            d2 x[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int k = 64 * s + 2 * cp + u;
+                x[u] = (live_s[bl] && k < m) ? Ts[bl * tst + k] : make_double2(0.0, 0.0);
+            }
+            const double v[4] = {x[0].x, x[0].y, x[1].x, x[1].y};
+            uint32_t d[8];
+            digits4(v, p2, d);
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) *reinterpret_cast<uint32_t*>(&Ad[lds_row(bl, tt) * rst + KC * s + 4 * cp]) = d[tt];
+        }
+    }
+    __syncthreads();
+#ifdef ACE_GYK_PROBE_NO_C
+    return;
+#endif
+    const int h = lane >> 5, ldo = 2 * m, ocb = NCB / 2, ncb = (ldo + ocb - 1) / ocb;
+    const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
+    const i4v* Bf = reinterpret_cast<const i4v*>(a.LK);
+    const int total = ncb * nksK;
+    auto bfl = [&](BSet& b, int f0) {
+#pragma unroll
+        for (int kk = 0; kk < SK; ++kk) {
+            const int f = min(f0 + kk, total - 1), cb = f / nksK, ks = f - cb * nksK;
+            const i4v* pp = Bf + ((long long)(cb * (NCB / 32) + 2 * w) * nksK + ks) * 64 + lane;
+            b.f[kk][0] = pp[0];
+            b.f[kk][1] = pp[(long long)nksK * 64];
+        }
+    };
+    const double* Ysd = reinterpret_cast<const double*>(Ts);
+    double dacc[4][2], nacc[4][2];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) dacc[R][0] = dacc[R][1] = nacc[R][0] = nacc[R][1] = 0.0;
+    auto epilogue = [&](int cbk, i16v (&acc)[4][2]) {
+        const int col = (cbk * (NCB / 64) + w) * 32 + (lane & 31), colc = min(col, ldo - 1);
+        double yo[4][2], ko[4][2];   // Y0, KY0 of the lane's 8 outputs, loaded as one batch
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int blo = 4 * R + 2 * q + h;
+                const long long off = (long long)(live_s[blo] ? j0 + blo : j0) * ldo + colc;
+                yo[R][q] = a.Yo[off];
+                ko[R][q] = a.KYo[off];
+            }
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                if (!live_s[blo] || col >= ldo) continue;
+                i16v cmb;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) cmb[e] = acc[R][0][e] + 128 * acc[R][1][e];
+                const double kyn = sc_s[blo] * recombine(cmb, q);
+                const long long off = (long long)j * ldo + col;
+                a.KYn[off] = kyn;
+                const double yn = Ysd[2 * blo * tst + col];
+                dacc[R][q] += (yn - yo[R][q]) * (kyn - ko[R][q]);
+                nacc[R][q] += yn * kyn;
+            }
+#pragma unroll
+        for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+    };
+    i16v acc[4][2];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+    BSet bA, bB;
+    bfl(bA, 0);
+    for (int f = 0; f < total; f += 2 * SK) {
+        bfl(bB, f + SK);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_mma(arow + 32 * (f % nksK), rst, bA, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        bfl(bA, f + 2 * SK);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_mma(arow + 32 * ((f + SK) % nksK), rst, bB, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((f + 2 * SK) % nksK == 0) epilogue(f / nksK, acc);
+    }
+    // dual terms: lanes of one half-wave share realisations; then the 8 waves in fixed order
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                dacc[R][q] += __shfl_xor(dacc[R][q], o, 64);
+                nacc[R][q] += __shfl_xor(nacc[R][q], o, 64);
+            }
+            if ((lane & 31) == 0) {
+                red[w][4 * R + 2 * q + h][0] = dacc[R][q];
+                red[w][4 * R + 2 * q + h][1] = nacc[R][q];
+            }
+        }
+    __syncthreads();
+    if (t < GRB && live_s[t]) {
+        double dv = 0.0, nv = 0.0;
+        for (int q = 0; q < 8; ++q) {
+            dv += red[q][t][0];
+            nv += red[q][t][1];
+        }
+        a.rs[j0 + t].dAtY = dv;
+        a.rs[j0 + t].nAtY = nv;
+    }
+}
+
+// G [m][m] c128 -> f64 MFMA B-operand fragments: ((ks * (mp/16) + ct) * 64 + lane) holds
+// G[16 ct + (lane & 15)][4 ks + (lane >> 4)] (zero padded to mp = m rounded up to 32).
+__global__ __launch_bounds__(256) void gyk_gfrag_kernel(int m, const double* __restrict__ Gp, double* __restrict__ Gf) {
+    const int mp = gyk_mp(m), nct = mp / 16;
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= (long long)mp * mp) return;
+    const int lane = (int)(e & 63);
+    const long long q = e >> 6;
+    const int ct = (int)(q % nct), ks = (int)(q / nct);
+    const int i = 16 * ct + (lane & 15), k = 4 * ks + (lane >> 4);
+    const d2 v = (i < m && k < m) ? reinterpret_cast<const d2*>(Gp)[(long long)i * m + k] : make_double2(0.0, 0.0);
+    reinterpret_cast<d2*>(Gf)[e] = v;
+}
+
 // K_int = rint(K / c^2) (exact: K = A A^H of a phase code is c^2 times a Gaussian-integer
 // matrix, and its f64 rounding error is far below c^2 / 2).  Real expansion entry (oc, kk)
 // of K_int as base-128 digits lo in [0, 127], hi = floor(v / 128); plane p of output tile
@@ -526,6 +877,25 @@ void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double*
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
     hipLaunchKernelGGL(i8ah_kernel<true>, grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
                        reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs);
+}
+size_t gyk_gfrag_bytes(int m) { return (size_t)gyk_mp(m) * gyk_mp(m) * 16; }
+size_t gyk_lds_bytes(int m) {
+    return (((size_t)GRB * (gyk_mp(m) + 1) * 16 + 255) & ~(size_t)255) + i8ah_lds_bytes(m);
+}
+void launch_gyk_gfrag(int m, const double* G, double* Gf, hipStream_t st) {
+    const long long tot = (long long)gyk_mp(m) * gyk_mp(m);
+    hipLaunchKernelGGL(gyk_gfrag_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, G, Gf);
+}
+void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st) {
+    static const bool attr = [] {
+        // dynamic + static (the 7 KiB reduction scratch) must fit the 160 KiB of the CU
+        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gyk_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, GYK_MAXDYN) == hipSuccess;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(gyk_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyk_lds_bytes(m), st, nb, m, a);
 }
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st) {

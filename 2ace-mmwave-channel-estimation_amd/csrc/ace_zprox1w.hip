@@ -111,19 +111,37 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     // they depend only on the Y-step and K Y, so they run first (their loads then do not queue
     // behind this kernel's stores)
     double dAtY = 0.0, nAtY = 0.0;
-    if (!INIT) {
+    if (!INIT && a.yfused) {   // gyk_kernel produced the dual terms and opt_Y
+        if (lane == 0) {
+            dAtY = st->dAtY;
+            nAtY = st->nAtY;
+        }
+    } else if (!INIT) {
         const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
         const d2* Yo = reinterpret_cast<const d2*>(a.Yold) + (long long)b * m;
         const d2* Kn = reinterpret_cast<const d2*>(a.KYnew) + (long long)b * m;
         const d2* Ko = reinterpret_cast<const d2*>(a.KYold) + (long long)b * m;
         d2* oY = reinterpret_cast<d2*>(a.optY) + (long long)b * m;
-        for (int i = lane; i < m; i += 64) {
-            const d2 yn = Yn[i], kn = Kn[i];
-            const d2 dy = csub(yn, Yo[i]), dk = csub(kn, Ko[i]);
+        auto term = [&](int i, d2 yn, d2 yo, d2 kn, d2 ko) {
+            const d2 dy = csub(yn, yo), dk = csub(kn, ko);
             dAtY += dy.x * dk.x + dy.y * dk.y;
             nAtY += yn.x * kn.x + yn.y * kn.y;
             if (improved_pre) oY[i] = yn;   // best-objective iterate (:344-351; iter_control agrees)
+        };
+        constexpr int YS = 4;   // the first 4 x 64 entries with all loads in flight at once
+        d2 yn[YS], yo[YS], kn[YS], ko[YS];
+#pragma unroll
+        for (int q = 0; q < YS; ++q) {
+            const int i = lane + 64 * q, ic = i < m ? i : 0;
+            yn[q] = Yn[ic];
+            yo[q] = Yo[ic];
+            kn[q] = Kn[ic];
+            ko[q] = Ko[ic];
         }
+#pragma unroll
+        for (int q = 0; q < YS; ++q)
+            if (lane + 64 * q < m) term(lane + 64 * q, yn[q], yo[q], kn[q], ko[q]);
+        for (int i = lane + 64 * YS; i < m; i += 64) term(i, Yn[i], Yo[i], Kn[i], Ko[i]);
     }
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
@@ -160,32 +178,37 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     double etr = 0.0;  // ||E||_F^2 = trace(E E^H)
     double sacc[4] = {0.0, 0.0, 0.0, 0.0};
     VMax svz, svn;
+    // Four chunks of 4 elements per lane, the loads of chunk c + 1 issued before the stores of
+    // chunk c (vmcnt retires in order: loads queued behind stores would wait for them); the
+    // loads are unconditional (clamped index, zeroed outside the tx x rx block).
+    struct Ch {
+        d2 x[4], n[4], z[4];
+    };
+    auto cload = [&](int c, Ch& q) {
 #pragma unroll
-    for (int e0 = 0; e0 < ZT * ZT; e0 += 64 * 8) {
-        d2 xv[8], nv[8], zv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5;
-            xv[u] = nv[u] = zv[u] = zero;
-            if (i < tx && j < rx) {
-                xv[u] = X[i + tx * j];
-                nv[u] = N[i + tx * j];
-                if (!INIT) zv[u] = Z[i + tx * j];
-            }
+        for (int u = 0; u < 4; ++u) {
+            const int e = lane + 64 * (4 * c + u), i = e & 31, j = e >> 5;
+            const int k = (i < tx && j < rx) ? i + tx * j : 0;
+            q.x[u] = X[k];
+            q.n[u] = N[k];
+            q.z[u] = INIT ? zero : Z[k];
         }
+    };
+    auto cwork = [&](int c, const Ch& q) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = e0 + lane + 64 * u, i = e & 31, j = e >> 5, k = i + tx * j;
+        for (int u = 0; u < 4; ++u) {
+            const int e = lane + 64 * (4 * c + u), i = e & 31, j = e >> 5, k = i + tx * j;
             const bool in = i < tx && j < rx;
-            const d2 x = wm ? xw(zv[u], nv[u], xv[u], imu) : xv[u];
-            const d2 ev = in ? make_double2(fma(nv[u].x, imu, x.x), fma(nv[u].y, imu, x.y)) : zero;
+            const d2 xv = in ? q.x[u] : zero, nv = in ? q.n[u] : zero, zv = in ? q.z[u] : zero;
+            const d2 x = wm ? xw(zv, nv, xv, imu) : xv;
+            const d2 ev = in ? make_double2(fma(nv.x, imu, x.x), fma(nv.y, imu, x.y)) : zero;
             etr += cabs2(ev);
             T0[i * ZHS + j] = ev;
             if (in && !INIT) {
                 if (improved_pre) oX[k] = x;
                 else if (keep_cur) Xc[k] = x;
                 const d2 d = csub(x, ev);
-                const d2 nn = cadd(nv[u], cscale(d, mu));
+                const d2 nn = cadd(nv, cscale(d, mu));
                 if (pp) {
                     Zn[k] = ev;
                     Nn[k] = nn;
@@ -193,11 +216,22 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                 sacc[0] += cabs2(x);
                 sacc[1] += cabs2(ev);
                 sacc[2] += cabs2(d);
-                sacc[3] += cabs2(csub(ev, zv[u]));
+                sacc[3] += cabs2(csub(ev, zv));
                 svz.add(ev);
                 svn.add(nn);
             }
         }
+    };
+    {
+        Ch c0, c1;
+        cload(0, c0);
+        cload(1, c1);
+        cwork(0, c0);
+        cload(2, c0);
+        cwork(1, c1);
+        cload(3, c1);
+        cwork(2, c0);
+        cwork(3, c1);
     }
     __syncthreads();
 #ifdef ACE_DEBUG_SWEEPS
@@ -680,8 +714,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
 #ifdef ACE_DEBUG_SWEEPS
     const unsigned long long dbg_t4 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0 && (b == 0 || b == 2000) && (a.it < 30 || a.it % 20 == 0))
-        printf("1w b %d it %d sweeps %d pre %llu jac %llu order+Q %llu emit %llu (x10ns)\n", b, a.it, sweeps,
-               dbg_t1 - dbg_t0, dbg_t2 - dbg_t1, dbg_t3 - dbg_t2, dbg_t4 - dbg_t3);
+        printf("1w b %d it %d sweeps %d pre %llu jac %llu order+Q %llu emit %llu (x10ns) scaled %d\n", b, a.it, sweeps,
+               dbg_t1 - dbg_t0, dbg_t2 - dbg_t1, dbg_t3 - dbg_t2, dbg_t4 - dbg_t3, flag_any);
+    if (lane == 0 && a.it >= 1 && a.it <= 8 && (b & 127) == 5) printf("cold b %d it %d sweeps %d scaled %d\n", b, a.it, sweeps, flag_any);
     if (lane == 0 && (b == 0 || b == 2000) && (a.it % 20 == 0))
         printf("1w b %d it %d fast: E %llu F %llu cert %llu rest %llu\n", b, a.it, dbg_fa - dbg_t0, dbg_fb - dbg_fa,
                dbg_fc - dbg_fb, dbg_t4 - dbg_fc);

@@ -19,6 +19,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <utility>
+#include <vector>
+#include <algorithm>
 
 namespace ace {
 
@@ -168,6 +170,130 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->done = cv.take<int>(256);
 }
 
+// ---- the unit path split into independent sub-batches on concurrent streams.  Each of the four
+// kernels of an iteration runs one work-group per CU for ~50-100 us with phases that are either
+// memory- or matrix-core-bound; with two sub-batches in flight the Z-step of one (HBM) runs
+// beside the GEMMs of the other.  ACE_SPLIT=k selects k sub-batches (default 2, 1 = off).
+static int split_count(int batch) {
+    static const int v = [] {
+        const char* e = getenv("ACE_SPLIT");
+        return e ? atoi(e) : 2;
+    }();
+    int k = v < 1 ? 1 : (v > 4 ? 4 : v);
+    while (k > 1 && batch / k < 256) --k;   // keep every sub-batch at least one full wave of CUs
+    return k;
+}
+
+// AdmmState of realisations [ob, ob + ...) of w (r = 1 layout)
+static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n) {
+    AdmmState h = w;
+    const long long on = 2 * ob * n, om = 2 * ob * m;
+    h.X = w.X + on;
+    h.Z = w.Z + on;
+    h.N = w.N + on;
+    h.Z2 = w.Z2 + on;
+    h.N2 = w.N2 + on;
+    h.V = w.V + on;
+    h.optX = w.optX + on;
+    h.Q = w.Q + 2 * ob * 32 * 32;
+    for (int i = 0; i < 2; ++i) {
+        h.Y[i] = w.Y[i] + om;
+        h.KY[i] = w.KY[i] + om;
+    }
+    h.M = w.M + om;
+    h.S = w.S + om;
+    h.T = w.T + om;
+    h.g = w.g + om;
+    h.optY = w.optY + om;
+    h.st = w.st + ob;
+    return h;
+}
+
+int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w, const ZArgs& za0, int batch,
+                       const double* B, int nsplit, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
+                       double* mu_out, hipStream_t st) {
+    const int m = L.m, n = L.n;
+    const int chunk = (batch / nsplit + 15) & ~15;
+    std::vector<hipStream_t> ss(nsplit, st);
+    std::vector<hipEvent_t> ev(nsplit);
+    for (int h = 0; h < nsplit; ++h) ACE_HIP(hipEventCreateWithFlags(&ev[h], hipEventDisableTiming));
+    for (int h = 1; h < nsplit; ++h) ACE_HIP(hipStreamCreateWithFlags(&ss[h], hipStreamNonBlocking));
+    ACE_HIP(hipEventRecord(ev[0], st));   // fork after init
+    for (int h = 1; h < nsplit; ++h) ACE_HIP(hipStreamWaitEvent(ss[h], ev[0], 0));
+    std::vector<AdmmState> ws(nsplit);
+    std::vector<int> nb(nsplit);
+    for (int h = 0; h < nsplit; ++h) {
+        const long long ob = (long long)h * chunk;
+        nb[h] = (int)std::max(0LL, std::min((long long)chunk, batch - ob));
+        ws[h] = state_slice(w, ob, m, n);
+    }
+    int q = 0, rc = ACE_OK;
+    for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
+        for (int h = 0; h < nsplit; ++h) {
+            if (nb[h] == 0) continue;
+            const AdmmState& wh = ws[h];
+            const hipStream_t sh = ss[h];
+            const double* Bh = B + (long long)h * chunk * m;
+            double* Zc = (it & 1) ? wh.Z : wh.Z2;   // Z, N of the previous iterate (ping-pong)
+            double* Nc = (it & 1) ? wh.N : wh.N2;
+            {
+                ProfScope ps(ACE_K_APPLY_A, sh);
+                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, sh);
+            }
+            {
+                ProfScope ps(ACE_K_APPLY_G, sh);
+                const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
+                                 L.LK8, L.c8, wh.st};
+                launch_gyk(nb[h], m, ga, sh);
+            }
+            {
+                ProfScope ps(ACE_K_APPLY_AH, sh);
+                launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh);
+            }
+            ZArgs za = za0;
+            za.it = it;
+            za.wmode = 1;
+            za.yfused = 1;
+            za.ypart = nullptr;
+            za.X = wh.X;
+            za.Z = Zc;
+            za.N = Nc;
+            za.Zn = (it & 1) ? wh.Z2 : wh.Z;
+            za.Nn = (it & 1) ? wh.N2 : wh.N;
+            za.Q = wh.Q;
+            za.st = wh.st;
+            za.optX = wh.optX;
+            za.optY = wh.optY;
+            za.Xcur = wh.V;
+            za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
+            {
+                ProfScope ps(ACE_K_ZSTEP, sh);
+                launch_zstep(p.variant, false, za, nb[h], sh);
+            }
+        }
+        q = 1 - q;
+        if (!p.fixed_iters && (it % 8 == 0) && it < p.maxiter) {
+            for (int h = 0; h < nsplit; ++h) ACE_HIP(hipStreamSynchronize(ss[h]));
+            int h_done = 0;
+            ACE_HIP(hipMemcpy(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost));
+            if (h_done >= batch) break;
+        }
+    }
+    for (int h = 1; h < nsplit; ++h) {   // join
+        ACE_HIP(hipEventRecord(ev[h], ss[h]));
+        ACE_HIP(hipStreamWaitEvent(st, ev[h], 0));
+    }
+    ACE_HIP(hipGetLastError());
+    {
+        ProfScope ps(ACE_K_FINAL, st);
+        launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st);
+    }
+    ACE_HIP(hipGetLastError());
+    for (int h = 1; h < nsplit; ++h) ACE_HIP(hipStreamDestroy(ss[h]));
+    for (int h = 0; h < nsplit; ++h) ACE_HIP(hipEventDestroy(ev[h]));
+    return rc;
+}
+
 int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch, const double* B,
              const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu_out,
              hipStream_t st) {
@@ -237,6 +363,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
 
     int q = 0;
     const int poll = 8;
+    const int nsplit = gyk ? split_count(batch) : 1;
+    if (nsplit > 1) return admm_iterate_split(L, p, w, za, batch, B, nsplit, Xo, Yo, iters, status, mu_out, st);
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {

@@ -446,11 +446,19 @@ def main():
             # the int8 digit-plane applies run for a phase-code codebook in the A2only r = 1 iteration
             i8 = (not args.private) and args.variant == "A2only" and os.environ.get("ACE_NO_I8") != "1"
             io = unit_i8_ops(m, n)
+            # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
+            # every launch of an iteration kernel covers bsz / nsplit realisations
+            nsplit = 1
+            if i8 and m <= 256:
+                nsplit = max(1, min(4, int(os.environ.get("ACE_SPLIT", "2"))))
+                while nsplit > 1 and bsz // nsplit < 256:
+                    nsplit -= 1
+            per_launch = -(-bsz // nsplit)
 
             def roofline(k):
                 avg_s = kernels[k]["avg_ms"] * 1e-3
                 if k in io and i8:   # exact int8 digit planes on the matrix cores
-                    per, pb = io[k] * bsz, ub[k] * bsz
+                    per, pb = io[k] * per_launch, ub[k] * per_launch
                     return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
                             "unit": "TOP/s", "frac": round(per / avg_s / 1e12 / PEAK_I8_TOPS, 4), "traffic": None,
                             "kernel": k, "ops_per_launch": per,
@@ -461,7 +469,7 @@ def main():
                                        "(exact: the codebook is a phase code); f64_equiv_tflops counts the same "
                                        "product as 8 flops per complex MAC"}
                 if k in uf:   # MFMA-bound complex f64 GEMM
-                    per = uf[k] * bsz
+                    per = uf[k] * per_launch
                     # algorithmic = conventional 8 flops per complex MAC; the 3M kernel executes 6
                     return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
                             "unit": "TFLOP/s", "frac": round(per / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
@@ -469,7 +477,7 @@ def main():
                             "executed_frac": round(0.75 * per / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
                             "flop_note": "achieved counts 8 real flops per complex MAC; the 3M (Gauss) kernel "
                                          "executes 6, so the matrix cores run at executed_frac of peak"}
-                per = ub[k] * bsz
+                per = ub[k] * per_launch
                 return {"bound": "hbm", "achieved": round(per / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(per / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
                         "kernel": k, "bytes_per_launch": per}
@@ -478,6 +486,7 @@ def main():
             # every timed class launches once per iteration: dominant = largest average launch
             dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
             roof = roofline(dom)
+            roof["realisations_per_launch"] = per_launch
             roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
                             f"region, on every {PROF_STRIDE}rd launch of each kernel class); peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); "
                             "traffic: PMC FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source")
@@ -486,6 +495,9 @@ def main():
                 roof["traffic"], roof["traffic_source"] = tr
             gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
             roof_gemm = roofline(gemm)
+            if gemm == "apply_G" and i8 and m <= 256:
+                roof_gemm["flop_note"] = ("gyk_kernel: g = G T (counted, f64 3M on the matrix cores) plus the Y-step, "
+                                          "K Y on the int8 matrix cores and the dual terms (not counted)")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             ns = args.cpu_recoveries or 256

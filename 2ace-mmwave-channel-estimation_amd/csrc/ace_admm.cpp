@@ -168,6 +168,7 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->ypart = cv.take(sizeof(double) * 5 * (size_t)batch * r * ((m + 63) / 64));
     s->st = cv.take<RealState>(sizeof(RealState) * (size_t)batch);
     s->done = cv.take<int>(256);
+    s->zeros = cv.take(16 * (size_t)n);
 }
 
 // ---- the unit path split into independent sub-batches on concurrent streams.  Each of the four
@@ -238,7 +239,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             double* Nc = (it & 1) ? wh.N : wh.N2;
             {
                 ProfScope ps(ACE_K_APPLY_A, sh);
-                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, sh);
+                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, w.zeros, sh);
             }
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
@@ -348,9 +349,11 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)
     za.Nn = nullptr;
+    za.zeros = w.zeros;
 
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
+    ACE_HIP(hipMemsetAsync(w.zeros, 0, 16 * (size_t)n, st));
     {
         ProfScope ps(ACE_K_INIT, st);
         applyA(0, X0, w.T, nullptr);                             // AX = A*X0
@@ -370,7 +373,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     for (int it = 1; it <= p.maxiter; ++it) {
         if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
-            launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, st);
+            launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);

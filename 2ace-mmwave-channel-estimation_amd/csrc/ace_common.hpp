@@ -29,6 +29,10 @@ struct RealState {
     // ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0) and ||A^H Y||^2 = Y^H K Y
     double dAtY, nAtY;
     int32_t iters, done, status, objcol;  // objcol: argmin column of the per-column objective
+    // 1 when the stored N is exactly zero (wmode Z-step, common case Z = E: N + mu (X - Z) is
+    // then zero in exact arithmetic and only its rounding residue would be stored); readers use
+    // the zero vector instead of N
+    int32_t nzero, pad_i[3];
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -106,7 +110,8 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
                       hipStream_t st);
 // T = (Y - M/mu) - c A (Z - N/mu)   (A: m x n phase code, c = *cmax)
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
-                       const double* M, double* T, const double* cmax, const RealState* rs, hipStream_t st);
+                       const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
+                       hipStream_t st);
 // W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st);
@@ -184,6 +189,7 @@ struct ZArgs {
     double* Nn;
     // the Y-step sums, the dual terms (RealState::dAtY, nAtY) and opt_Y come from gyk_kernel
     int yfused;
+    const double* zeros;   // n zero complex entries (the N of realisations with nzero set)
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

@@ -144,6 +144,7 @@ struct AdmmState {
     double* ypart;  // fused Y-step partials [batch][ceil(m/64)][5] (r = 1 iterations)
     RealState* st;
     int* done;
+    double* zeros;  // [n] c128 zeros (N of realisations with RealState::nzero)
 };
 void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s);
 // Runs init (:296-310), the iterations (:318-383) and returns the best-objective iterate

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
                                                     const double* __restrict__ Zp, const double* __restrict__ Np,
                                                     const double* __restrict__ Yp, const double* __restrict__ Mp,
                                                     double* __restrict__ Tp, const double* __restrict__ cptr,
-                                                    const RealState* __restrict__ rs) {
+                                                    const RealState* __restrict__ rs, const double* __restrict__ zeros) {
     __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
     __shared__ double sc_s[RB], imu_s[RB];
     __shared__ int live_s[RB];
@@ -175,7 +175,8 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
     const bool live = jb < nb && !rs[jb].done;
     const double imu = live ? 1.0 / rs[jb].mu : 0.0;
     const d2* z = reinterpret_cast<const d2*>(Zp) + (long long)(live ? jb : 0) * Kc;
-    const d2* nn = reinterpret_cast<const d2*>(Np) + (long long)(live ? jb : 0) * Kc;
+    const d2* nn = (live && rs[jb].nzero) ? reinterpret_cast<const d2*>(zeros)
+                                          : reinterpret_cast<const d2*>(Np) + (long long)(live ? jb : 0) * Kc;
     double p2, sc;
     plane_scale(live ? rs[jb].vbound : 0.0, *cptr, p2, sc);
     if (cq == 0) {
@@ -856,10 +857,11 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
 size_t i8ah_lds_bytes(int kc) { return (size_t)ROWS * (32 * i8_nks(kc) + 16); }
 
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
-                       const double* M, double* T, const double* cmax, const RealState* rs, hipStream_t st) {
+                       const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
+                       hipStream_t st) {
     dim3 grid((nb + RB - 1) / RB, i8_ncols(m) / NCB, 1), block(NT);
     hipLaunchKernelGGL(i8a_kernel, grid, block, 0, st, nb, n, m, i8_nks(n), reinterpret_cast<const i4v*>(LA), Z, N,
-                       Y, M, T, cmax, rs);
+                       Y, M, T, cmax, rs, zeros);
 }
 size_t i8k_frag_bytes(int m) { return (size_t)2 * ((2 * m + NCB / 2 - 1) / (NCB / 2)) * (NCB / 2) * i8_nks(m) * 32; }
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st) {

@@ -71,7 +71,11 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
 
     const double mu = INIT ? 1.0 : st->mu;
     const d2* X = reinterpret_cast<const d2*>(a.X) + (long long)b * n;
-    const d2* N = reinterpret_cast<const d2*>(a.N) + (long long)b * n;
+    // wmode + ping-pong: N may be the exact zero vector (RealState::nzero), and in the common case
+    // Z = E the new N is stored as exact zero (see RealState::nzero)
+    const bool flushN = !INIT && a.wmode && a.Zn && a.Zn != a.Z && a.zeros;
+    const bool nz_in = flushN && st->nzero;
+    const d2* N = nz_in ? reinterpret_cast<const d2*>(a.zeros) : reinterpret_cast<const d2*>(a.N) + (long long)b * n;
     const d2* Z = reinterpret_cast<const d2*>(a.Z) + (long long)b * n;
     d2* Nn = reinterpret_cast<d2*>(a.Nn ? a.Nn : a.N) + (long long)b * n;
     d2* Zn = reinterpret_cast<d2*>(a.Zn ? a.Zn : a.Z) + (long long)b * n;
@@ -211,7 +215,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                 const d2 nn = cadd(nv, cscale(d, mu));
                 if (pp) {
                     Zn[k] = ev;
-                    Nn[k] = nn;
+                    if (!flushN) Nn[k] = nn;
                 }
                 sacc[0] += cabs2(x);
                 sacc[1] += cabs2(ev);
@@ -372,11 +376,12 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     if (lane == 0) flag_any = 0;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     VMax vz, vn;   // max |Z|, |N| of the outputs: the next apply's bound on |Z - N/mu|
+    const bool nz_out = pp && fast && flushN;
     if (pp && fast) {   // Z = E: the outputs written in phase 1 stand
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = sacc[q];
         vz = svz;
-        vn = svn;
+        if (!flushN) vn = svn;   // else N' is stored as exact zero
     } else {
     if (!fast) {
     // H = F F^H (:428), upper blocks (0,0), (0,1), (1,1) -> packed buffer 0
@@ -738,6 +743,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
     improved = __shfl(improved, 0, 64);
     write_vbound();
+    if (lane == 0) st->nzero = nz_out ? 1 : 0;
 #ifdef ACE_DEBUG_SWEEPS
     if (lane == 0 && a.it == 100) {
         const unsigned long long te = __builtin_amdgcn_s_memrealtime();

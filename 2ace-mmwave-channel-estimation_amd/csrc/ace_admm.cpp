@@ -287,7 +287,8 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     ACE_HIP(hipGetLastError());
     {
         ProfScope ps(ACE_K_FINAL, st);
-        launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st);
+        launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st, w.Z,
+                          w.Z2);
     }
     ACE_HIP(hipGetLastError());
     for (int h = 1; h < nsplit; ++h) ACE_HIP(hipStreamDestroy(ss[h]));
@@ -440,7 +441,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     {
         ProfScope ps(ACE_K_FINAL, st);
         launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, wmode ? w.V : w.X, w.Y[q], Xo, Yo, iters, status,
-                          mu_out, w.st, st);
+                          mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr);
     }
     ACE_HIP(hipGetLastError());
     return ACE_OK;

@@ -32,7 +32,12 @@ struct RealState {
     // 1 when the stored N is exactly zero (wmode Z-step, common case Z = E: N + mu (X - Z) is
     // then zero in exact arithmetic and only its rounding residue would be stored); readers use
     // the zero vector instead of N
-    int32_t nzero, pad_i[3];
+    int32_t nzero;
+    // where opt_X lives: 0 the opt_X buffer; 1 / 2 the Z / Z2 ping-pong buffer (wmode: when the
+    // best iterate had N = 0 and Z = E, X = Z' exactly and the copy is deferred until that buffer
+    // is about to be overwritten)
+    int32_t optsrc;
+    int32_t pad_i[2];
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -247,7 +252,8 @@ void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, cons
 // opt_X / opt_Y (nc columns) or, if the objective never was finite, the current iterate.
 void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
                        const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters,
-                       uint32_t* status, double* mu, RealState* rs, hipStream_t st);
+                       uint32_t* status, double* mu, RealState* rs, hipStream_t st,
+                       const double* Zb1 = nullptr, const double* Zb2 = nullptr);
 void launch_conj_transpose(int rows, int cols, const double* A, double* AH, hipStream_t st);
 void launch_synth_codebook(uint64_t seed, long long first, int count, int m, int n, double* A, hipStream_t st);
 void launch_synth_channels(uint64_t seed, long long first, int count, int m, int tx, int rx, int L, double snr_db,

@@ -111,6 +111,23 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const bool keep_cur = wm && !improved_pre && !(st->opt_obj < INFINITY);   // finalize's fallback X
     d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
     d2* Xc = reinterpret_cast<d2*>(a.Xcur) + (long long)b * n;
+    // Deferred opt_X (RealState::optsrc): with N = 0 and Z = E the new Z' equals X exactly, so an
+    // improved iterate is only recorded as "in the Z' buffer"; it is copied to opt_X when that
+    // buffer is about to be overwritten (here, two iterations later) if no better iterate came.
+    const int zn_id = 1 + (a.it & 1);   // Z' buffer of this iteration: Z2 for odd it, Z for even
+    int optsrc = INIT ? 0 : st->optsrc;
+    if (pp && optsrc == zn_id) {
+        for (int k0 = 0; k0 < n; k0 += 64 * 8) {
+            d2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = Zn[min(k0 + lane + 64 * u, n - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (k0 + lane + 64 * u < n) oX[k0 + lane + 64 * u] = v[u];
+        }
+        optsrc = 0;
+    }
+    const bool defer_opt = improved_pre && nz_in && pp;   // decided after the certificate
     // m-space dual terms ||A^H (Y - Y0)||^2 = dY^H (K Y - K Y0), ||A^H Y||^2 = Y^H K Y, and opt_Y:
     // they depend only on the Y-step and K Y, so they run first (their loads then do not queue
     // behind this kernel's stores)
@@ -209,7 +226,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
             etr += cabs2(ev);
             T0[i * ZHS + j] = ev;
             if (in && !INIT) {
-                if (improved_pre) oX[k] = x;
+                if (improved_pre && !defer_opt) oX[k] = x;
                 else if (keep_cur) Xc[k] = x;
                 const d2 d = csub(x, ev);
                 const d2 nn = cadd(nv, cscale(d, mu));
@@ -633,6 +650,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     // copied in the same pass that reads it (iter_control below makes the same decision).
     // emit_v: element k with its X, N, Z_old already loaded (opt_X was copied in phase 1)
     auto emit_v = [&](int k, d2 x, d2 nn, d2 zo, d2 znew) {
+        if (defer_opt) oX[k] = x;   // Z' != X on this path: the copy cannot be deferred
         vz.add(znew);
         if (!INIT) {
             const d2 d = csub(x, znew);
@@ -743,7 +761,11 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         improved = iter_control(a, st, mu, s_nX2, s_nZ2, s_jn2, s_dZ2, s_dAtY, s_nAtY);
     improved = __shfl(improved, 0, 64);
     write_vbound();
-    if (lane == 0) st->nzero = nz_out ? 1 : 0;
+    if (lane == 0) {
+        st->nzero = nz_out ? 1 : 0;
+        if (improved_pre) optsrc = (defer_opt && pp && fast) ? zn_id : 0;
+        st->optsrc = optsrc;
+    }
 #ifdef ACE_DEBUG_SWEEPS
     if (lane == 0 && a.it == 100) {
         const unsigned long long te = __builtin_amdgcn_s_memrealtime();

@@ -351,6 +351,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)
     za.Nn = nullptr;
     za.zeros = w.zeros;
+    za.nuclear = p.variant == ACE_VARIANT_NUCLEAR;
 
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));

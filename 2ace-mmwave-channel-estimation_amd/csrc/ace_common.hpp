@@ -195,6 +195,7 @@ struct ZArgs {
     // the Y-step sums, the dual terms (RealState::dAtY, nAtY) and opt_Y come from gyk_kernel
     int yfused;
     const double* zeros;   // n zero complex entries (the N of realisations with nzero set)
+    int nuclear;           // one-wave kernel: A2nuclear r = 1 prox Z = E max(0, |E| - 1/mu) / |E|
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

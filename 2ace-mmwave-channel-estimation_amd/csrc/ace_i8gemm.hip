@@ -500,24 +500,6 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     }
     __syncthreads();
 
-    // the Y-step inputs of the lane's 8 elements, loaded before the G T loop so that they land
-    // while it runs (unconditional, clamped addresses; per-element branches would serialise
-    // 8 memory round trips)
-    d2 mi[2][4], yov[2][4];
-    double biv[2][4], muv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int jl = (lane >> 4) + 4 * r;
-        muv[r] = a.rs[live_s[jl] ? j0 + jl : j0].mu;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int i = min(16 * (2 * w + c) + (lane & 15), m - 1);
-            const long long off = (long long)(live_s[jl] ? j0 + jl : j0) * m + i;
-            mi[c][r] = reinterpret_cast<const d2*>(a.M)[off];
-            yov[c][r] = reinterpret_cast<const d2*>(a.Yo)[off];
-            biv[c][r] = a.B[off];
-        }
-    }
     // ---- g = G T: wave w owns output tiles 2w, 2w + 1 (16 complex each)
     const int nct = mp / 16, nks = mp / 4, nstage = nks / GSK;
     const int ct0 = min(2 * w, nct - 1), ct1 = min(2 * w + 1, nct - 1);
@@ -578,6 +560,24 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             gcomp(gB, tB);
             __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // the Y-step inputs of the lane's 8 elements as one batch of loads (unconditional, clamped
+    // addresses; per-element branches would serialise 8 memory round trips).  Issued after the
+    // G T loop: held across it they would push the kernel past 256 VGPRs into scratch.
+    d2 mi[2][4], yov[2][4];
+    double biv[2][4], muv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int jl = (lane >> 4) + 4 * r;
+        muv[r] = a.rs[live_s[jl] ? j0 + jl : j0].mu;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int i = min(16 * (2 * w + c) + (lane & 15), m - 1);
+            const long long off = (long long)(live_s[jl] ? j0 + jl : j0) * m + i;
+            mi[c][r] = reinterpret_cast<const d2*>(a.M)[off];
+            yov[c][r] = reinterpret_cast<const d2*>(a.Yo)[off];
+            biv[c][r] = a.B[off];
         }
     }
     __syncthreads();   // every wave is done with T: Ts becomes Y_new

@@ -406,11 +406,16 @@ static bool use_4wave_zstep() {
 }
 
 // the one-wave A2only kernel forms X from W = A^H g itself (ZArgs::wmode)
-bool zstep_takes_w(int variant, int r) { return variant != ACE_VARIANT_NUCLEAR && r == 1 && !use_4wave_zstep(); }
+bool zstep_takes_w(int variant, int r) {
+    (void)variant;   // A2only and A2nuclear (r = 1) both run the one-wave kernel
+    return r == 1 && !use_4wave_zstep();
+}
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st) {
 #define ACE_ZL(V, I, G) hipLaunchKernelGGL((zstep_kernel<V, I, G>), dim3(batch), dim3(256), 0, st, a)
-    if (variant == ACE_VARIANT_NUCLEAR) {
+    if (variant == ACE_VARIANT_NUCLEAR && a.r == 1 && !use_4wave_zstep()) {
+        launch_zstep1w(init, a, batch, st);   // ZArgs::nuclear selects the soft threshold
+    } else if (variant == ACE_VARIANT_NUCLEAR) {
         if (a.r == 1) {
             if (init) ACE_ZL(ACE_VARIANT_NUCLEAR, true, false);
             else ACE_ZL(ACE_VARIANT_NUCLEAR, false, false);

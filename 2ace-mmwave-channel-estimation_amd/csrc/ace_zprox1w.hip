@@ -81,7 +81,8 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     d2* Zn = reinterpret_cast<d2*>(a.Zn ? a.Zn : a.Z) + (long long)b * n;
     const bool pp = !INIT && a.Zn && a.Zn != a.Z && a.Nn != a.N;   // ping-pong outputs
     d2* Qg = reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx;
-    const bool warm = (!INIT) && a.warm;
+    const bool nuc = a.nuclear;   // inferLowRank_Nuclear.m:411-419 at r = 1 (no eigendecomposition)
+    const bool warm = (!INIT) && a.warm && !nuc;
     const double imu = 1.0 / mu;
     // wmode: the X buffer holds W = A^H g and X = (Z - N/mu) + W is formed here
     const bool wm = !INIT && a.wmode;
@@ -355,7 +356,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         __syncthreads();
     } else {
         if (warm) store_f();
-        if (!INIT) {
+        if (!INIT && !nuc) {
             if (lane < ZT) {
                 double d = 0.0;
                 for (int j = 0; j < ZT; ++j) d += cabs2(T0[lane * ZHS + j]);
@@ -400,7 +401,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         vz = svz;
         if (!flushN) vn = svn;   // else N' is stored as exact zero
     } else {
-    if (!fast) {
+    if (!fast && !nuc) {
     // H = F F^H (:428), upper blocks (0,0), (0,1), (1,1) -> packed buffer 0
     {
         d4v hr[3], hi[3];
@@ -712,6 +713,13 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     } else {
         // Z = E: all loads of a chunk are issued before any of its stores (the stores to N, Z and
         // opt_X would otherwise serialise every element behind a full memory round trip)
+        // (nuclear r = 1: Z = E f with f = max(0, ||E|| - 1/mu) / ||E||, the SVD soft threshold of
+        // the n x 1 iterate, inferLowRank_Nuclear.m:415-417)
+        double fz = 1.0;
+        if (nuc) {
+            const double nzv = sqrt(wave_sum(etr));
+            fz = nzv > 0.0 ? fmax(0.0, nzv - imu) / nzv : 0.0;
+        }
         constexpr int CH = 8;
         for (int k0 = 0; k0 < n; k0 += 64 * CH) {
             d2 xv[CH], nv[CH], zv[CH];
@@ -729,7 +737,8 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
             for (int u = 0; u < CH; ++u) {
                 const int k = k0 + lane + 64 * u;
                 const d2 x = wm ? xw(zv[u], nv[u], xv[u], imu) : xv[u];
-                if (k < n) emit_v(k, x, nv[u], zv[u], make_double2(fma(nv[u].x, imu, x.x), fma(nv[u].y, imu, x.y)));
+                const d2 e = make_double2(fma(nv[u].x, imu, x.x), fma(nv[u].y, imu, x.y));
+                if (k < n) emit_v(k, x, nv[u], zv[u], nuc ? cscale(e, fz) : e);
             }
         }
     }

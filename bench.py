@@ -444,7 +444,7 @@ def main():
                     kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
 
             # the int8 digit-plane applies run for a phase-code codebook in the A2only r = 1 iteration
-            i8 = (not args.private) and args.variant == "A2only" and os.environ.get("ACE_NO_I8") != "1"
+            i8 = (not args.private) and os.environ.get("ACE_NO_I8") != "1"
             io = unit_i8_ops(m, n)
             # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
             # every launch of an iteration kernel covers bsz / nsplit realisations

@@ -158,6 +158,7 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->Q = cv.take(cz * (size_t)batch * 32 * 32);
     s->Z2 = cv.take(cz * (size_t)batch * n);
     s->N2 = cv.take(cz * (size_t)batch * n);
+    s->AX = cv.take(cz * (size_t)batch * m);
     for (int i = 0; i < 2; ++i) s->Y[i] = cv.take(cz * bm);
     for (int i = 0; i < 2; ++i) s->KY[i] = cv.take(cz * bm);
     s->M = cv.take(cz * bm);
@@ -194,6 +195,7 @@ static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n) {
     h.N = w.N + on;
     h.Z2 = w.Z2 + on;
     h.N2 = w.N2 + on;
+    h.AX = w.AX + om;
     h.V = w.V + on;
     h.optX = w.optX + on;
     h.Q = w.Q + 2 * ob * 32 * 32;
@@ -239,12 +241,12 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             double* Nc = (it & 1) ? wh.N : wh.N2;
             {
                 ProfScope ps(ACE_K_APPLY_A, sh);
-                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, w.zeros, sh);
+                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, w.zeros, wh.AX, sh);
             }
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                                 L.LK8, L.c8, wh.st};
+                                 L.LK8, L.c8, wh.st, wh.AX};
                 launch_gyk(nb[h], m, ga, sh);
             }
             {
@@ -375,7 +377,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     for (int it = 1; it <= p.maxiter; ++it) {
         if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
-            launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, st);
+            launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
@@ -385,7 +387,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         }
         if (gyk) {
             ProfScope ps(ACE_K_APPLY_G, st);
-            const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st};
+            const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st,
+                             w.AX};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st);

@@ -37,7 +37,11 @@ struct RealState {
     // best iterate had N = 0 and Z = E, X = Z' exactly and the copy is deferred until that buffer
     // is about to be overwritten)
     int32_t optsrc;
-    int32_t pad_i[2];
+    // 1 when the next iteration's V = Z - N/mu equals this iteration's X exactly (wmode, N = 0
+    // on entry and Z' = E = X): A V is then the AX = (Y - M/mu) - g that gyk_kernel stored, and
+    // apply_A skips its product (ace_i8gemm.hip::i8a_kernel)
+    int32_t avok;
+    int32_t pad_i;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -113,10 +117,12 @@ int i8_ncols(int mc);
 size_t i8_frag_bytes(int mc, int kc);
 void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t* LA, int8_t* LH, int* flag,
                       hipStream_t st);
-// T = (Y - M/mu) - c A (Z - N/mu)   (A: m x n phase code, c = *cmax)
+// T = (Y - M/mu) - c A (Z - N/mu)   (A: m x n phase code, c = *cmax).  With AX != nullptr, a
+// 16-realisation block whose realisations all have RealState::avok takes A V = AX (the previous
+// Y-step's A X, X = V exactly) and skips the product.
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
-                       hipStream_t st);
+                       const double* AX, hipStream_t st);
 // W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st);
@@ -143,6 +149,7 @@ struct GykArgs {
     const int8_t* LK;   // K digit planes (launch_i8k_expand)
     const double* c8;   // c, c^2
     RealState* rs;
+    double* AX;         // optional: AX = (Y - M/mu) - g of the Y-step ([nb][m]), apply_A's next A V
 };
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)

@@ -140,6 +140,7 @@ struct AdmmParams {
 struct AdmmState {
     double *X, *Z, *N, *V, *optX, *Q;
     double *Z2, *N2;  // ping-pong partners of Z, N for the r = 1 wmode iteration ([batch][n])
+    double* AX;       // r = 1 unit path: AX of the last Y-step ([batch][m], RealState::avok)
     double *Y[2], *KY[2], *M, *S, *T, *g, *optY;
     double* ypart;  // fused Y-step partials [batch][ceil(m/64)][5] (r = 1 iterations)
     RealState* st;

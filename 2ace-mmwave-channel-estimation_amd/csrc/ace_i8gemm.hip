@@ -164,13 +164,43 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
                                                     const double* __restrict__ Zp, const double* __restrict__ Np,
                                                     const double* __restrict__ Yp, const double* __restrict__ Mp,
                                                     double* __restrict__ Tp, const double* __restrict__ cptr,
-                                                    const RealState* __restrict__ rs, const double* __restrict__ zeros) {
+                                                    const RealState* __restrict__ rs, const double* __restrict__ zeros,
+                                                    const double* __restrict__ AXp) {
     __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
     __shared__ double sc_s[RB], imu_s[RB];
-    __shared__ int live_s[RB];
+    __shared__ int live_s[RB], avok_s[RB];
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int j0 = blockIdx.x * RB, cb = blockIdx.y;
+    if (t < RB) {   // per realisation (the result never depends on the block it shares)
+        const int j = j0 + t;
+        avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;
+    }
+    // Steady state of the unit path: V = X of the previous iteration for every realisation of the
+    // block (RealState::avok), so A V is the AX its Y-step stored: T = (Y - M/mu) - AX, no product.
+    if (AXp) {
+        int ok = 1;
+        if (t < RB) {
+            const int j = j0 + t;
+            const bool lv = j < nb && !rs[j].done;
+            ok = !lv || rs[j].avok;
+            live_s[t] = lv;
+            imu_s[t] = lv ? 1.0 / rs[j].mu : 0.0;
+        }
+        if (__syncthreads_and(ok)) {   // complex pairs: 16-byte accesses
+            const int ldo = Mc, c0 = cb * (NCB / 2), cw = min(NCB / 2, ldo - c0);
+            for (int idx = t; idx < RB * cw; idx += NT) {
+                const int bl = idx / cw;
+                if (!live_s[bl]) continue;
+                const long long off = (long long)(j0 + bl) * ldo + c0 + idx - bl * cw;
+                const d2 y = reinterpret_cast<const d2*>(Yp)[off], mm = reinterpret_cast<const d2*>(Mp)[off],
+                         ax = reinterpret_cast<const d2*>(AXp)[off];
+                const double im = imu_s[bl];
+                reinterpret_cast<d2*>(Tp)[off] = make_double2(fma(-mm.x, im, y.x) - ax.x, fma(-mm.y, im, y.y) - ax.y);
+            }
+            return;
+        }
+    }
     const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: realisation bl, entry 32 s + cq
     const bool live = jb < nb && !rs[jb].done;
     const double imu = live ? 1.0 / rs[jb].mu : 0.0;
@@ -271,7 +301,9 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
                 const int col = (ct0 + c) * 32 + (lane & 31);
                 if (col >= ldo) continue;
                 const long long off = (long long)j * ldo + col;
-                Tp[off] = fma(-Mp[off], im, Yp[off]) - scb * recombine(acc[R][c], q);
+                // a realisation with RealState::avok takes A V = AX in any block
+                const double av = avok_s[blo] ? AXp[off] : scb * recombine(acc[R][c], q);
+                Tp[off] = fma(-Mp[off], im, Yp[off]) - av;
             }
         }
 }
@@ -621,6 +653,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             const d2 y = cscale(cc, f);
             const d2 jv = csub(ax, y);
             reinterpret_cast<d2*>(a.g)[off] = gv;
+            if (a.AX) reinterpret_cast<d2*>(a.AX)[off] = ax;
             reinterpret_cast<d2*>(a.M)[off] = cadd(mii, cscale(jv, mu));
             reinterpret_cast<d2*>(a.Yn)[off] = y;
             Ts[jl * tst + i] = y;
@@ -858,10 +891,10 @@ size_t i8ah_lds_bytes(int kc) { return (size_t)ROWS * (32 * i8_nks(kc) + 16); }
 
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
-                       hipStream_t st) {
+                       const double* AX, hipStream_t st) {
     dim3 grid((nb + RB - 1) / RB, i8_ncols(m) / NCB, 1), block(NT);
     hipLaunchKernelGGL(i8a_kernel, grid, block, 0, st, nb, n, m, i8_nks(n), reinterpret_cast<const i4v*>(LA), Z, N,
-                       Y, M, T, cmax, rs, zeros);
+                       Y, M, T, cmax, rs, zeros, AX);
 }
 size_t i8k_frag_bytes(int m) { return (size_t)2 * ((2 * m + NCB / 2 - 1) / (NCB / 2)) * (NCB / 2) * i8_nks(m) * 32; }
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st) {

@@ -208,7 +208,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         if (t == 0) {  // rank-profile tail rescaling (:469-480), sequential sums
             double* s2 = rs2;
             for (int k = 0; k < tx; ++k) s2[k] = fmax(0.0, wv[ord[k]]);
-            for (int pi = 0; pi < pf.np; ++pi) {
+            #pragma unroll  // constant trip count: the profile stays in registers
+            for (int pi = 0; pi < 4; ++pi) {
+                if (pi >= pf.np) break;
                 const int rr = pf.rl[pi];
                 const double f = pf.fl[pi];
                 double vr = 0.0, v = 0.0;

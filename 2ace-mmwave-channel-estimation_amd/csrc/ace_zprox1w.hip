@@ -118,13 +118,13 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const int zn_id = 1 + (a.it & 1);   // Z' buffer of this iteration: Z2 for odd it, Z for even
     int optsrc = INIT ? 0 : st->optsrc;
     if (pp && optsrc == zn_id) {
-        for (int k0 = 0; k0 < n; k0 += 64 * 8) {
-            d2 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = Zn[min(k0 + lane + 64 * u, n - 1)];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (k0 + lane + 64 * u < n) oX[k0 + lane + 64 * u] = v[u];
+        for (int k = lane; k < n; k += 64 * 4) {   // four loads in flight, named (no local array)
+            const d2 v0 = Zn[k], v1 = Zn[min(k + 64, n - 1)], v2 = Zn[min(k + 128, n - 1)],
+                     v3 = Zn[min(k + 192, n - 1)];
+            oX[k] = v0;
+            if (k + 64 < n) oX[k + 64] = v1;
+            if (k + 128 < n) oX[k + 128] = v2;
+            if (k + 192 < n) oX[k + 192] = v3;
         }
         optsrc = 0;
     }
@@ -179,7 +179,8 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     // profile rank is <= 16 the certificate needs only F's first 16 rows (I = 0); the second
     // half is fetched only if the certificate fails.
     int maxr = 0;
-    for (int pi = 0; pi < pf.np; ++pi) maxr = max(maxr, pf.rl[pi]);
+    #pragma unroll
+    for (int pi = 0; pi < 4; ++pi) maxr = pi < pf.np ? max(maxr, pf.rl[pi]) : maxr;
     const bool top16 = warm && maxr <= 16;
     d2 qv[2][8];
     auto load_q = [&](int I) {
@@ -342,7 +343,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         }
         const double v = wave_sum(etr);
         bool ok = v > 0.0;
-        for (int pi = 0; pi < pf.np; ++pi) {
+        #pragma unroll  // constant trip count: the profile stays in registers
+        for (int pi = 0; pi < 4; ++pi) {
+            if (pi >= pf.np) break;
             const double vr = __shfl(val, pf.rl[pi] - 1, 64);
             ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
         }
@@ -374,7 +377,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                 double v = 0.0;
                 for (int k = 0; k < ZT; ++k) v += rs2[k];
                 int ok = v > 0.0;
-                for (int pi = 0; pi < pf.np; ++pi) {
+                #pragma unroll  // constant trip count: the profile stays in registers
+                for (int pi = 0; pi < 4; ++pi) {
+                    if (pi >= pf.np) break;
                     double vr = 0.0;
                     for (int k = 0; k < pf.rl[pi]; ++k) vr += rs2[k];
                     ok &= vr > pf.fl[pi] * v * (1.0 + 1e-9);
@@ -592,7 +597,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     __syncthreads();
     if (lane == 0) {  // rank-profile tail rescaling (:469-480), sequential sums
         for (int k = 0; k < tx; ++k) rs2[k] = fmax(0.0, wv[ord[k]]);
-        for (int pi = 0; pi < pf.np; ++pi) {
+        #pragma unroll  // constant trip count: the profile stays in registers
+        for (int pi = 0; pi < 4; ++pi) {
+            if (pi >= pf.np) break;
             const int r = pf.rl[pi];
             const double f = pf.fl[pi];
             double vr = 0.0, v = 0.0;
@@ -772,6 +779,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     write_vbound();
     if (lane == 0) {
         st->nzero = nz_out ? 1 : 0;
+        st->avok = (nz_in && nz_out) ? 1 : 0;   // V' = Z' = E = X: A V' is the Y-step's AX
         if (improved_pre) optsrc = (defer_opt && pp && fast) ? zn_id : 0;
         st->optsrc = optsrc;
     }

@@ -46,7 +46,7 @@ int main() {
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int which = 0; which < 2; ++which) {
         auto run = [&]() {
-            if (which == 0) launch_i8_apply_A(nb, n, m, LA, Z, N, Y, M, T, c8, rs, 0);
+            if (which == 0) launch_i8_apply_A(nb, n, m, LA, Z, N, Y, M, T, c8, rs, N, nullptr, 0);
             else launch_i8_apply_AH(nb, m, n, LH, g, W, c8, rs, 0);
         };
         for (int i = 0; i < 3; ++i) run();

@@ -230,12 +230,25 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
         nb[h] = (int)std::max(0LL, std::min((long long)chunk, batch - ob));
         ws[h] = state_slice(w, ob, m, n);
     }
+    // Stagger: sub-batch h >= 1 starts its first iteration once sub-batch 0 has issued `stg`
+    // kernels of it, so that the sub-batches run different kernels (HBM- vs matrix-core-bound)
+    // side by side instead of the same one (ACE_STAGGER, 0 = start together)
+    static const int stg = [] {
+        const char* e = getenv("ACE_STAGGER");
+        return e ? atoi(e) : 0;
+    }();
+    hipEvent_t evs = nullptr;
+    if (stg > 0 && nsplit > 1) ACE_HIP(hipEventCreateWithFlags(&evs, hipEventDisableTiming));
+    auto stagger_mark = [&](int h, int it, int k) -> hipError_t {
+        return (evs && h == 0 && it == 1 && k == stg) ? hipEventRecord(evs, ss[0]) : hipSuccess;
+    };
     int q = 0, rc = ACE_OK;
     for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
         for (int h = 0; h < nsplit; ++h) {
             if (nb[h] == 0) continue;
             const AdmmState& wh = ws[h];
             const hipStream_t sh = ss[h];
+            if (evs && h > 0 && it == 1) ACE_HIP(hipStreamWaitEvent(sh, evs, 0));
             const double* Bh = B + (long long)h * chunk * m;
             double* Zc = (it & 1) ? wh.Z : wh.Z2;   // Z, N of the previous iterate (ping-pong)
             double* Nc = (it & 1) ? wh.N : wh.N2;
@@ -243,16 +256,19 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
                 ProfScope ps(ACE_K_APPLY_A, sh);
                 launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, w.zeros, wh.AX, sh);
             }
+            ACE_HIP(stagger_mark(h, it, 1));
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
                                  L.LK8, L.c8, wh.st, wh.AX};
                 launch_gyk(nb[h], m, ga, sh);
             }
+            ACE_HIP(stagger_mark(h, it, 2));
             {
                 ProfScope ps(ACE_K_APPLY_AH, sh);
                 launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh);
             }
+            ACE_HIP(stagger_mark(h, it, 3));
             ZArgs za = za0;
             za.it = it;
             za.wmode = 1;
@@ -293,6 +309,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
                           w.Z2);
     }
     ACE_HIP(hipGetLastError());
+    if (evs) ACE_HIP(hipEventDestroy(evs));
     for (int h = 1; h < nsplit; ++h) ACE_HIP(hipStreamDestroy(ss[h]));
     for (int h = 0; h < nsplit; ++h) ACE_HIP(hipEventDestroy(ev[h]));
     return rc;

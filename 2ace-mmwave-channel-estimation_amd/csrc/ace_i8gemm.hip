@@ -40,6 +40,17 @@
 namespace ace {
 
 namespace {
+// Phase timestamps of work-group 5 (diagnostic build only: -DACE_PHASE_STAMPS)
+#ifdef ACE_PHASE_STAMPS
+#define STAMP_DECL unsigned long long ts_[12] = {}
+#define STAMP(i) do { if (blockIdx.x == 5 && threadIdx.x == 0) ts_[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define STAMP_PRINT(name, k) do { if (blockIdx.x == 5 && threadIdx.x == 0) { printf("%s", name); for (int i_ = 1; i_ < k; ++i_) printf(" %llu", ts_[i_] - ts_[i_ - 1]); printf("\n"); } } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_PRINT(name, k)
+#endif
+
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef int i16v __attribute__((ext_vector_type(16)));
 
@@ -177,7 +188,8 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
         avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;
     }
     // Steady state of the unit path: V = X of the previous iteration for every realisation of the
-    // block (RealState::avok), so A V is the AX its Y-step stored: T = (Y - M/mu) - AX, no product.
+    // block (RealState::avok), so A V is the AX its Y-step stored and gyk_kernel forms
+    // T = (Y - M/mu) - AX itself: nothing to do here.
     if (AXp) {
         int ok = 1;
         if (t < RB) {
@@ -187,19 +199,7 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
             live_s[t] = lv;
             imu_s[t] = lv ? 1.0 / rs[j].mu : 0.0;
         }
-        if (__syncthreads_and(ok)) {   // complex pairs: 16-byte accesses
-            const int ldo = Mc, c0 = cb * (NCB / 2), cw = min(NCB / 2, ldo - c0);
-            for (int idx = t; idx < RB * cw; idx += NT) {
-                const int bl = idx / cw;
-                if (!live_s[bl]) continue;
-                const long long off = (long long)(j0 + bl) * ldo + c0 + idx - bl * cw;
-                const d2 y = reinterpret_cast<const d2*>(Yp)[off], mm = reinterpret_cast<const d2*>(Mp)[off],
-                         ax = reinterpret_cast<const d2*>(AXp)[off];
-                const double im = imu_s[bl];
-                reinterpret_cast<d2*>(Tp)[off] = make_double2(fma(-mm.x, im, y.x) - ax.x, fma(-mm.y, im, y.y) - ax.y);
-            }
-            return;
-        }
+        if (__syncthreads_and(ok)) return;   // gyk_kernel forms T itself for these realisations
     }
     const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: realisation bl, entry 32 s + cq
     const bool live = jb < nb && !rs[jb].done;
@@ -333,6 +333,8 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int j0 = blockIdx.x * RB;
     const int bl = t >> 5, cp = t & 31, jb = j0 + bl;
+    STAMP_DECL;
+    STAMP(0);
     const bool live = jb < nb && !rs[jb].done;
     const d2* g = reinterpret_cast<const d2*>(Gp) + (long long)jb * Kc;
 
@@ -395,6 +397,7 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
         for (int tt = 0; tt < 8; ++tt) *reinterpret_cast<uint32_t*>(&Ad[lds_row(bl, tt) * rst + KC * s + 4 * cp]) = d[tt];
     }
     __syncthreads();
+    STAMP(1);
 
     const int h = lane >> 5, ldo = 2 * Mc, ocb = KY ? NCB / 2 : NCB, ncb = (ldo + ocb - 1) / ocb;
     const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
@@ -459,6 +462,8 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
         __builtin_amdgcn_sched_barrier(0);
         if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc);
     }
+    STAMP(2);
+    if (!KY) STAMP_PRINT("i8ah prologue|sweep:", 3);
 }
 
 // Codebook check and expansion.  cmax = max |component| of A (device scalar).  Each
@@ -514,23 +519,43 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ double red[8][GRB][7];
     __shared__ double sc_s[GRB], p2_s[GRB];
-    __shared__ int live_s[GRB], imp_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB];
+    __shared__ double imu0_s[GRB];
     const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
     const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
     d2* Ts = reinterpret_cast<d2*>(smem);               // [16][tst]: T, then Y_new
     int8_t* Ad = reinterpret_cast<int8_t*>(smem) + ((GRB * tst * 16 + 255) & ~255);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB;
+    STAMP_DECL;
+    STAMP(0);
     if (t < GRB) {
         const int j = j0 + t;
-        live_s[t] = j < nb && !a.rs[j].done;
+        const bool lv = j < nb && !a.rs[j].done;
+        live_s[t] = lv;
+        avok_s[t] = lv && a.AX && a.rs[j].avok;
+        imu0_s[t] = lv ? 1.0 / a.rs[j].mu : 0.0;
     }
     __syncthreads();
+    // T: from apply_A, or -- when V is exactly the previous X (RealState::avok) -- formed here as
+    // T = (Y - M/mu) - AX with apply_A's expression (apply_A then writes nothing for the block)
     for (int idx = t; idx < GRB * mp; idx += NT) {
         const int jl = idx / mp, k = idx - jl * mp, j = j0 + jl;
-        Ts[jl * tst + k] = (live_s[jl] && k < m) ? reinterpret_cast<const d2*>(a.T)[(long long)j * m + k]
-                                                 : make_double2(0.0, 0.0);
+        d2 v = make_double2(0.0, 0.0);
+        if (live_s[jl] && k < m) {
+            const long long o = (long long)j * m + k;
+            if (avok_s[jl]) {
+                const d2 y = reinterpret_cast<const d2*>(a.Yo)[o], mm = reinterpret_cast<const d2*>(a.M)[o],
+                         ax = reinterpret_cast<const d2*>(a.AX)[o];
+                const double im = imu0_s[jl];
+                v = make_double2(fma(-mm.x, im, y.x) - ax.x, fma(-mm.y, im, y.y) - ax.y);
+            } else {
+                v = reinterpret_cast<const d2*>(a.T)[o];
+            }
+        }
+        Ts[jl * tst + k] = v;
     }
     __syncthreads();
+    STAMP(1);
 
     // ---- g = G T: wave w owns output tiles 2w, 2w + 1 (16 complex each)
     const int nct = mp / 16, nks = mp / 4, nstage = nks / GSK;
@@ -613,6 +638,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         }
     }
     __syncthreads();   // every wave is done with T: Ts becomes Y_new
+    STAMP(2);
 #ifdef ACE_GYK_PROBE_ONLY_A
     {
         double sacc = 0.0;
@@ -685,6 +711,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             for (int k = 0; k < 7; ++k) red[w][(lane >> 4) + 4 * r][k] = v7[r][k];
     }
     __syncthreads();
+    STAMP(3);
     if (t < GRB) {
         double v[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int q = 0; q < 8; ++q) {   // fixed order over the waves
@@ -710,6 +737,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         sc_s[t] = sc;
     }
     __syncthreads();
+    STAMP(4);
 #ifdef ACE_GYK_PROBE_P2
     return;
 #endif
@@ -739,6 +767,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         }
     }
     __syncthreads();
+    STAMP(5);
 #ifdef ACE_GYK_PROBE_NO_C
     return;
 #endif
@@ -806,6 +835,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         if ((f + 2 * SK) % nksK == 0) epilogue(f / nksK, acc);
     }
+    STAMP(6);
     // dual terms: lanes of one half-wave share realisations; then the 8 waves in fixed order
 #pragma unroll
     for (int R = 0; R < 4; ++R)
@@ -831,6 +861,8 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         a.rs[j0 + t].dAtY = dv;
         a.rs[j0 + t].nAtY = nv;
     }
+    STAMP(7);
+    STAMP_PRINT("gyk T|GT|Ystep+shfl|red+RS|optY+digits|KY|dual:", 8);
 }
 
 // G [m][m] c128 -> f64 MFMA B-operand fragments: ((ks * (mp/16) + ct) * 64 + lane) holds

@@ -278,8 +278,10 @@ def unit_flops(m, n, tx, rx):
 
 def unit_i8_ops(m, n):
     """int8 matrix-core ops executed per realisation per launch by the digit-plane applies
-    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC."""
-    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m)}
+    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC;
+    gyk_kernel's K Y: 8 digit planes of Y x 2 base-128 planes of K_int x (2m x 2m) x 2."""
+    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m),
+            "apply_G": 2.0 * 8 * 2 * (2 * m) * (2 * m)}
 
 
 def unit_bytes(m, n, tx, rx):
@@ -289,10 +291,14 @@ def unit_bytes(m, n, tx, rx):
                       zero vector (RealState::nzero) and is neither read nor written, opt_X is deferred
                       to the Z' ping-pong buffer (RealState::optsrc), and the dual terms / opt_Y come
                       from gyk_kernel's RealState fields
-      apply_A (i8):   read Z, Y, M; write T (N = 0 is read from a shared zero page)
+      apply_A (i8):   read Z, Y, M; write T (N = 0 is read from a shared zero page); in the steady
+                      state (RealState::avok) it only checks the block and gyk forms T
+      apply_G (gyk):  read Y, M, AX (T), M, Y0, B (f64), Y0 and K Y0 (dual terms); write g, M, Y, AX,
+                      K Y, opt_Y
       apply_AH (i8):  read g; write W"""
     return {
         "zstep": 16.0 * 3 * n + 16.0 * 16 * tx,
+        "apply_G": 16.0 * (3 + 2 + 2) * m + 8.0 * m + 16.0 * 6 * m,
         "apply_A": 16.0 * (n + 3 * m),
         "apply_AH": 16.0 * (m + n),
     }
@@ -325,7 +331,8 @@ def cpu_baseline(args, n_samples):
                        f"solve {t_solve:.2f}s")}
 
 
-PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel"}
+PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false>",
+              "apply_G": "gyk_kernel"}
 
 
 def _pmc_traffic(cls):
@@ -459,8 +466,24 @@ def main():
                     nsplit -= 1
             per_launch = -(-bsz // nsplit)
 
+            gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
+
             def roofline(k):
                 avg_s = kernels[k]["avg_ms"] * 1e-3
+                if k == "apply_G" and gyk:   # f64 G T + int8 K Y + the Y-step's HBM traffic, phase after phase
+                    f, o, b = uf[k] * per_launch, io[k] * per_launch, ub[k] * per_launch
+                    tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
+                    return {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
+                            "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                            "kernel": k, "flops_per_launch": f,
+                            "int8": {"achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS, "unit": "TOP/s",
+                                     "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4), "ops_per_launch": o},
+                            "hbm": {"achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                    "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
+                            "serial_frac": round((tf + to + tb) / avg_s, 4),
+                            "flop_note": "gyk_kernel runs g = G T (f64 3M; achieved counts 8 flops per complex MAC), "
+                                         "the Y-step (HBM) and K Y (int8 digit planes) one after the other in each "
+                                         "work-group; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"}
                 if k in io and i8:   # exact int8 digit planes on the matrix cores
                     per, pb = io[k] * per_launch, ub[k] * per_launch
                     return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
@@ -491,6 +514,10 @@ def main():
             dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
             roof = roofline(dom)
             roof["realisations_per_launch"] = per_launch
+            # the nsplit sub-batch launches of a class run at the same time on disjoint CUs (rocprofv3
+            # kernel trace, tools/timeline.py): the chip-level rate is nsplit x the per-launch rate
+            roof["concurrent_launches"] = nsplit
+            roof["chip_frac"] = round(roof["frac"] * nsplit, 4)
             roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
                             f"region, on every {PROF_STRIDE}rd launch of each kernel class); peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); "
                             "traffic: PMC FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source")
@@ -499,9 +526,8 @@ def main():
                 roof["traffic"], roof["traffic_source"] = tr
             gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
             roof_gemm = roofline(gemm)
-            if gemm == "apply_G" and i8 and m <= 256:
-                roof_gemm["flop_note"] = ("gyk_kernel: g = G T (counted, f64 3M on the matrix cores) plus the Y-step, "
-                                          "K Y on the int8 matrix cores and the dual terms (not counted)")
+            roof_gemm["concurrent_launches"] = nsplit
+            roof_gemm["chip_frac"] = round(roof_gemm["frac"] * nsplit, 4)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             ns = args.cpu_recoveries or 256

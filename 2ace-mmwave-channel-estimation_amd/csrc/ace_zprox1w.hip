@@ -548,11 +548,13 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     {
-                        const double st0 = dpp_shr1(Rt[r][0]), st1 = dpp_shr1(Rt[r][1]);
-                        const double sb0 = dpp_shr1(Rb[r][0]), sb1 = dpp_shr1(Rb[r][1]);
+                        // one shift for the top row: lane 0 sends its bottom column (new top(1) =
+                        // bot(0)), every other lane its top column (new top(k) = top(k-1))
+                        const double s0 = kl == 0 ? Rb[r][0] : Rt[r][0], s1 = kl == 0 ? Rb[r][1] : Rt[r][1];
+                        const double st0 = dpp_shr1(s0), st1 = dpp_shr1(s1);
                         const double lb0 = dpp_shl1(Rb[r][0]), lb1 = dpp_shl1(Rb[r][1]);
-                        const double nt0 = kl == 0 ? Rt[r][0] : (kl == 1 ? sb0 : st0);
-                        const double nt1 = kl == 0 ? Rt[r][1] : (kl == 1 ? sb1 : st1);
+                        const double nt0 = kl == 0 ? Rt[r][0] : st0;
+                        const double nt1 = kl == 0 ? Rt[r][1] : st1;
                         const double nb0 = kl == P - 1 ? Rt[r][0] : lb0;
                         const double nb1 = kl == P - 1 ? Rt[r][1] : lb1;
                         if (act) {

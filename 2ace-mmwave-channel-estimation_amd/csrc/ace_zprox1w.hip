@@ -545,6 +545,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                 // new top(k) = top(0) | bot(0) | top(k-1) for k = 0 | 1 | >=2; new bot(k) = bot(k+1) | top(P-1).
                 // The shifts run on every lane (DPP sources must be active); lanes k >= P keep theirs.
                 const bool act = P > 1 && kl < P;
+                // every lane of each 16-lane row takes part when tx = 32 (P = 16): that case runs
+                // without the per-lane masking selects
+                auto shift = [&](bool all) {
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     {
@@ -557,7 +560,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                         const double nt1 = kl == 0 ? Rt[r][1] : st1;
                         const double nb0 = kl == P - 1 ? Rt[r][0] : lb0;
                         const double nb1 = kl == P - 1 ? Rt[r][1] : lb1;
-                        if (act) {
+                        if (all || act) {
                             Rt[r][0] = nt0;
                             Rt[r][1] = nt1;
                             Rb[r][0] = nb0;
@@ -565,6 +568,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                         }
                     }
                 }
+                };
+                if (P == 16) shift(true);
+                else shift(false);
             }
             cur ^= 1;
             __syncthreads();

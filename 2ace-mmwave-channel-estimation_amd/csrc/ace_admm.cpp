@@ -260,7 +260,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                                 L.LK8, L.c8, wh.st, wh.AX};
+                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q};
                 launch_gyk(nb[h], m, ga, sh);
             }
             ACE_HIP(stagger_mark(h, it, 2));
@@ -306,7 +306,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     {
         ProfScope ps(ACE_K_FINAL, st);
         launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st, w.Z,
-                          w.Z2);
+                          w.Z2, w.Y[0], w.Y[1]);
     }
     ACE_HIP(hipGetLastError());
     if (evs) ACE_HIP(hipEventDestroy(evs));
@@ -405,7 +405,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         if (gyk) {
             ProfScope ps(ACE_K_APPLY_G, st);
             const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st,
-                             w.AX};
+                             w.AX, 2 - q};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st);
@@ -462,7 +462,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     {
         ProfScope ps(ACE_K_FINAL, st);
         launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, wmode ? w.V : w.X, w.Y[q], Xo, Yo, iters, status,
-                          mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr);
+                          mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr, gyk ? w.Y[0] : nullptr,
+                          gyk ? w.Y[1] : nullptr);
     }
     ACE_HIP(hipGetLastError());
     return ACE_OK;

@@ -41,7 +41,9 @@ struct RealState {
     // on entry and Z' = E = X): A V is then the AX = (Y - M/mu) - g that gyk_kernel stored, and
     // apply_A skips its product (ace_i8gemm.hip::i8a_kernel)
     int32_t avok;
-    int32_t pad_i;
+    // where opt_Y lives (gyk_kernel, like optsrc for opt_X): 0 the opt_Y buffer; 1 / 2 the Y[0] /
+    // Y[1] ping-pong buffer holding the best Y_new, copied only before that buffer is overwritten
+    int32_t optysrc;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -150,6 +152,7 @@ struct GykArgs {
     const double* c8;   // c, c^2
     RealState* rs;
     double* AX;         // optional: AX = (Y - M/mu) - g of the Y-step ([nb][m]), apply_A's next A V
+    int yn_id;          // 1 + index of Yn in the Y ping-pong pair: opt_Y deferred (RealState::optysrc); 0 = copy
 };
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
@@ -261,7 +264,8 @@ void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, cons
 void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
                        const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters,
                        uint32_t* status, double* mu, RealState* rs, hipStream_t st,
-                       const double* Zb1 = nullptr, const double* Zb2 = nullptr);
+                       const double* Zb1 = nullptr, const double* Zb2 = nullptr, const double* Yb1 = nullptr,
+                       const double* Yb2 = nullptr);
 void launch_conj_transpose(int rows, int cols, const double* A, double* AH, hipStream_t st);
 void launch_synth_codebook(uint64_t seed, long long first, int count, int m, int n, double* A, hipStream_t st);
 void launch_synth_channels(uint64_t seed, long long first, int count, int m, int tx, int rx, int L, double snr_db,

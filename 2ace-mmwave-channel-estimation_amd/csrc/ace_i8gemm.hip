@@ -519,7 +519,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ double red[8][GRB][7];
     __shared__ double sc_s[GRB], p2_s[GRB];
-    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB];
     __shared__ double imu0_s[GRB];
     const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
     const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
@@ -534,8 +534,17 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         live_s[t] = lv;
         avok_s[t] = lv && a.AX && a.rs[j].avok;
         imu0_s[t] = lv ? 1.0 / a.rs[j].mu : 0.0;
+        oys_s[t] = lv ? a.rs[j].optysrc : 0;
     }
     __syncthreads();
+    // deferred opt_Y (RealState::optysrc): the best Y_new still lives in the buffer this iteration's
+    // Y-step is about to overwrite -- save it first (rare: no better iterate in the last iteration)
+    if (a.yn_id)
+        for (int r = 0; r < GRB; ++r)
+            if (oys_s[r] == a.yn_id)
+                for (int i = t; i < m; i += NT)
+                    reinterpret_cast<d2*>(a.optY)[(long long)(j0 + r) * m + i] =
+                        reinterpret_cast<const d2*>(a.Yn)[(long long)(j0 + r) * m + i];
     // T: from apply_A, or -- when V is exactly the previous X (RealState::avok) -- formed here as
     // T = (Y - M/mu) - AX with apply_A's expression (apply_A then writes nothing for the block)
     for (int idx = t; idx < GRB * mp; idx += NT) {
@@ -731,6 +740,8 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             rs.dY2 = v[4];
             imp = sqrt(v[0]) < rs.opt_obj;   // iter_control makes the same decision (opt_Y here)
             plane_scale(v[5] + v[6], a.c8[1], p2, sc);
+            if (a.yn_id)   // opt_Y deferred: Y_new stays in Yn until that buffer comes round again
+                rs.optysrc = imp ? a.yn_id : (oys_s[t] == a.yn_id ? 0 : oys_s[t]);
         }
         imp_s[t] = imp;
         p2_s[t] = p2;
@@ -743,7 +754,8 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
 #endif
     for (int idx = t; idx < GRB * m; idx += NT) {   // opt_Y (:344-351)
         const int jl = idx / m, i = idx - jl * m;
-        if (live_s[jl] && imp_s[jl]) reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
+        if (!a.yn_id && live_s[jl] && imp_s[jl])
+            reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
     }
 #ifdef ACE_GYK_PROBE_P3
     return;

@@ -193,14 +193,16 @@ __global__ __launch_bounds__(256) void finalize_r_kernel(int n, int m, int r, in
                                                          const double* optY, const double* Xcur, const double* Ycur,
                                                          double* Xo, double* Yo, int32_t* iters, uint32_t* status,
                                                          double* muo, RealState* st, const double* Zb1,
-                                                         const double* Zb2) {
+                                                         const double* Zb2, const double* Yb1, const double* Yb2) {
     const int b = blockIdx.x;
     const bool have = st[b].opt_obj < INFINITY;
     const int os = st[b].optsrc;   // deferred opt_X copy (r = 1 wmode): the Z / Z2 buffer holds it
     const double* ox = (os == 1 && Zb1) ? Zb1 : ((os == 2 && Zb2) ? Zb2 : optX);
     const d2* sx = have ? reinterpret_cast<const d2*>(ox) + (long long)b * nc * n
                         : reinterpret_cast<const d2*>(Xcur) + (long long)b * r * n;
-    const d2* sy = have ? reinterpret_cast<const d2*>(optY) + (long long)b * nc * m
+    const int oy = st[b].optysrc;   // deferred opt_Y copy (gyk_kernel): the Y[0] / Y[1] buffer holds it
+    const double* oyp = (oy == 1 && Yb1) ? Yb1 : ((oy == 2 && Yb2) ? Yb2 : optY);
+    const d2* sy = have ? reinterpret_cast<const d2*>(oyp) + (long long)b * nc * m
                         : reinterpret_cast<const d2*>(Ycur) + (long long)b * r * m;
     d2* dx = reinterpret_cast<d2*>(Xo) + (long long)b * nc * n;
     d2* dy = reinterpret_cast<d2*>(Yo) + (long long)b * nc * m;
@@ -443,9 +445,10 @@ void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, cons
 }
 void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
                        const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
-                       double* mu, RealState* rs, hipStream_t st, const double* Zb1, const double* Zb2) {
+                       double* mu, RealState* rs, hipStream_t st, const double* Zb1, const double* Zb2,
+                       const double* Yb1, const double* Yb2) {
     hipLaunchKernelGGL(finalize_r_kernel, dim3(batch), dim3(256), 0, st, n, m, r, nc, optX, optY, Xc, Yc, Xo, Yo,
-                       iters, status, mu, rs, Zb1, Zb2);
+                       iters, status, mu, rs, Zb1, Zb2, Yb1, Yb2);
 }
 
 void launch_anorm(int m, int n, const double* A, double tol_abs, double* anorm, hipStream_t st) {

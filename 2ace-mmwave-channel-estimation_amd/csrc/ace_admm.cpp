@@ -252,15 +252,11 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             const double* Bh = B + (long long)h * chunk * m;
             double* Zc = (it & 1) ? wh.Z : wh.Z2;   // Z, N of the previous iterate (ping-pong)
             double* Nc = (it & 1) ? wh.N : wh.N2;
-            {
-                ProfScope ps(ACE_K_APPLY_A, sh);
-                launch_i8_apply_A(nb[h], n, m, L.LA8, Zc, Nc, wh.Y[q], wh.M, wh.T, L.c8, wh.st, w.zeros, wh.AX, sh);
-            }
             ACE_HIP(stagger_mark(h, it, 1));
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q};
+                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n};
                 launch_gyk(nb[h], m, ga, sh);
             }
             ACE_HIP(stagger_mark(h, it, 2));
@@ -392,7 +388,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
-        if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
+        if (i8 && !gyk) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
@@ -405,7 +401,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         if (gyk) {
             ProfScope ps(ACE_K_APPLY_G, st);
             const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st,
-                             w.AX, 2 - q};
+                             w.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st);

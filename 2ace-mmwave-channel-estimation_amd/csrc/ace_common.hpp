@@ -153,6 +153,13 @@ struct GykArgs {
     RealState* rs;
     double* AX;         // optional: AX = (Y - M/mu) - g of the Y-step ([nb][m]), apply_A's next A V
     int yn_id;          // 1 + index of Yn in the Y ping-pong pair: opt_Y deferred (RealState::optysrc); 0 = copy
+    // apply_A folded in (LA != nullptr): T = (Y - M/mu) - A (Z - N/mu) for blocks with a realisation
+    // whose V is not the previous X (RealState::avok), on the int8 matrix cores, straight into LDS
+    const int8_t* LA;   // launch_i8_expand image of A
+    const double* Z;
+    const double* N;
+    const double* zeros;
+    int n;
 };
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)

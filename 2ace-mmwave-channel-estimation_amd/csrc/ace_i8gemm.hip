@@ -171,36 +171,18 @@ __device__ __forceinline__ void stage_mma(const int8_t* arow, int rstride, const
 // apply_A:  T = (Y - M/mu) - c A V,  V = Z - N/mu  (K = n complex, outputs m complex).
 constexpr int SKR = SK * 32;       // K reals per stage
 constexpr int RSA = SKR + 16;      // LDS row stride of a stage image (bytes): conflict-free b128 reads
-__global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
-                                                    const double* __restrict__ Zp, const double* __restrict__ Np,
-                                                    const double* __restrict__ Yp, const double* __restrict__ Mp,
-                                                    double* __restrict__ Tp, const double* __restrict__ cptr,
-                                                    const RealState* __restrict__ rs, const double* __restrict__ zeros,
-                                                    const double* __restrict__ AXp) {
-    __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
-    __shared__ double sc_s[RB], imu_s[RB];
-    __shared__ int live_s[RB], avok_s[RB];
-
+// The body of one 16-realisation block (blockIdx-free): A8 = 2 x ROWS x RSA bytes of LDS, the four
+// per-realisation scratch arrays in LDS (avok_s filled by the caller).  TOL: T goes to LDS rows
+// of ldt doubles (gyk_kernel) instead of the global [nb][2 Mc] array.
+template <bool TOL>
+__device__ __forceinline__ void i8a_block(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                          const double* __restrict__ Zp, const double* __restrict__ Np,
+                                          const double* __restrict__ Yp, const double* __restrict__ Mp,
+                                          double* __restrict__ Tp, int ldt, const double* __restrict__ cptr,
+                                          const RealState* __restrict__ rs, const double* __restrict__ zeros,
+                                          const double* __restrict__ AXp, int8_t (*As)[ROWS * RSA], double* sc_s,
+                                          double* imu_s, int* live_s, const int* avok_s, int j0, int cb) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int j0 = blockIdx.x * RB, cb = blockIdx.y;
-    if (t < RB) {   // per realisation (the result never depends on the block it shares)
-        const int j = j0 + t;
-        avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;
-    }
-    // Steady state of the unit path: V = X of the previous iteration for every realisation of the
-    // block (RealState::avok), so A V is the AX its Y-step stored and gyk_kernel forms
-    // T = (Y - M/mu) - AX itself: nothing to do here.
-    if (AXp) {
-        int ok = 1;
-        if (t < RB) {
-            const int j = j0 + t;
-            const bool lv = j < nb && !rs[j].done;
-            ok = !lv || rs[j].avok;
-            live_s[t] = lv;
-            imu_s[t] = lv ? 1.0 / rs[j].mu : 0.0;
-        }
-        if (__syncthreads_and(ok)) return;   // gyk_kernel forms T itself for these realisations
-    }
     const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: realisation bl, entry 32 s + cq
     const bool live = jb < nb && !rs[jb].done;
     const double imu = live ? 1.0 / rs[jb].mu : 0.0;
@@ -303,9 +285,30 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
                 const long long off = (long long)j * ldo + col;
                 // a realisation with RealState::avok takes A V = AX in any block
                 const double av = avok_s[blo] ? AXp[off] : scb * recombine(acc[R][c], q);
-                Tp[off] = fma(-Mp[off], im, Yp[off]) - av;
+                const double tv = fma(-Mp[off], im, Yp[off]) - av;
+                if (TOL) Tp[blo * ldt + col] = tv;
+                else Tp[off] = tv;
             }
         }
+}
+
+__global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                                    const double* __restrict__ Zp, const double* __restrict__ Np,
+                                                    const double* __restrict__ Yp, const double* __restrict__ Mp,
+                                                    double* __restrict__ Tp, const double* __restrict__ cptr,
+                                                    const RealState* __restrict__ rs, const double* __restrict__ zeros,
+                                                    const double* __restrict__ AXp) {
+    __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
+    __shared__ double sc_s[RB], imu_s[RB];
+    __shared__ int live_s[RB], avok_s[RB];
+    const int t = threadIdx.x, j0 = blockIdx.x * RB;
+    if (t < RB) {   // per realisation (the result never depends on the block it shares)
+        const int j = j0 + t;
+        avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;
+    }
+    __syncthreads();
+    i8a_block<false>(nb, Kc, Mc, nks, Bf, Zp, Np, Yp, Mp, Tp, 0, cptr, rs, zeros, AXp, As, sc_s, imu_s, live_s, avok_s,
+                     j0, blockIdx.y);
 }
 
 // apply_AH in the Z-step's wmode:  W = c A^H g  (K = m complex, outputs n complex).
@@ -545,8 +548,19 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
                 for (int i = t; i < m; i += NT)
                     reinterpret_cast<d2*>(a.optY)[(long long)(j0 + r) * m + i] =
                         reinterpret_cast<const d2*>(a.Yn)[(long long)(j0 + r) * m + i];
-    // T: from apply_A, or -- when V is exactly the previous X (RealState::avok) -- formed here as
-    // T = (Y - M/mu) - AX with apply_A's expression (apply_A then writes nothing for the block)
+    // T = (Y - M/mu) - A V.  A block with a realisation whose V is not the previous X runs the
+    // digit-plane product (apply_A's block body, digit stages in the Ad region, T into Ts; the
+    // realisations with RealState::avok take A V = AX there too); otherwise T is formed here as
+    // (Y - M/mu) - AX with the same expression.
+    int need = 0;
+    if (a.LA && t < GRB) need = live_s[t] && !avok_s[t];
+    if (__syncthreads_or(need)) {
+        for (int idx = t; idx < GRB * tst; idx += NT) Ts[idx] = make_double2(0.0, 0.0);   // padding, dead rows
+        __syncthreads();
+        i8a_block<true>(nb, a.n, m, i8_nks_dev(a.n), reinterpret_cast<const i4v*>(a.LA), a.Z, a.N, a.Yo, a.M,
+                        reinterpret_cast<double*>(Ts), 2 * tst, a.c8, a.rs, a.zeros, a.AX,
+                        reinterpret_cast<int8_t(*)[ROWS * RSA]>(Ad), sc_s, p2_s, live_s, avok_s, j0, 0);
+    } else
     for (int idx = t; idx < GRB * mp; idx += NT) {
         const int jl = idx / mp, k = idx - jl * mp, j = j0 + jl;
         d2 v = make_double2(0.0, 0.0);
@@ -958,8 +972,9 @@ void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double*
                        reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs);
 }
 size_t gyk_gfrag_bytes(int m) { return (size_t)gyk_mp(m) * gyk_mp(m) * 16; }
-size_t gyk_lds_bytes(int m) {
-    return (((size_t)GRB * (gyk_mp(m) + 1) * 16 + 255) & ~(size_t)255) + i8ah_lds_bytes(m);
+size_t gyk_lds_bytes(int m) {   // Ts, then the Ad region: K Y digit planes, or apply_A's digit stages
+    return (((size_t)GRB * (gyk_mp(m) + 1) * 16 + 255) & ~(size_t)255) +
+           (i8ah_lds_bytes(m) > (size_t)2 * ROWS * RSA ? i8ah_lds_bytes(m) : (size_t)2 * ROWS * RSA);
 }
 void launch_gyk_gfrag(int m, const double* G, double* Gf, hipStream_t st) {
     const long long tot = (long long)gyk_mp(m) * gyk_mp(m);

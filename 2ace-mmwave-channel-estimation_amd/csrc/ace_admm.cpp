@@ -388,7 +388,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
-        if (i8 && !gyk) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
+        if (gyk) {
+            // T = (Y - M/mu) - A V is formed inside gyk_kernel (apply_A folded in)
+        } else if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep

@@ -246,3 +246,31 @@ def test_split_streams_match_single_batch(gpu):
         torch.cuda.synchronize()
         assert np.array_equal(sub.X.cpu().numpy(), Xb[lo:lo + 64]), lo
         assert np.array_equal(sub.iters.cpu().numpy(), big.iters.cpu().numpy()[lo:lo + 64])
+
+
+@pytest.mark.parametrize("batch", [64, 1024])
+def test_unit_path_launches_three_kernels_per_iteration(gpu, batch):
+    """The phase-code r = 1 iteration is gyk_kernel + apply_AH + Z-step: no apply_A, pre, Y-step
+    or K Y launch (with and without concurrent sub-batches), one launch of each per iteration and
+    sub-batch."""
+    import ctypes as C
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    from ace_amd._lib import LIB, KERNEL_CLASSES, check
+    A, B, X0, _ = synth_problem(31, 0, batch, 256, 32, 32)
+    iters = 20
+    infer_admm_batch(A, B, X0, 32, 32, maxiter=iters, fixed_iters=True)   # warm-up (setup caches)
+    torch.cuda.synchronize()
+    check(LIB.ace_prof_sample(1, 0))
+    check(LIB.ace_prof_start(4096))
+    infer_admm_batch(A, B, X0, 32, 32, maxiter=iters, fixed_iters=True)
+    torch.cuda.synchronize()
+    kt = (C.c_double * len(KERNEL_CLASSES))()
+    kn = (C.c_int32 * len(KERNEL_CLASSES))()
+    check(LIB.ace_prof_stop(kt, kn))
+    n = dict(zip(KERNEL_CLASSES, kn))
+    subs = 2 if batch >= 512 else 1
+    for k in ("apply_A", "pre", "ystep", "apply_K"):
+        assert n[k] == 0, (k, n)
+    for k in ("apply_G", "apply_AH", "zstep"):
+        assert n[k] == iters * subs, (k, n)

@@ -474,17 +474,27 @@ def main():
                 if k == "apply_G" and gyk:   # f64 G T + int8 K Y + the Y-step's HBM traffic, phase after phase
                     f, o, b = uf[k] * per_launch, io[k] * per_launch, ub[k] * per_launch
                     tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
-                    return {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
-                            "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "traffic": None,
-                            "kernel": k, "flops_per_launch": f,
-                            "int8": {"achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS, "unit": "TOP/s",
-                                     "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4), "ops_per_launch": o},
-                            "hbm": {"achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                    "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
-                            "serial_frac": round((tf + to + tb) / avg_s, 4),
-                            "flop_note": "gyk_kernel runs g = G T (f64 3M; achieved counts 8 flops per complex MAC), "
-                                         "the Y-step (HBM) and K Y (int8 digit planes) one after the other in each "
-                                         "work-group; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"}
+                    res = {
+                        "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
+                                "flops_per_launch": f},
+                        "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
+                                 "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
+                                 "ops_per_launch": o},
+                        "hbm": {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
+                    }
+                    # the bound is the resource that needs the most time at its peak
+                    main = max((("f64", tf), ("int8", to), ("hbm", tb)), key=lambda x: x[1])[0]
+                    out = dict(res[main])
+                    out.update({"traffic": None, "kernel": k, "resource": main,
+                                "other_resources": {r: v for r, v in res.items() if r != main},
+                                "serial_frac": round((tf + to + tb) / avg_s, 4),
+                                "flop_note": "gyk_kernel runs g = G T (f64 3M; f64 achieved counts 8 flops per complex "
+                                             "MAC), the Y-step (HBM) and K Y (int8 digit planes) one after the other in "
+                                             "each work-group; bound = the resource with the largest time at peak; "
+                                             "serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"})
+                    return out
                 if k in io and i8:   # exact int8 digit planes on the matrix cores
                     per, pb = io[k] * per_launch, ub[k] * per_launch
                     return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,

@@ -1,0 +1,41 @@
+"""The roofline accounting of bench.py: algorithmic bytes / ops per realisation and
+iteration of the unit path, and the bench contract's metric name.  Host-only."""
+import importlib.util
+import pathlib
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_unit_bytes_match_design():
+    b = _bench()
+    m, n, tx = 256, 1024, 32
+    ub = b.unit_bytes(m, n, tx, tx)
+    # Z-step steady state: read W, Z (n complex each) and Q's top 16 columns (tx x 16); write Z'
+    assert ub["zstep"] == 16 * 3 * n + 16 * 16 * tx == 56 * 1024
+    # gyk: read Y, M, AX, M, Y0, B (f64), Y0, KY0; write g, M, Y, AX, KY, opt_Y
+    assert ub["apply_G"] == 54 * 1024
+    # apply_AH: read g, write W
+    assert ub["apply_AH"] == 16 * (m + n)
+
+
+def test_int8_ops_and_flops():
+    b = _bench()
+    io = b.unit_i8_ops(256, 1024)
+    assert io["apply_AH"] == 2 * 8 * 2048 * 512 == io["apply_A"]
+    assert io["apply_G"] == 2 * 8 * 2 * 512 * 512      # K Y: 8 digit planes of Y x 2 planes of K_int
+    uf = b.unit_flops(256, 1024, 32, 32)
+    assert uf["apply_G"] == 8 * 256 * 256              # g = G T, 8 flops per complex MAC
+
+
+def test_metric_is_baselines():
+    import json
+    b = _bench()
+    base = json.loads((ROOT / "BASELINE.json").read_text())
+    assert b.METRIC == base["metric"]

@@ -37,8 +37,14 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->m = m;
     L->n = n;
     L->AH = shared ? cv.take(cz * n * m) : nullptr;
-    L->K = cv.take(cz * mats * m * m);
-    L->G = cv.take(cz * mats * m * m);
+    const bool pc = !shared && pc_supported(m, n);   // room for the private phase-code path
+    L->K = cv.take(mats * std::max(cz * m * m, pc ? pc_gw_bytes(m) : 0));
+    L->G = cv.take(mats * std::max(cz * m * m, pc ? pc_gt_bytes(m) : 0));
+    L->pcodes = pc ? cv.take<uint32_t>(pc_codes_bytes(m, n) * (size_t)batch) : nullptr;
+    L->pcb = pc ? cv.take(sizeof(double) * (size_t)batch) : nullptr;
+    L->pcflag = pc ? cv.take<int>(sizeof(int)) : nullptr;
+    L->pc_ok = false;
+    L->batch = batch;
     L->ns = shared ? cv.take(cz * 4 * m * m) : nullptr;
     L->LA8 = shared ? cv.take<int8_t>(i8_frag_bytes(m, n)) : nullptr;
     L->LAH8 = shared ? cv.take<int8_t>(i8_frag_bytes(n, m)) : nullptr;
@@ -127,11 +133,33 @@ int ns_inverse(LinOps& L, hipStream_t st) {
     return ACE_OK;
 }
 
+// Private phase-code codebooks: code images, then G_b from the exact K_b (ace_private.hip).
+// Returns with L.pc_ok = false (and nothing else changed) when some A_b is not a phase code.
+static int pc_setup(LinOps& L, int batch, hipStream_t st) {
+    const int m = L.m, n = L.n;
+    L.pc_ok = false;
+    if (L.shared || !L.pcodes || !L.allow_i8 || i8_disabled() || !pc_supported(m, n) || batch != L.batch) return ACE_OK;
+    ACE_HIP(hipMemsetAsync(L.pcflag, 0, sizeof(int), st));
+    launch_pc_pack(batch, m, n, L.A, L.pcb, L.pcodes, L.pcflag, st);
+    int flag = 1;
+    ACE_HIP(hipMemcpyAsync(&flag, L.pcflag, sizeof(int), hipMemcpyDeviceToHost, st));
+    ACE_HIP(hipStreamSynchronize(st));
+    if (flag != 0) return ACE_OK;
+    launch_pc_ginv(batch, m, n, L.pcodes, L.pcb, L.K, L.G, st);
+    ACE_HIP(hipGetLastError());
+    L.pc_ok = true;
+    return ACE_OK;
+}
+
 int linops_setup(LinOps& L, int batch, hipStream_t st) {
     const int m = L.m, n = L.n;
     const int mats = L.shared ? 1 : batch;
     const long long mm = (long long)m * m, mn = (long long)m * n;
     ProfScope ps(ACE_K_SETUP, st);
+    if (!L.shared) {
+        ACE_TRY(pc_setup(L, batch, st));
+        if (L.pc_ok) return ACE_OK;
+    }
     // K[j][i] = sum_k conj(A[i][k]) A[j][k]  : GEMM with L = conj(A), V = rows of A
     launch_zgemm(0, true, m, n, m, L.A, n, mn, L.A, n, mn, L.K, nullptr, m, mm, mats, st);
     if (L.shared) {
@@ -323,8 +351,10 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const bool fused = fast && L.shared;              // pre_kernel folded into the shared-A GEMMs
     // phase-code A: int8 digit-plane applies; apply_AH writes W = A^H g and the Z-step forms X
     const bool i8 = fused && L.i8ok && zstep_takes_w(p.variant, r);
-    const bool wmode = i8;
-    const bool gyk = wmode && L.gyk_ok;               // g, Y-step, K Y and the dual terms in one kernel
+    const bool gyk = i8 && L.gyk_ok;                  // g, Y-step, K Y and the dual terms in one kernel
+    // private phase-code codebooks: T, g = G T, Y-step, W = A^H g and the dual terms in one kernel
+    const bool pc = !L.shared && L.pc_ok && r == 1 && zstep_takes_w(p.variant, r);
+    const bool wmode = i8 || pc;
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -377,7 +407,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st);
         za.it = 0;
         launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)
-        applyMM(L.K, w.Y[0], w.KY[0]);                           // K*Y (for A'*Y terms)
+        if (!pc) applyMM(L.K, w.Y[0], w.KY[0]);                  // K*Y (for A'*Y terms)
     }
     ACE_HIP(hipGetLastError());
 
@@ -388,7 +418,12 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
-        if (gyk) {
+        if (pc) {
+            ProfScope ps(ACE_K_APPLY_G, st);
+            const PgkArgs pa{m, n, L.pcodes, L.pcodes + pc_codesA_off(batch, m, n), L.G, L.pcb, B, w.Y[q], w.M,
+                             w.Y[1 - q], w.X, w.optY, w.st, w.AX, 2 - q, Zc, Nc, w.zeros};
+            launch_pgk(batch, pa, st);
+        } else if (gyk) {
             // T = (Y - M/mu) - A V is formed inside gyk_kernel (apply_A folded in)
         } else if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
@@ -400,7 +435,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
             { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }      // T = S - A V
         }
-        if (gyk) {
+        if (pc) {
+            // g, the Y-step, W = A^H g and the dual terms came from pgk_kernel
+        } else if (gyk) {
             ProfScope ps(ACE_K_APPLY_G, st);
             const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st,
                              w.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n};
@@ -417,12 +454,12 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
             }
         }
-        if (!gyk) {   // K Y
+        if (!gyk && !pc) {   // K Y
             ProfScope ps(ACE_K_APPLY_K, st);
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
         }
-        {
+        if (!pc) {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
             if (wmode) launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st);
             else if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
@@ -437,7 +474,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             za.Nn = No;
         }
         za.ypart = fused && !gyk ? w.ypart : nullptr;
-        za.yfused = gyk;
+        za.yfused = gyk || pc;
         za.ytiles = (m + 63) / 64;
         za.Ynew = w.Y[1 - q];
         za.Yold = w.Y[q];
@@ -460,8 +497,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     {
         ProfScope ps(ACE_K_FINAL, st);
         launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, wmode ? w.V : w.X, w.Y[q], Xo, Yo, iters, status,
-                          mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr, gyk ? w.Y[0] : nullptr,
-                          gyk ? w.Y[1] : nullptr);
+                          mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr, (gyk || pc) ? w.Y[0] : nullptr,
+                          (gyk || pc) ? w.Y[1] : nullptr);
     }
     ACE_HIP(hipGetLastError());
     return ACE_OK;

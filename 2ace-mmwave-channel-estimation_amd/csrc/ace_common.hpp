@@ -172,6 +172,41 @@ void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, 
 // out[0] = max |x_i| over n doubles
 void launch_max_abs(long long n, const double* x, double* out, hipStream_t st);
 
+// Private phase-code codebooks (ace_private.hip): 2-bit code images of each A_b, G_b = (I + A_b A_b^H)^{-1}
+// as lower 16 x 16 tiles, and the per-realisation iteration kernel (T, g = G T, Y-step, W = A^H g and the
+// dual terms on the int8 matrix cores).
+constexpr int PC_MAXM = 256, PC_MAXN = 2048;
+bool pc_supported(int m, int n);
+size_t pc_codes_bytes(int m, int n);             // per realisation (uint32 images)
+size_t pc_codesA_off(int batch, int m, int n);   // dword offset of the A images in the batch's code buffer
+size_t pc_gw_bytes(int m);                       // Gauss-Jordan workspace per realisation
+size_t pc_gt_bytes(int m);                       // G tiles per realisation
+// cb[b] = max |component| of A_b; codes; *flag |= 1 unless every entry of every A_b is cb[b] j^k
+void launch_pc_pack(int batch, int m, int n, const double* A, double* cb, uint32_t* codes, int* flag, hipStream_t st);
+// Gw <- I + A A^H (exact from the codes), inverted in place; Gt <- its lower tiles
+void launch_pc_ginv(int batch, int m, int n, const uint32_t* codes, const double* cb, double* Gw, double* Gt,
+                    hipStream_t st);
+struct PgkArgs {
+    int m, n;
+    const uint32_t* codesH;   // A^H images of the batch (launch_pc_pack)
+    const uint32_t* codesA;   // A images (codes + pc_codesA_off)
+    const double* Gt;
+    const double* cb;
+    const double* B;
+    const double* Yo;
+    double* M;
+    double* Yn;
+    double* W;                // [b][n] c128 out: W = A^H g (the Z-step's wmode forms X)
+    double* optY;
+    RealState* rs;
+    double* AX;
+    int yn_id;                // as GykArgs::yn_id
+    const double* Z;          // V = Z - N/mu for the cold A V
+    const double* N;
+    const double* zeros;
+};
+void launch_pgk(int batch, const PgkArgs& a, hipStream_t st);
+
 // Arguments of the Z-step kernel (ace_zprox.hip).
 struct ZArgs {
     int n, m, tx, rx;

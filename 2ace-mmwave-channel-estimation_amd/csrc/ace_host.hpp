@@ -124,6 +124,13 @@ struct LinOps {
     double* Gf;     // G in f64 MFMA fragment order for gyk_kernel (m <= GYK_MAXM), set when gyk_ok
     bool gyk_ok;
     bool allow_i8;  // caller's choice (ace_admm_cfg::f64_applies == 0), set before linops_setup
+    // private regime, phase-code A_b (ace_private.hip): 2-bit code images, c_b, and G_b as lower
+    // tiles in G (K holds the Gauss-Jordan workspace); pc_ok is set by linops_setup
+    uint32_t* pcodes;
+    double* pcb;
+    int* pcflag;
+    bool pc_ok;
+    int batch;      // realisations of the private operators
 };
 size_t linops_bytes(bool shared, int batch, int m, int n);
 void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L);

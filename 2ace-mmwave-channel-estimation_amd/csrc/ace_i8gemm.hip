@@ -33,9 +33,7 @@
 // bound |Z| + |N|/mu formed as Z and N are written); apply_AH takes max|g| over the
 // realisation's m entries in a pre-pass.  A non-finite bound yields NaN outputs for that
 // realisation (the f64 product would not be finite either).
-#include "ace_common.hpp"
-
-#include <cfloat>
+#include "ace_i8.hpp"
 
 namespace ace {
 
@@ -51,9 +49,6 @@ namespace {
 #define STAMP_PRINT(name, k)
 #endif
 
-typedef int i4v __attribute__((ext_vector_type(4)));
-typedef int i16v __attribute__((ext_vector_type(16)));
-
 constexpr int RB = 16;           // realisations per work-group
 constexpr int ROWS = RB * 8;     // MFMA rows per work-group (realisation, digit)
 constexpr int KC = 128;          // K padding granule (reals) and apply_AH's staging block
@@ -62,13 +57,6 @@ constexpr int NT = 512;          // threads (8 waves)
 constexpr int KSC = KC / 32;     // MFMA K-steps per granule
 
 __device__ __forceinline__ int i8_nks_dev(int kc) { return (2 * kc + KC - 1) / KC * KSC; }
-
-// LDS row of (realisation bl in 0..15, digit t in 0..7): inverse of the accumulator map
-// row = (g & 3) + 8 (g >> 2) + 4 h  ->  realisation 4R + 2 (g >> 3) + h, digit (g & 3) + 4 ((g >> 2) & 1)
-__device__ __forceinline__ int lds_row(int bl, int t) {
-    const int R = bl >> 2, q = (bl >> 1) & 1, h = bl & 1;
-    return 32 * R + 16 * q + 8 * (t >> 2) + 4 * h + (t & 3);
-}
 
 // Fixed-point digits of 2 complex entries (4 reals) as 8 packed dwords (byte i = real i).
 __device__ __forceinline__ void digits4(const double (&v)[4], double p2, uint32_t (&out)[8]) {
@@ -97,11 +85,6 @@ __device__ __forceinline__ void digits4(const double (&v)[4], double p2, uint32_
     }
 }
 
-__device__ __forceinline__ int exp_of(double bound) {
-    int e = bound > 0.0 ? ilogb(bound) + 1 : 0;
-    return e < -960 ? -960 : (e > 1000 ? 1000 : e);
-}
-
 // A fragments of one K-step from the LDS digit image: rows 32R + (lane & 31), k bytes
 // 16 (lane >> 5) .. +15 of the step.
 __device__ __forceinline__ void aload(const int8_t* arow, int rstride, i4v (&af)[4]) {
@@ -119,23 +102,6 @@ __device__ __forceinline__ void kstep(const i4v (&af)[4], i4v b0, i4v b1, i16v (
         acc[R][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], b0, acc[R][0], 0, 0, 0);
         acc[R][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[R], b1, acc[R][1], 0, 0, 0);
     }
-}
-
-// Recombined digit planes of output column col for realisation 4R + 2q + (lane >> 5):
-// sum_t acc[8q + t] 128^t (Horner from the signed top digit).
-__device__ __forceinline__ double recombine(const i16v& a, int q) {
-    double v = (double)a[8 * q + 7];
-#pragma unroll
-    for (int tt = 6; tt >= 0; --tt) v = fma(v, 128.0, (double)a[8 * q + tt]);
-    return v;
-}
-
-// Exponent and scale of one realisation's digit planes from a bound on max|component|.
-__device__ __forceinline__ void plane_scale(double bound, double c, double& p2, double& sc) {
-    const bool finite = bound <= DBL_MAX;
-    const int e = finite ? exp_of(bound) : 0;
-    p2 = ldexp(1.0, 54 - e);
-    sc = finite ? c * ldexp(1.0, e - 54) : __builtin_nan("");
 }
 
 // ---- software pipeline shared by both applies.  A "stage" is SK = 2 MFMA K-steps (64 K

@@ -403,7 +403,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     ACE_HIP(hipMemsetAsync(w.zeros, 0, 16 * (size_t)n, st));
     {
         ProfScope ps(ACE_K_INIT, st);
-        applyA(0, X0, w.T, nullptr);                             // AX = A*X0
+        if (pc) launch_pc_apply_a(batch, m, n, L.pcodes + pc_codesA_off(batch, m, n), L.pcb, X0, w.T, st);
+        else applyA(0, X0, w.T, nullptr);                        // AX = A*X0
         launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st);
         za.it = 0;
         launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)

@@ -206,6 +206,9 @@ struct PgkArgs {
     const double* zeros;
 };
 void launch_pgk(int batch, const PgkArgs& a, hipStream_t st);
+// P0 = A X0 (init, InferADMM :296-300) from the code images (codesA = codes + pc_codesA_off)
+void launch_pc_apply_a(int batch, int m, int n, const uint32_t* codesA, const double* cb, const double* X0, double* P0,
+                       hipStream_t st);
 
 // Arguments of the Z-step kernel (ace_zprox.hip).
 struct ZArgs {

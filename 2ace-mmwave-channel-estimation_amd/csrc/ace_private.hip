@@ -32,6 +32,17 @@ namespace {
 
 constexpr int PNT = 256;   // threads of the per-realisation kernels
 
+// Phase timestamps of work-group 5 (diagnostic build only: -DACE_PHASE_STAMPS)
+#ifdef ACE_PHASE_STAMPS
+#define PSTAMP_DECL unsigned long long ts_[12] = {}
+#define PSTAMP(i) do { if (blockIdx.x == 5 && threadIdx.x == 0) ts_[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PSTAMP_PRINT(name, k) do { if (blockIdx.x == 5 && threadIdx.x == 0) { printf("%s", name); for (int i_ = 1; i_ < k; ++i_) printf(" %llu", ts_[i_] - ts_[i_ - 1]); printf("\n"); } } while (0)
+#else
+#define PSTAMP_DECL
+#define PSTAMP(i)
+#define PSTAMP_PRINT(name, k)
+#endif
+
 struct PcDims {
     int m, n, mt, mp, mp32, nb32, ntile, nctH, nksH, nkgH, nctA, nksA, nkgA, nwR;
 };
@@ -67,49 +78,24 @@ __device__ __forceinline__ int code_shift(int p, int u) { return 8 * (u & 3) + 2
 
 // ---- setup -------------------------------------------------------------------------------
 
-// c_b = max |component| of A_b (NaN if some component is not finite)
-__global__ __launch_bounds__(PNT) void pc_cmax_kernel(int m, int n, const double* __restrict__ A,
-                                                      double* __restrict__ cb) {
-    const long long cnt = 2LL * m * n;
-    const double* a = A + (long long)blockIdx.x * cnt;
-    double mx = 0.0, sn = 0.0;
-    for (long long e = threadIdx.x; e < cnt; e += PNT) {
-        const double v = fabs(a[e]);
-        mx = fmax(mx, v);
-        sn += 0.0 * v;
-    }
-    __shared__ double red[2][PNT / 64];
-    mx = wave_max(mx);
-    sn = wave_sum(sn);
-    if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = mx;
-        red[1][threadIdx.x >> 6] = sn;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a0 = 0.0, s0 = 0.0;
-        for (int w = 0; w < PNT / 64; ++w) {
-            a0 = fmax(a0, red[0][w]);
-            s0 += red[1][w];
-        }
-        cb[blockIdx.x] = a0 + s0;
-    }
-}
-
-// One work-group per (realisation, 32-row block of A_b): check and encode the rows, then emit
+// One work-group per (realisation, 32-row block of A_b): check and encode the rows (c_b = the
+// first entry's magnitude; any entry that is not exactly c_b j^k sets *flag), then emit
 // the A^H image (this block is one K-step pair), the A image (two output tiles) and the
 // row-major codes (16 per dword) used by pc_k.
 __global__ __launch_bounds__(PNT) void pc_pack_kernel(int m, int n, const double* __restrict__ A,
-                                                      const double* __restrict__ cb, uint32_t* __restrict__ cH,
+                                                      double* __restrict__ cb, uint32_t* __restrict__ cH,
                                                       uint32_t* __restrict__ cA, uint32_t* __restrict__ cR,
                                                       int* __restrict__ flag) {
     extern __shared__ unsigned char cs[];   // [32][np] code bytes (0 outside A)
     const PcDims d = pc_dims(m, n);
     const int b = blockIdx.x, rb = blockIdx.y, t = threadIdx.x;
     const int np = 16 * d.nksA;
-    const double c = cb[b];
     const d2* a = reinterpret_cast<const d2*>(A) + (long long)b * m * n;
+    // c_b from the first entry; every entry must then be exactly c_b j^k
+    const d2 a00 = a[0];
+    const double c = fmax(fabs(a00.x), fabs(a00.y));
     int bad = !(c > 0.0 && c <= 1.7e308);
+    if (rb == 0 && t == 0) cb[b] = c;
     for (int e = t; e < 32 * np; e += PNT) {
         const int il = e / np, k = e - il * np, i = 32 * rb + il;
         unsigned char code = 0;
@@ -275,15 +261,18 @@ __global__ __launch_bounds__(PNT) void gj_panel_kernel(int mp32, int k, double* 
         d2 col[32];
 #pragma unroll
         for (int c = 0; c < 32; ++c) col[c] = G[(k0 + c) * mp32 + j];
-        for (int r = 0; r < 32; ++r) {
-            double sr = 0.0, si = 0.0;
+        for (int r0 = 0; r0 < 32; r0 += 4) {   // four rows: independent FMA chains
+            double sr[4] = {0.0, 0.0, 0.0, 0.0}, si[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int c = 0; c < 32; ++c) {
-                const d2 pv = Ps[r * GJS + c];
-                sr = fma(pv.x, col[c].x, fma(-pv.y, col[c].y, sr));
-                si = fma(pv.x, col[c].y, fma(pv.y, col[c].x, si));
-            }
-            G[(k0 + r) * mp32 + j] = make_double2(sr, si);
+            for (int c = 0; c < 32; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const d2 pv = Ps[(r0 + u) * GJS + c];
+                    sr[u] = fma(pv.x, col[c].x, fma(-pv.y, col[c].y, sr[u]));
+                    si[u] = fma(pv.x, col[c].y, fma(pv.y, col[c].x, si[u]));
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) G[(k0 + r0 + u) * mp32 + j] = make_double2(sr[u], si[u]);
         }
     }
 }
@@ -305,20 +294,22 @@ __global__ __launch_bounds__(PNT) void gj_update_kernel(int mp32, int k, double*
         d2 rc[32];
 #pragma unroll
         for (int c = 0; c < 32; ++c) rc[c] = inblk ? Pm[c * GJS + (j - (int)k0)] : G[(k0 + c) * mp32 + j];
-        for (int r = 0; r < 32; ++r) {
-            double sr = 0.0, si = 0.0;
+        for (int r0 = 0; r0 < 32; r0 += 4) {   // four rows: independent FMA chains
+            d2 o[4];
 #pragma unroll
-            for (int c = 0; c < 32; ++c) {
-                const d2 cv = Cs[r * GJS + c];
-                sr = fma(cv.x, rc[c].x, fma(-cv.y, rc[c].y, sr));
-                si = fma(cv.x, rc[c].y, fma(cv.y, rc[c].x, si));
-            }
-            d2* o = &G[(i0 + r) * mp32 + j];
-            if (inblk) *o = make_double2(-sr, -si);
-            else {
-                const d2 v = *o;
-                *o = make_double2(v.x - sr, v.y - si);
-            }
+            for (int u = 0; u < 4; ++u) o[u] = inblk ? make_double2(0.0, 0.0) : G[(i0 + r0 + u) * mp32 + j];
+            double sr[4] = {0.0, 0.0, 0.0, 0.0}, si[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < 32; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const d2 cv = Cs[(r0 + u) * GJS + c];
+                    sr[u] = fma(cv.x, rc[c].x, fma(-cv.y, rc[c].y, sr[u]));
+                    si[u] = fma(cv.x, rc[c].y, fma(cv.y, rc[c].x, si[u]));
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                G[(i0 + r0 + u) * mp32 + j] = make_double2(o[u].x - sr[u], o[u].y - si[u]);
         }
     }
 }
@@ -373,6 +364,8 @@ __device__ __forceinline__ void put_digits4(int8_t* Ad, RowOff row, int i0, cons
     }
 }
 
+__device__ __forceinline__ d2 d2zero() { return make_double2(0.0, 0.0); }
+
 // owner wave of 16-row tile row I of G (snake over groups of 4 rows: balanced triangle)
 __device__ __forceinline__ int tile_owner(int I) {
     const int g = I >> 2, r = I & 3;
@@ -398,6 +391,83 @@ __host__ __device__ __forceinline__ PgkLds pgk_lds(int m, int n) {
     return L;
 }
 
+// avs[0 .. 2m) = c A v for one realisation on the int8 matrix cores (all PNT threads): the 8
+// digit planes of v (vget(k), k < n, against 2^e >= bound) in 8 LDS rows of rstA bytes (MFMA rows
+// lds_row(0, tt) = 8 (tt >> 2) + (tt & 3); the other 24 rows read as zero), the codebook operand
+// expanded from the realisation's A image cA.  Ends with the block synchronised.
+template <class VGet>
+__device__ __forceinline__ void pc_av_block(const PcDims& d, int rstA, int8_t* Ad, const uint4* __restrict__ cA,
+                                            double bound, double c, VGet vget, double* avs) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    double p2, sc;
+    plane_scale(bound, c, p2, sc);
+    for (int g4 = t; g4 < 4 * d.nksA; g4 += PNT) {
+        d2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = 4 * g4 + u;
+            v[u] = k < d.n ? vget(k) : make_double2(0.0, 0.0);
+        }
+        put_digits4(Ad, [&](int tt) { return tt * rstA; }, 4 * g4, v, p2);
+    }
+    __syncthreads();
+    const int r32 = lane & 31;
+    const bool rok = (r32 & 4) == 0 && r32 < 16;
+    const int8_t* abase = Ad + ((r32 & 3) + 4 * (r32 >> 3)) * rstA + 16 * (lane >> 5);
+    const bool im = lane & 1;   // output real: even = Re, odd = Im
+    const uint32_t lutX = im ? LUT_Q : LUT_P, lutY = im ? LUT_P : LUT_NQ;   // a v: (p x - q y, q x + p y)
+    for (int ct = w; ct < d.nctA; ct += PNT / 64) {
+        const uint4* cp = cA + (size_t)ct * d.nkgA * 32 + ((lane & 31) >> 1) * 2 + (lane >> 5);
+        i16v acc = i16v{};
+        for (int kg = 0; kg < d.nkgA; ++kg) {
+            const uint4 cw = cp[(size_t)kg * 32];
+            const uint32_t cwv[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const int ks = 8 * kg + 2 * j + p;
+                    if (ks < d.nksA) {
+                        const i4v af = rok ? *reinterpret_cast<const i4v*>(abase + 32 * ks) : i4v{0, 0, 0, 0};
+                        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, code_frag(cwv[j], p, lutX, lutY), acc, 0, 0, 0);
+                    }
+                }
+        }
+        const int col = 32 * ct + (lane & 31);
+        if (lane < 32 && col < 2 * d.m) avs[col] = sc * recombine(acc, 0);
+    }
+    __syncthreads();
+}
+
+// init (:296-300): P0 = A X0 for the private phase-code path (one work-group per realisation)
+__global__ __launch_bounds__(PNT) void pc_apply_a_kernel(int m, int n, const uint32_t* __restrict__ codesA,
+                                                         const double* __restrict__ cb, const double* __restrict__ X0,
+                                                         double* __restrict__ P0) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ double red[2][PNT / 64];
+    const PcDims d = pc_dims(m, n);
+    const int b = blockIdx.x, t = threadIdx.x;
+    const d2* x = reinterpret_cast<const d2*>(X0) + (long long)b * n;
+    VMax vm;
+    for (int k = t; k < n; k += PNT) vm.add(x[k]);
+    const double mx = wave_max(vm.m), sn = wave_sum(vm.s);
+    if ((t & 63) == 0) {
+        red[0][t >> 6] = mx;
+        red[1][t >> 6] = sn;
+    }
+    __syncthreads();
+    double bound = 0.0, sticky = 0.0;
+    for (int w = 0; w < PNT / 64; ++w) {
+        bound = fmax(bound, red[0][w]);
+        sticky += red[1][w];
+    }
+    double* avs = reinterpret_cast<double*>(smem);
+    int8_t* Ad = reinterpret_cast<int8_t*>(smem) + ((16 * d.mp + 15) & ~15);
+    pc_av_block(d, 32 * d.nksA + 16, Ad, reinterpret_cast<const uint4*>(codesA) + (size_t)b * d.nctA * d.nkgA * 32,
+                bound + sticky, cb[b], [&](int k) { return x[k]; }, avs);
+    for (int e = t; e < 2 * m; e += PNT) P0[(long long)b * 2 * m + e] = avs[e];
+}
+
 __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ double red[4][12];
@@ -405,6 +475,8 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     RealState* rs = a.rs + b;
     if (rs->done) return;
+    PSTAMP_DECL;
+    PSTAMP(0);
     const PcDims d = pc_dims(m, n);
     const PgkLds L = pgk_lds(m, n);
     d2* Ts = reinterpret_cast<d2*>(smem + L.ts);
@@ -417,8 +489,7 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
     const long long om = (long long)b * m;
     const int i = t;
     const bool iv = i < m;
-    const d2 zero = make_double2(0.0, 0.0);
-    d2 yo = zero, mi = zero;
+    d2 yo = d2zero(), mi = d2zero();
     double bi = 0.0;
     if (iv) {
         yo = reinterpret_cast<const d2*>(a.Yo)[om + i];
@@ -427,13 +498,37 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         // deferred opt_Y (RealState::optysrc): the best Y_new is in the buffer this Y-step overwrites
         if (a.yn_id && oys == a.yn_id) reinterpret_cast<d2*>(a.optY)[om + i] = reinterpret_cast<const d2*>(a.Yn)[om + i];
     }
-    for (int e = t; e < 4 * d.mp; e += PNT) cp[e] = zero;
-    if (lane == 0) {   // this wave's tile stream: owned tile rows ascending, K = 0..I
-        int f = 0;
-        for (int I = 0; I < d.mt; ++I)
-            if (tile_owner(I) == w)
-                for (int K = 0; K <= I; ++K) tl[64 * w + f++] = (uint16_t)((I << 8) | K);
-        red[w][11] = (double)f;
+    for (int e = t; e < 4 * d.mp; e += PNT) cp[e] = d2zero();
+    // this wave's stream of G tiles: owned tile rows ascending, K = 0..I
+    int ntw = 0;
+    for (int I = 0; I < d.mt; ++I)
+        if (tile_owner(I) == w) {
+            if (lane <= I) tl[64 * w + ntw + lane] = (uint16_t)((I << 8) | lane);
+            ntw += I + 1;
+        }
+    ntw = __builtin_amdgcn_readfirstlane(ntw);
+    // the first G tiles are requested now: their latency overlaps the T phase
+    const int r16 = lane & 15, q4 = lane >> 4;
+    const d2* gtb = reinterpret_cast<const d2*>(a.Gt) + (size_t)b * d.ntile * 256 + (4 * q4) * 16 + r16;
+    auto tptr = [&](int f) -> const d2* {
+        const int code = tl[64 * w + (f < ntw ? f : (ntw > 0 ? ntw - 1 : 0))];
+        const int I = code >> 8, K = code & 255;
+        return gtb + (size_t)(I * (I + 1) / 2 + K) * 256;
+    };
+    auto load = [&](d2 (&gv)[4], int f) {
+        const d2* p = tptr(f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // streamed once per iteration: non-temporal (keep L2 for the rest)
+            typedef double dv2 __attribute__((ext_vector_type(2)));
+            const dv2 v = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p + 16 * j));
+            gv[j] = make_double2(v.x, v.y);
+        }
+    };
+    d2 b0[4], b1[4], b2[4], b3[4];
+    if (ntw > 0) {   // (a wave owns no tile row when m <= 48)
+        load(b0, 0);
+        load(b1, 1);
+        load(b2, 2);
     }
 
     // ---- T = (Y - M/mu) - A V  (the expression of i8a_block / gyk_kernel)
@@ -442,82 +537,36 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
             const d2 ax = reinterpret_cast<const d2*>(a.AX)[om + i];
             Ts[i] = make_double2(fma(-mi.x, imu, yo.x) - ax.x, fma(-mi.y, imu, yo.y) - ax.y);
         } else if (i < d.mp) {
-            Ts[i] = zero;
+            Ts[i] = d2zero();
         }
     } else {
-        // digit planes of V = Z - N/mu (8 rows, row tt at tt * rstA) against the Z-step's bound
-        double p2, sc;
-        plane_scale(rs->vbound, c, p2, sc);
         const d2* zp = reinterpret_cast<const d2*>(a.Z) + (long long)b * n;
         const d2* np = rs->nzero ? reinterpret_cast<const d2*>(a.zeros) : reinterpret_cast<const d2*>(a.N) + (long long)b * n;
-        for (int g4 = t; g4 < 4 * d.nksA; g4 += PNT) {
-            d2 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int k = 4 * g4 + u;
-                v[u] = zero;
-                if (k < n) {
-                    const d2 z = zp[k], nn = np[k];
-                    v[u] = make_double2(fma(-nn.x, imu, z.x), fma(-nn.y, imu, z.y));
-                }
-            }
-            put_digits4(Ad, [&](int tt) { return tt * L.rstA; }, 4 * g4, v, p2);
-        }
-        __syncthreads();
-        // A V on the int8 matrix cores: rows = the 8 digit planes (MFMA rows lds_row(0, tt) =
-        // 8 (tt >> 2) + (tt & 3); the other 24 rows are zero), codebook operand from the A image
-        const int r32 = lane & 31;
-        const bool rok = (r32 & 4) == 0 && r32 < 16;
-        const int8_t* abase = Ad + ((r32 & 3) + 4 * (r32 >> 3)) * L.rstA + 16 * (lane >> 5);
-        const bool im = lane & 1;   // output real: even = Re, odd = Im
-        const uint32_t lutX = im ? LUT_Q : LUT_P, lutY = im ? LUT_P : LUT_NQ;   // a v: (p x - q y, q x + p y)
         double* avs = reinterpret_cast<double*>(grow);
-        for (int ct = w; ct < d.nctA; ct += 4) {
-            const uint4* cpA = reinterpret_cast<const uint4*>(a.codesA) +
-                               ((size_t)b * d.nctA + ct) * d.nkgA * 32 + ((lane & 31) >> 1) * 2 + (lane >> 5);
-            i16v acc = i16v{};
-            for (int kg = 0; kg < d.nkgA; ++kg) {
-                const uint4 cw = cpA[(size_t)kg * 32];
-                const uint32_t cwv[4] = {cw.x, cw.y, cw.z, cw.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int p = 0; p < 2; ++p) {
-                        const int ks = 8 * kg + 2 * j + p;
-                        if (ks < d.nksA) {
-                            const i4v af = rok ? *reinterpret_cast<const i4v*>(abase + 32 * ks) : i4v{0, 0, 0, 0};
-                            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, code_frag(cwv[j], p, lutX, lutY), acc, 0, 0, 0);
-                        }
-                    }
-            }
-            const int col = 32 * ct + (lane & 31);
-            if (lane < 32 && col < 2 * m) avs[col] = sc * recombine(acc, 0);
-        }
+        pc_av_block(d, L.rstA, Ad, reinterpret_cast<const uint4*>(a.codesA) + (size_t)b * d.nctA * d.nkgA * 32,
+                    rs->vbound, c, [&](int k) {
+                        const d2 z = zp[k], nn = np[k];
+                        return make_double2(fma(-nn.x, imu, z.x), fma(-nn.y, imu, z.y));
+                    }, avs);
         __syncthreads();
         if (iv) Ts[i] = make_double2(fma(-mi.x, imu, yo.x) - avs[2 * i], fma(-mi.y, imu, yo.y) - avs[2 * i + 1]);
-        else if (i < d.mp) Ts[i] = zero;
+        else if (i < d.mp) Ts[i] = d2zero();
     }
     __syncthreads();
+    PSTAMP(1);
 
     // ---- g = G T over the lower tiles: a tile (I, K) adds G_IK T_K to rows I (lane-owned row
     // sums) and, for K < I, G_IK^H T_I to rows K (reduced over the tile's 16 rows, accumulated in
     // the wave's column sums).  Each wave streams its tile rows with loads three tiles ahead.
     {
-        const int r16 = lane & 15, q = lane >> 4;
-        const int ntw = (int)red[w][11];
-        const d2* gtb = reinterpret_cast<const d2*>(a.Gt) + (size_t)b * d.ntile * 256 + (4 * q) * 16 + r16;
-        auto tptr = [&](int f) -> const d2* {
-            const int code = tl[64 * w + (f < ntw ? f : (ntw > 0 ? ntw - 1 : 0))];
-            const int I = code >> 8, K = code & 255;
-            return gtb + (size_t)(I * (I + 1) / 2 + K) * 256;
-        };
-        d2 racc = zero, trow = zero;
+        const int q = q4;
+        d2 racc = d2zero(), trow = d2zero();
         d2* cpw = cp + w * d.mp;
         auto compute = [&](const d2 (&gv)[4], int f) {
             const int code = tl[64 * w + f];
             const int I = code >> 8, K = code & 255;
             if (K == 0) {
-                racc = zero;
+                racc = d2zero();
                 trow = Ts[16 * I + r16];
             }
             d2 v[4];
@@ -558,17 +607,6 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
                 if (q == 0) grow[16 * I + r16] = racc;
             }
         };
-        auto load = [&](d2 (&gv)[4], int f) {
-            const d2* p = tptr(f);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) gv[j] = p[16 * j];
-        };
-        d2 b0[4], b1[4], b2[4], b3[4];
-        if (ntw > 0) {   // (a wave owns no tile row when m <= 48)
-        load(b0, 0);
-        load(b1, 1);
-        load(b2, 2);
-        }
         for (int f0 = 0; f0 < ntw; f0 += 4) {
             load(b3, f0 + 3);
             compute(b0, f0);
@@ -581,9 +619,22 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         }
     }
     __syncthreads();
+    PSTAMP(2);
+
+    // A^H codes of this wave's first two output tiles, requested before the Y-step
+    const uint4* cpH = reinterpret_cast<const uint4*>(a.codesH) + (size_t)b * d.nctH * d.nkgH * 32 +
+                       ((lane & 31) >> 1) * 2 + (lane >> 5);
+    auto cload = [&](uint4 (&cw)[2], int ct) {
+        const int cc = ct < d.nctH ? ct : d.nctH - 1;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) cw[kg] = kg < d.nkgH ? cpH[((size_t)cc * d.nkgH + kg) * 32] : make_uint4(0, 0, 0, 0);
+    };
+    uint4 cq0[2], cq1[2], cq2[2];
+    cload(cq0, w);
+    cload(cq1, w + 4);
 
     // ---- Y-step on entry i (gyk_kernel's arithmetic): g, ArgMinY, M update, sums
-    d2 gv = zero, y = zero, dy = zero;
+    d2 gv = d2zero(), y = d2zero(), dy = d2zero();
     double sv[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // 5 sums, 3 max |.|, 3 NaN-sticky terms
     if (iv) {
         gv = grow[i];
@@ -592,7 +643,7 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         const d2 ax = csub(csub(yo, cscale(mi, imu)), gv);
         d2 cc = cadd(ax, cscale(mi, imu));
         double dd = sqrt(cabs2(cc));
-        if (dd == 0.0) {   // ArgMinY zero guard (:516-520 / :524-528)
+        if (dd == 0.0) {   // ArgMinY d2zero() guard (:516-520 / :524-528)
             cc = make_double2(1.0, 0.0);
             dd = 1.0;
         }
@@ -622,9 +673,9 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         grow[i] = y;
         cp[i] = dy;
     } else if (i < d.mp) {
-        Ts[i] = zero;
-        grow[i] = zero;
-        cp[i] = zero;
+        Ts[i] = d2zero();
+        grow[i] = d2zero();
+        cp[i] = d2zero();
     }
 #pragma unroll
     for (int k = 0; k < 11; ++k) sv[k] = (k >= 5 && k < 8) ? wave_max(sv[k]) : wave_sum(sv[k]);
@@ -654,16 +705,19 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         if (a.yn_id) rs->optysrc = imp ? a.yn_id : (oys == a.yn_id ? 0 : oys);
     }
 
-    // ---- digit planes of g, Y_new, dY (right-hand sides 0, 1, 2; slot 3 zero) over the m inputs
+    PSTAMP(3);
+    // ---- digit planes of g, Y_new, dY (right-hand sides 0, 1, 2; slot 3 d2zero()) over the m inputs
     for (int e = t; e < 4 * 4 * d.nksH; e += PNT) {
         const int r = e / (4 * d.nksH), g4 = e - r * 4 * d.nksH;
         const d2* src = r == 0 ? Ts : (r == 1 ? grow : cp);
         d2 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = (r < 3 && 4 * g4 + u < m) ? src[4 * g4 + u] : zero;
-        put_digits4(Ad, [&](int tt) { return lds_row(r, tt) * L.rstH; }, 4 * g4, v, r < 3 ? p2v[r] : 1.0);
+        for (int u = 0; u < 4; ++u) v[u] = (r < 3 && 4 * g4 + u < m) ? src[4 * g4 + u] : d2zero();
+        const double p2r = r == 0 ? p2v[0] : (r == 1 ? p2v[1] : (r == 2 ? p2v[2] : 1.0));   // (no dynamic register index)
+        put_digits4(Ad, [&](int tt) { return lds_row(r, tt) * L.rstH; }, 4 * g4, v, p2r);
     }
     __syncthreads();
+    PSTAMP(4);
 
     // ---- W = c A^H g and the dual terms on the int8 matrix cores: rows = (right-hand side, digit),
     // codebook operand expanded from the A^H codes, one 32-column output tile per pass
@@ -674,20 +728,9 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         for (int ks = 0; ks < 16; ++ks) af[ks] = ks < d.nksH ? *reinterpret_cast<const i4v*>(arow + 32 * ks) : i4v{0, 0, 0, 0};
         const bool im = lane & 1;
         const uint32_t lutX = im ? LUT_NQ : LUT_P, lutY = im ? LUT_P : LUT_Q;   // conj(a) g: (p x + q y, p y - q x)
-        const uint4* cpH = reinterpret_cast<const uint4*>(a.codesH) + (size_t)b * d.nctH * d.nkgH * 32 +
-                           ((lane & 31) >> 1) * 2 + (lane >> 5);
         double* Wb = a.W + (long long)b * 2 * n;
         double dacc = 0.0, nacc = 0.0;
-        uint4 cn[2];
-        auto cload = [&](uint4 (&cw)[2], int ct) {
-            const int cc = ct < d.nctH ? ct : d.nctH - 1;
-#pragma unroll
-            for (int kg = 0; kg < 2; ++kg) cw[kg] = kg < d.nkgH ? cpH[((size_t)cc * d.nkgH + kg) * 32] : make_uint4(0, 0, 0, 0);
-        };
-        cload(cn, w);
-        for (int ct = w; ct < d.nctH; ct += 4) {
-            uint4 cw[2] = {cn[0], cn[1]};
-            cload(cn, ct + 4);
+        auto tile = [&](const uint4 (&cw)[2], int ct) {
             i16v acc = i16v{};
 #pragma unroll
             for (int ks = 0; ks < 16; ++ks) {
@@ -698,17 +741,22 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
                     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[ks], code_frag(dw, ks & 1, lutX, lutY), acc, 0, 0, 0);
                 }
             }
+            // lanes 0..31: slots 0 (g) and 2 (dY); lanes 32..63: slot 1 (Y_new).  Straight-line, so
+            // that the compiler keeps both accumulators in registers (no lane-indexed selection)
             const int col = 32 * ct + (lane & 31);
-            if (col < 2 * n) {
-                if (lane < 32) {   // slots 0 (g) and 2 (dY)
-                    Wb[col] = scv[0] * recombine(acc, 0);
-                    const double dv = scv[2] * recombine(acc, 1);
-                    dacc += dv * dv;
-                } else {           // slot 1 (Y_new)
-                    const double yv = scv[1] * recombine(acc, 0);
-                    nacc += yv * yv;
-                }
-            }
+            const bool lo = lane < 32, in = col < 2 * n;
+            const double v0 = (lo ? scv[0] : scv[1]) * recombine(acc, 0), v1 = scv[2] * recombine(acc, 1);
+            if (lo && in) Wb[col] = v0;
+            dacc += (lo && in) ? v1 * v1 : 0.0;
+            nacc += (!lo && in) ? v0 * v0 : 0.0;
+        };
+        for (int ct = w; ct < d.nctH; ct += 12) {   // codes three column tiles ahead
+            cload(cq2, ct + 8);
+            tile(cq0, ct);
+            cload(cq0, ct + 12);
+            if (ct + 4 < d.nctH) tile(cq1, ct + 4);
+            cload(cq1, ct + 16);
+            if (ct + 8 < d.nctH) tile(cq2, ct + 8);
         }
         dacc = wave_sum(dacc);
         nacc = wave_sum(nacc);
@@ -727,6 +775,8 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
         rs->dAtY = dv;   // ||A^H (Y - Y0)||^2
         rs->nAtY = nv;   // ||A^H Y||^2
     }
+    PSTAMP(5);
+    PSTAMP_PRINT("pgk A|B|Ystep|digits|AH:", 6);
 }
 
 }  // namespace
@@ -746,7 +796,6 @@ void launch_pc_pack(int batch, int m, int n, const double* A, double* cb, uint32
     uint32_t* cH = codes;
     uint32_t* cA = cH + (size_t)batch * d.nctH * d.nkgH * 128;
     uint32_t* cR = cA + (size_t)batch * d.nctA * d.nkgA * 128;
-    hipLaunchKernelGGL(pc_cmax_kernel, dim3(batch), dim3(PNT), 0, st, m, n, A, cb);
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_pack_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
@@ -767,6 +816,18 @@ void launch_pc_ginv(int batch, int m, int n, const uint32_t* codes, const double
         if (d.nb32 > 1) hipLaunchKernelGGL(gj_update_kernel, dim3(batch, d.nb32 - 1), dim3(PNT), 0, st, d.mp32, k, Gw);
     }
     hipLaunchKernelGGL(pc_tiles_kernel, dim3(batch, d.ntile), dim3(PNT), 0, st, m, Gw, Gt);
+}
+
+void launch_pc_apply_a(int batch, int m, int n, const uint32_t* codesA, const double* cb, const double* X0, double* P0,
+                       hipStream_t st) {
+    const PcDims d = pc_dims(m, n);
+    const size_t lds = ((16 * (size_t)d.mp + 15) & ~(size_t)15) + 8 * (size_t)(32 * d.nksA + 16);
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_apply_a_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(pc_apply_a_kernel, dim3(batch), dim3(PNT), lds, st, m, n, codesA, cb, X0, P0);
 }
 
 void launch_pgk(int batch, const PgkArgs& a, hipStream_t st) {

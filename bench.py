@@ -305,9 +305,27 @@ def unit_bytes(m, n, tx, rx):
     }
 
 
+def private_bytes(m, n):
+    """Algorithmic HBM bytes per realisation per iteration of pgk_kernel (private phase-code
+    codebooks, ace_private.hip) in the steady state (A V = AX):
+      G_b = (I + A_b A_b^H)^{-1}: its Hermitian lower triangle, m (m + 1) / 2 complex128
+      A_b^H: 2-bit codes, m n / 4 bytes
+      read Y, M, AX (c128) and B (f64); write AX, M, Y_new; write W = A^H g (n c128)"""
+    return 16.0 * m * (m + 1) / 2 + m * n / 4.0 + 16.0 * 6 * m + 8.0 * m + 16.0 * n
+
+
+def private_ops(m, n):
+    """pgk_kernel's matrix-core and vector work per realisation per iteration: int8 ops of the three
+    digit-plane right-hand sides (g, Y, Y - Y0; 8 digits each) times the 2x2 real expansion of A^H,
+    and f64 flops of g = G T (8 per complex MAC over the full Hermitian G)."""
+    return {"int8": 2.0 * 3 * 8 * (2 * n) * (2 * m), "f64": 8.0 * m * m}
+
+
 def cpu_baseline(args, n_samples):
     """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
-    timed on the host cores on a bounded sample of the same workload."""
+    timed on the host cores on a bounded sample of the same workload.  Shared codebook: one
+    U = inv(A'A + I) amortised over a GPU-sized batch, as on the GPU.  Private codebooks: one U
+    per realisation, inside the timed sample (as on the GPU, whose setup is in the timed step)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import ace_oracle_c as OC
     from ace_amd import synth
@@ -315,48 +333,60 @@ def cpu_baseline(args, n_samples):
     n = tx * tx
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
     A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not args.private)
-    t0 = time.perf_counter()
-    U = OC.make_U(A[0], nthreads=cores)
-    t_setup = time.perf_counter() - t0
     var = 0 if args.variant == "A2only" else 1
     t0 = time.perf_counter()
-    OC.infer_admm_r1_batch(A[:1], U[None], B, X0, tx, tx, variant=var, fixed_iters=True, maxiter=args.iters,
-                           nthreads=cores)
+    if args.private:
+        U = np.stack([OC.make_U(a, nthreads=cores) for a in A])
+    else:
+        U = OC.make_U(A[0], nthreads=cores)[None]
+    t_setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    OC.infer_admm_r1_batch(A if args.private else A[:1], U, B, X0, tx, tx, variant=var, fixed_iters=True,
+                           maxiter=args.iters, nthreads=cores)
     t_solve = time.perf_counter() - t0
-    # setup amortised over a full GPU-sized batch, as on the GPU
-    t_total = t_solve + t_setup * n_samples / args.batch
+    if args.private:
+        t_total = t_solve + t_setup
+        setup_note = f"U=inv(A'A+I) per realisation {t_setup:.2f}s"
+    else:
+        t_total = t_solve + t_setup * n_samples / args.batch
+        setup_note = f"U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}"
     return {"value": n_samples / t_total, "unit": "recoveries/s", "cores": cores, "kind": "port",
             "sample": (f"{n_samples} recoveries of the same workload ({args.iters} fixed iters, m={args.m}, "
-                       f"n={n}, shared codebook) on {cores} threads of "
-                       f"{_cpu_model()}; U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}; "
-                       f"solve {t_solve:.2f}s")}
+                       f"n={n}, {'private' if args.private else 'shared'} codebook) on {cores} threads of "
+                       f"{_cpu_model()}; {setup_note}; solve {t_solve:.2f}s")}
 
 
 PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false>",
               "apply_G": "gyk_kernel"}
 
 
-def _pmc_traffic(cls):
+PMC_KERNEL_PRIVATE = {"zstep": "zstep1w_kernel<false>", "apply_G": "pgk_kernel"}
+
+
+def _pmc_traffic(cls, private=False):
     """HBM bytes per launch (PMC FETCH_SIZE, gfx950-corrected, + WRITE_SIZE) of a kernel class from
-    the newest committed profiles/*_pmc_hbm.json (written by tools/pmc_summary.py from separate
-    rocprofv3 --pmc passes of this benchmark), or None."""
-    name = PMC_KERNEL.get(cls)
+    the newest committed profiles/*_pmc_hbm.json that has it (written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc passes of this benchmark; private-codebook profiles are named
+    *_private_pmc_hbm.json), or None."""
+    name = (PMC_KERNEL_PRIVATE if private else PMC_KERNEL).get(cls)
     def version(f):   # r<round>_v<version>_pmc_hbm.json
         parts = f.name.split("_")
         try:
             return int(parts[0][1:]), int(parts[1][1:])
         except (IndexError, ValueError):
             return -1, -1
-    files = sorted((ROOT / "profiles").glob("r*_pmc_hbm.json"), key=version)
-    if not name or not files:
+    files = sorted((f for f in (ROOT / "profiles").glob("r*_pmc_hbm.json") if ("_private_" in f.name) == private),
+                   key=version)
+    if not name:
         return None
-    try:
-        d = json.loads(files[-1].read_text())
-    except (OSError, ValueError):
-        return None
-    for k, v in d.items():
-        if k.split(" grid=")[0].strip().startswith(name):
-            return round(v["hbm_bytes"]), f"profiles/{files[-1].name}"
+    for f in reversed(files):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.split(" grid=")[0].strip().startswith(name):
+                return round(v["hbm_bytes"]), f"profiles/{f.name}"
     return None
 
 
@@ -468,9 +498,26 @@ def main():
             per_launch = -(-bsz // nsplit)
 
             gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
+            # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
+            pc = args.private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
 
             def roofline(k):
                 avg_s = kernels[k]["avg_ms"] * 1e-3
+                if k == "apply_G" and pc:
+                    b, po = private_bytes(m, n) * per_launch, private_ops(m, n)
+                    o, f = po["int8"] * per_launch, po["f64"] * per_launch
+                    return {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                            "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                            "kernel": k, "bytes_per_launch": b,
+                            "other_resources": {
+                                "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
+                                         "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
+                                         "ops_per_launch": o},
+                                "f64": {"bound": "valu", "achieved": round(f / avg_s / 1e12, 3),
+                                        "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                                        "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "flops_per_launch": f}},
+                            "bytes_note": "per realisation: G_b lower triangle (c128) + A_b^H as 2-bit codes + "
+                                          "Y, M, AX, B in and AX, M, Y out + W = A^H g out (bench.private_bytes)"}
                 if k == "apply_G" and gyk:   # f64 G T + int8 K Y + the Y-step's HBM traffic, phase after phase
                     f, o, b = uf[k] * per_launch, io[k] * per_launch, ub[k] * per_launch
                     tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
@@ -521,6 +568,8 @@ def main():
                         "kernel": k, "bytes_per_launch": per}
 
             timed = [k for k in kernels if k in uf or k in ub]
+            if pc:   # pgk_kernel and the Z-step are the only iteration launches
+                timed = [k for k in kernels if k in ("apply_G", "zstep")]
             # every timed class launches once per iteration: dominant = largest average launch
             dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
             roof = roofline(dom)
@@ -532,16 +581,17 @@ def main():
             roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
                             f"region, on every {PROF_STRIDE}th launch of each kernel class); peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); "
                             "traffic: PMC FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source")
-            tr = _pmc_traffic(dom)
+            tr = _pmc_traffic(dom, private=pc)
             if tr:
                 roof["traffic"], roof["traffic_source"] = tr
-            gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
-            roof_gemm = roofline(gemm)
-            roof_gemm["concurrent_launches"] = nsplit
-            roof_gemm["chip_frac"] = round(roof_gemm["frac"] * nsplit, 4)
+            if not pc:
+                gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
+                roof_gemm = roofline(gemm)
+                roof_gemm["concurrent_launches"] = nsplit
+                roof_gemm["chip_frac"] = round(roof_gemm["frac"] * nsplit, 4)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            ns = args.cpu_recoveries or 256
+            ns = args.cpu_recoveries or (32 if args.private else 256)
             cpu = cpu_baseline(args, ns)
         line = {
             "metric": METRIC,

@@ -34,6 +34,16 @@ def test_int8_ops_and_flops():
     assert uf["apply_G"] == 8 * 256 * 256              # g = G T, 8 flops per complex MAC
 
 
+def test_private_bytes_and_ops():
+    b = _bench()
+    m, n = 256, 1024
+    # G_b lower triangle (c128) + A^H codes (2 bits) + Y, M, AX (c128) and B (f64) in, AX, M, Y out + W out
+    assert b.private_bytes(m, n) == 16 * m * (m + 1) // 2 + m * n // 4 + 16 * 6 * m + 8 * m + 16 * n
+    po = b.private_ops(m, n)
+    assert po["int8"] == 2 * 3 * 8 * (2 * n) * (2 * m)   # three digit-plane right-hand sides (g, Y, Y - Y0)
+    assert po["f64"] == 8 * m * m
+
+
 def test_metric_is_baselines():
     import json
     b = _bench()

@@ -26,6 +26,9 @@
 //   W = A^H g, |A^H Y|^2, |A^H (Y - Y0)|^2   one int8 GEMM with three digit-plane right-hand sides
 #include "ace_i8.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace ace {
 
 namespace {
@@ -310,6 +313,78 @@ __global__ __launch_bounds__(PNT) void gj_update_kernel(int mp32, int k, double*
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 G[(i0 + r0 + u) * mp32 + j] = make_double2(o[u].x - sr[u], o[u].y - si[u]);
+        }
+    }
+}
+
+// ---- recursive block inversion of the HPD I + K (Schur complements; the default since r02).
+// For H = [[A, B^H], [B, D]] (A: h x h, D: r x r):
+//   F = B A^{-1},  S = D - F B^H,  T = F^H S^{-1},
+//   H^{-1} = [[A^{-1} + T F, -T], [-T^H, S^{-1}]]
+// with A^{-1} and S^{-1} by recursion down to 32 x 32 blocks (inv32_kernel, Gauss-Jordan in LDS).
+// Every product is one batched launch of the complex 3M GEMM (ace_gemm.hip) over the batch's
+// matrices: 2/3 m^3 complex MACs per matrix against m^3 for the full Gauss-Jordan, on the matrix
+// cores instead of LDS-broadcast FMAs.  S is HPD whenever H is, so no pivoting is needed.
+
+// in-place inverse of one HPD 32 x 32 block per realisation (Gauss-Jordan without pivoting)
+__global__ __launch_bounds__(PNT) void inv32_kernel(int ld, long long stride, double* __restrict__ H) {
+    __shared__ d2 Ps[32 * GJS];
+    __shared__ d2 rowb[32], colb[32];
+    const int t = threadIdx.x;
+    d2* G = reinterpret_cast<d2*>(H) + (size_t)blockIdx.x * stride;
+    for (int e = t; e < 1024; e += PNT) Ps[(e >> 5) * GJS + (e & 31)] = G[(size_t)(e >> 5) * ld + (e & 31)];
+    __syncthreads();
+    for (int p = 0; p < 32; ++p) {
+        if (t < 32) {
+            const d2 pv = Ps[p * GJS + p];
+            const double den = pv.x * pv.x + pv.y * pv.y;
+            const d2 pinv = make_double2(pv.x / den, -pv.y / den);
+            const d2 a = (t == p) ? make_double2(1.0, 0.0) : Ps[p * GJS + t];
+            rowb[t] = cmul(a, pinv);
+            colb[t] = Ps[t * GJS + p];
+        }
+        __syncthreads();
+        for (int e = t; e < 1024; e += PNT) {
+            const int r = e >> 5, c = e & 31;
+            if (r == p) {
+                Ps[r * GJS + c] = rowb[c];
+            } else {
+                const d2 base = (c == p) ? make_double2(0.0, 0.0) : Ps[r * GJS + c];
+                Ps[r * GJS + c] = csub(base, cmul(colb[r], rowb[c]));
+            }
+        }
+        __syncthreads();
+    }
+    for (int e = t; e < 1024; e += PNT) G[(size_t)(e >> 5) * ld + (e & 31)] = Ps[(e >> 5) * GJS + (e & 31)];
+}
+
+// F (rows x cols, ld cols) -> Fh = F^H (cols x rows, ld rows)                       (neg = false)
+// T (rows x cols, ld cols) -> Up = -T (ldu), Lo = -T^H (ldl)                         (neg = true)
+template <bool NEG>
+__global__ __launch_bounds__(PNT) void ctrans_kernel(int rows, int cols, const double* __restrict__ src,
+                                                     long long sstride, double* __restrict__ up, int ldu,
+                                                     double* __restrict__ lo, int ldl, long long dstride) {
+    __shared__ d2 tile[32][33];
+    const int b = blockIdx.z, tr = blockIdx.y, tc = blockIdx.x, t = threadIdx.x;
+    const d2* s = reinterpret_cast<const d2*>(src) + (size_t)b * sstride;
+    d2* u = reinterpret_cast<d2*>(up) + (size_t)b * dstride;
+    d2* l = reinterpret_cast<d2*>(lo) + (size_t)b * dstride;
+    for (int e = t; e < 1024; e += PNT) {
+        const int r = e >> 5, c = e & 31, i = 32 * tr + r, j = 32 * tc + c;
+        d2 v = make_double2(0.0, 0.0);
+        if (i < rows && j < cols) v = s[(size_t)i * cols + j];
+        if (NEG) {
+            v = make_double2(-v.x, -v.y);
+            if (i < rows && j < cols) u[(size_t)i * ldu + j] = v;
+        }
+        tile[r][c] = v;
+    }
+    __syncthreads();
+    for (int e = t; e < 1024; e += PNT) {
+        const int r = e >> 5, c = e & 31, j = 32 * tc + r, i = 32 * tr + c;   // out (j, i) = conj(in (i, j))
+        if (i < rows && j < cols) {
+            const d2 v = tile[c][r];
+            l[(size_t)j * ldl + i] = make_double2(v.x, -v.y);
         }
     }
 }
@@ -786,7 +861,17 @@ size_t pc_codes_bytes(int m, int n) {   // per realisation: A^H image, A image, 
     const PcDims d = pc_dims(m, n);
     return (size_t)d.nctH * d.nkgH * 512 + (size_t)d.nctA * d.nkgA * 512 + (size_t)m * d.nwR * 4;
 }
-size_t pc_gw_bytes(int m) { const PcDims d = pc_dims(m, 16); return (size_t)d.mp32 * d.mp32 * 16; }
+// scratch (complex elements) of pc_inv_rec for an s x s block: F, F^H, T of this level + the deeper one
+static long long pc_inv_scratch(int s) {
+    if (s <= 32) return 0;
+    const int h = 32 * ((s / 32) / 2), r = s - h;
+    return 3LL * r * h + std::max(pc_inv_scratch(h), pc_inv_scratch(r));
+}
+// the matrix (mp32 x mp32) and the recursion's scratch
+size_t pc_gw_bytes(int m) {
+    const PcDims d = pc_dims(m, 16);
+    return 16 * ((size_t)d.mp32 * d.mp32 + (size_t)pc_inv_scratch(d.mp32));
+}
 size_t pc_gt_bytes(int m) { const PcDims d = pc_dims(m, 16); return (size_t)d.ntile * 256 * 16; }
 size_t pc_codesA_off(int batch, int m, int n) { const PcDims d = pc_dims(m, n); return (size_t)batch * d.nctH * d.nkgH * 128; }
 bool pc_supported(int m, int n) { return m >= 1 && m <= PC_MAXM && n >= 1 && n <= PC_MAXN && pgk_lds(m, n).total <= 64 * 1024; }
@@ -805,17 +890,79 @@ void launch_pc_pack(int batch, int m, int n, const double* A, double* cb, uint32
                        cA, cR, flag);
 }
 
+// H^{-1} in place for the s x s Hermitian block at H (leading dimension ld, realisation stride hs,
+// complex elements) of nb realisations; scr: scratch with realisation stride ss (complex)
+static void pc_inv_rec(int nb, int s, double* H, int ld, long long hs, double* scr, long long ss, hipStream_t st) {
+    if (s <= 32) {
+        hipLaunchKernelGGL(inv32_kernel, dim3(nb), dim3(PNT), 0, st, ld, hs, H);
+        return;
+    }
+    const int h = 32 * ((s / 32) / 2), r = s - h;
+    double* A = H;
+    double* B = H + 2 * (size_t)h * ld;       // rows h.., columns 0..h
+    double* D = B + 2 * (size_t)h;            // rows h.., columns h..
+    double* Up = H + 2 * (size_t)h;           // rows 0..h, columns h..
+    double* F = scr;                          // r x h
+    double* Fh = F + 2 * (size_t)r * h;       // h x r
+    double* T = Fh + 2 * (size_t)h * r;       // h x r
+    double* next = T + 2 * (size_t)h * r;
+    pc_inv_rec(nb, h, A, ld, hs, next, ss, st);
+    // F = B A^{-1} = B (A^{-1})^H                                 (C = V L^H with V = B, L = A^{-1})
+    launch_zgemm(0, true, h, h, r, A, ld, hs, B, ld, hs, F, nullptr, h, ss, nb, st);
+    hipLaunchKernelGGL(ctrans_kernel<false>, dim3((h + 31) / 32, (r + 31) / 32, nb), dim3(PNT), 0, st, r, h, F, ss,
+                       nullptr, 0, Fh, r, ss);
+    // S = D - F B^H (in place)
+    launch_zgemm(1, true, r, h, r, B, ld, hs, F, h, ss, D, D, ld, hs, nb, st);
+    pc_inv_rec(nb, r, D, ld, hs, next, ss, st);
+    // T = F^H S^{-1}; A^{-1} + T F = A^{-1} + T (F^H)^H; off-diagonal blocks -T, -T^H
+    launch_zgemm(0, true, r, r, h, D, ld, hs, Fh, r, ss, T, nullptr, r, ss, nb, st);
+    launch_zgemm(2, true, h, r, h, Fh, r, ss, T, r, ss, A, A, ld, hs, nb, st);
+    hipLaunchKernelGGL(ctrans_kernel<true>, dim3((r + 31) / 32, (h + 31) / 32, nb), dim3(PNT), 0, st, h, r, T, ss,
+                       Up, ld, B, ld, hs);
+}
+
+static bool pc_use_gj() {   // ACE_PC_GJ=1: the blocked Gauss-Jordan of r01 (A/B comparisons)
+    static const bool v = [] {
+        const char* e = getenv("ACE_PC_GJ");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 void launch_pc_ginv(int batch, int m, int n, const uint32_t* codes, const double* cb, double* Gw, double* Gt,
                     hipStream_t st) {
+    if (!pc_use_gj()) {
+        const PcDims d = pc_dims(m, n);
+        const uint32_t* cR = codes + (size_t)batch * d.nctH * d.nkgH * 128 + (size_t)batch * d.nctA * d.nkgA * 128;
+        const long long s2 = (long long)d.mp32 * d.mp32;   // complex elements per matrix
+        // matrices [batch][mp32][mp32], then the scratch [batch][pc_inv_scratch]
+        double* scr = Gw + 2 * s2 * batch;
+        const long long ss = std::max(1LL, pc_inv_scratch(d.mp32));
+        hipLaunchKernelGGL(pc_k_kernel, dim3(batch, d.nb32 * (d.nb32 + 1) / 2), dim3(PNT), (size_t)64 * (d.nwR + 1) * 4,
+                           st, m, n, cR, cb, Gw);
+        pc_inv_rec(batch, d.mp32, Gw, d.mp32, s2, scr, ss, st);
+        hipLaunchKernelGGL(pc_tiles_kernel, dim3(batch, d.ntile), dim3(PNT), 0, st, m, Gw, Gt);
+        return;
+    }
     const PcDims d = pc_dims(m, n);
     const uint32_t* cR = codes + (size_t)batch * d.nctH * d.nkgH * 128 + (size_t)batch * d.nctA * d.nkgA * 128;
-    hipLaunchKernelGGL(pc_k_kernel, dim3(batch, d.nb32 * (d.nb32 + 1) / 2), dim3(PNT), (size_t)64 * (d.nwR + 1) * 4, st,
-                       m, n, cR, cb, Gw);
-    for (int k = 0; k < d.nb32; ++k) {
-        hipLaunchKernelGGL(gj_panel_kernel, dim3(batch), dim3(PNT), 0, st, d.mp32, k, Gw);
-        if (d.nb32 > 1) hipLaunchKernelGGL(gj_update_kernel, dim3(batch, d.nb32 - 1), dim3(PNT), 0, st, d.mp32, k, Gw);
+    static const int chunk_env = [] {
+        const char* e = getenv("ACE_PC_CHUNK");
+        return e ? atoi(e) : 0;
+    }();
+    const int chunk = chunk_env > 0 ? chunk_env : batch;
+    const size_t gws = (size_t)2 * d.mp32 * d.mp32, gts = (size_t)d.ntile * 512;
+    for (int b0 = 0; b0 < batch; b0 += chunk) {
+        const int nb = std::min(chunk, batch - b0);
+        double* Gwc = Gw + gws * b0;
+        hipLaunchKernelGGL(pc_k_kernel, dim3(nb, d.nb32 * (d.nb32 + 1) / 2), dim3(PNT), (size_t)64 * (d.nwR + 1) * 4,
+                           st, m, n, cR + (size_t)b0 * m * d.nwR, cb + b0, Gwc);
+        for (int k = 0; k < d.nb32; ++k) {
+            hipLaunchKernelGGL(gj_panel_kernel, dim3(nb), dim3(PNT), 0, st, d.mp32, k, Gwc);
+            if (d.nb32 > 1) hipLaunchKernelGGL(gj_update_kernel, dim3(nb, d.nb32 - 1), dim3(PNT), 0, st, d.mp32, k, Gwc);
+        }
+        hipLaunchKernelGGL(pc_tiles_kernel, dim3(nb, d.ntile), dim3(PNT), 0, st, m, Gwc, Gt + gts * b0);
     }
-    hipLaunchKernelGGL(pc_tiles_kernel, dim3(batch, d.ntile), dim3(PNT), 0, st, m, Gw, Gt);
 }
 
 void launch_pc_apply_a(int batch, int m, int n, const uint32_t* codesA, const double* cb, const double* X0, double* P0,

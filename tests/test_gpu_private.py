@@ -48,7 +48,7 @@ def _launches(fn):
     return dict(zip(KERNEL_CLASSES, kn))
 
 
-@pytest.mark.parametrize("tx,m", [(16, 64), (16, 20), (16, 48), (32, 256)])
+@pytest.mark.parametrize("tx,m", [(16, 64), (16, 20), (16, 48), (16, 160), (32, 256)])
 @pytest.mark.parametrize("fixed", [True, False])
 def test_private_phase_code_matches_oracle(gpu, tx, m, fixed):
     from ace_amd import infer_admm_host

@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--seed", type=int, default=58659179)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-regime-p", action="store_true", help="unit mode: skip the regime-P measurement")
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
     ap.add_argument("--mode", default="unit", choices=["unit", "pipeline", "phaselift", "beamformer"])
@@ -321,7 +322,7 @@ def private_ops(m, n):
     return {"int8": 2.0 * 3 * 8 * (2 * n) * (2 * m), "f64": 8.0 * m * m}
 
 
-def cpu_baseline(args, n_samples):
+def cpu_baseline(args, n_samples, private):
     """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
     timed on the host cores on a bounded sample of the same workload.  Shared codebook: one
     U = inv(A'A + I) amortised over a GPU-sized batch, as on the GPU.  Private codebooks: one U
@@ -332,19 +333,19 @@ def cpu_baseline(args, n_samples):
     tx = args.tx
     n = tx * tx
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not args.private)
+    A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not private)
     var = 0 if args.variant == "A2only" else 1
     t0 = time.perf_counter()
-    if args.private:
+    if private:
         U = np.stack([OC.make_U(a, nthreads=cores) for a in A])
     else:
         U = OC.make_U(A[0], nthreads=cores)[None]
     t_setup = time.perf_counter() - t0
     t0 = time.perf_counter()
-    OC.infer_admm_r1_batch(A if args.private else A[:1], U, B, X0, tx, tx, variant=var, fixed_iters=True,
+    OC.infer_admm_r1_batch(A if private else A[:1], U, B, X0, tx, tx, variant=var, fixed_iters=True,
                            maxiter=args.iters, nthreads=cores)
     t_solve = time.perf_counter() - t0
-    if args.private:
+    if private:
         t_total = t_solve + t_setup
         setup_note = f"U=inv(A'A+I) per realisation {t_setup:.2f}s"
     else:
@@ -352,7 +353,7 @@ def cpu_baseline(args, n_samples):
         setup_note = f"U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}"
     return {"value": n_samples / t_total, "unit": "recoveries/s", "cores": cores, "kind": "port",
             "sample": (f"{n_samples} recoveries of the same workload ({args.iters} fixed iters, m={args.m}, "
-                       f"n={n}, {'private' if args.private else 'shared'} codebook) on {cores} threads of "
+                       f"n={n}, {'private' if private else 'shared'} codebook) on {cores} threads of "
                        f"{_cpu_model()}; {setup_note}; solve {t_solve:.2f}s")}
 
 
@@ -423,6 +424,26 @@ def main():
             dist.destroy_process_group()
         return
 
+    line = unit_bench(args, args.private, dev, rank, world)
+    if not args.private and not args.no_regime_p and args.variant == "A2only":
+        # both codebook regimes, each against its own bound; the headline value is
+        # regime S (one codebook for the batch, as in Vs_M.m:192-194 and main.py's one cb_train per call)
+        lp = unit_bench(args, True, dev, rank, world)
+        if rank == 0:
+            line["regime_P"] = {k: lp[k] for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline",
+                                                   "kernels_ms", "checks")}
+            line["regime_P"]["codebook"] = lp["config"]["codebook"]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def unit_bench(args, private, dev, rank, world):
+    """One unit-metric measurement (regime S or P); returns the JSON line dict on rank 0."""
+    import torch
+    import torch.distributed as dist
     import ace_amd
     from ace_amd import infer_admm_batch, synth_problem
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
@@ -430,7 +451,7 @@ def main():
 
     tx = args.tx
     n, m, bsz = tx * tx, args.m, args.batch
-    A, B, X0, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, a_shared=not args.private, device=dev)
+    A, B, X0, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, a_shared=not private, device=dev)
     ws = ace_amd.solver.Workspace()
     out = None
     from ace_amd.dist import gather_to_root
@@ -486,7 +507,7 @@ def main():
                     kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
 
             # the int8 digit-plane applies run for a phase-code codebook in the A2only r = 1 iteration
-            i8 = (not args.private) and os.environ.get("ACE_NO_I8") != "1"
+            i8 = (not private) and os.environ.get("ACE_NO_I8") != "1"
             io = unit_i8_ops(m, n)
             # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
             # every launch of an iteration kernel covers bsz / nsplit realisations
@@ -499,7 +520,7 @@ def main():
 
             gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
             # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
-            pc = args.private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
+            pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
 
             def roofline(k):
                 avg_s = kernels[k]["avg_ms"] * 1e-3
@@ -591,8 +612,8 @@ def main():
                 roof_gemm["chip_frac"] = round(roof_gemm["frac"] * nsplit, 4)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            ns = args.cpu_recoveries or (32 if args.private else 256)
-            cpu = cpu_baseline(args, ns)
+            ns = args.cpu_recoveries or (32 if private else 256)
+            cpu = cpu_baseline(args, ns, private)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -611,7 +632,7 @@ def main():
                              "refinement solve (r=1), 200 fixed iterations" if args.variant == "A2only" and tx == 32
                              else f"{args.variant}, tx=rx={tx}, m={m}, {args.iters} fixed iterations"),
                 "variant": args.variant,
-                "codebook": "private per realisation (regime P)" if args.private else "shared (regime S)",
+                "codebook": "private per realisation (regime P)" if private else "shared (regime S)",
                 "batch_per_gpu": bsz,
                 "global_batch": world * bsz,
                 "m": m, "n": n, "iters": args.iters,
@@ -623,10 +644,9 @@ def main():
             "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "checks": {"all_iters_ran": it_ok, "finite": finite},
         }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        return line
+    return None
+
 
 
 if __name__ == "__main__":

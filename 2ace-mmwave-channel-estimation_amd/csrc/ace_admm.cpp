@@ -57,6 +57,12 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->allow_i8 = true;
 }
 
+// ACE_LAZY_DUAL=0 keeps K Y in gyk_kernel every iteration (A/B comparisons); read per solve.
+static bool lazy_dual_enabled() {
+    const char* e = getenv("ACE_LAZY_DUAL");
+    return !(e && e[0] == '0');
+}
+
 // ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
 static bool i8_disabled() {
     static const bool v = [] {
@@ -270,6 +276,9 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     auto stagger_mark = [&](int h, int it, int k) -> hipError_t {
         return (evs && h == 0 && it == 1 && k == stg) ? hipEventRecord(evs, ss[0]) : hipSuccess;
     };
+    // steady-state Z-steps under the perturbation certificate (zlean_kernel), A2only only
+    const bool lean = p.variant != ACE_VARIANT_NUCLEAR && za0.warm && za0.Q && zlean_enabled();
+    const DualCtl dc{za0.tol_abs, za0.tol_rel, za0.rho, za0.fixed_iters, n, 1, w.done};
     int q = 0, rc = ACE_OK;
     for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
         for (int h = 0; h < nsplit; ++h) {
@@ -284,7 +293,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n};
+                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc};
                 launch_gyk(nb[h], m, ga, sh);
             }
             ACE_HIP(stagger_mark(h, it, 2));
@@ -308,9 +317,14 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.optX = wh.optX;
             za.optY = wh.optY;
             za.Xcur = wh.V;
+            za.Ynew = wh.Y[1 - q];   // (dual_fixup)
+            za.Yold = wh.Y[q];
+            za.fixup_now = it == p.maxiter;
             za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
+            za.lean = lean;
             {
                 ProfScope ps(ACE_K_ZSTEP, sh);
+                if (lean) launch_zlean(za, nb[h], sh);
                 launch_zstep(p.variant, false, za, nb[h], sh);
             }
         }
@@ -397,6 +411,10 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.Nn = nullptr;
     za.zeros = w.zeros;
     za.nuclear = p.variant == ACE_VARIANT_NUCLEAR;
+    // the fused g / Y-step kernel skips K Y; the Z-step forms the dual terms when the convergence
+    // test needs them (RealState::dpend), from the shared f64 K
+    za.lazy_dual = (gyk && lazy_dual_enabled()) ? 1 : 0;
+    za.Kf = L.K;
 
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
@@ -441,7 +459,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         } else if (gyk) {
             ProfScope ps(ACE_K_APPLY_G, st);
             const GykArgs ga{L.Gf, w.T, B, w.Y[q], w.M, w.Y[1 - q], w.g, w.KY[q], w.KY[1 - q], w.optY, L.LK8, L.c8, w.st,
-                             w.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n};
+                             w.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za.lazy_dual,
+                             DualCtl{za.tol_abs, za.tol_rel, za.rho, za.fixed_iters, n, 1, w.done}};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st);
@@ -481,7 +500,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.Yold = w.Y[q];
         za.KYnew = w.KY[1 - q];
         za.KYold = w.KY[q];
-        { ProfScope ps(ACE_K_ZSTEP, st); launch_zstep(p.variant, false, za, batch, st); }
+        za.lean = wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled();
+        za.fixup_now = it == p.maxiter;
+        {
+            ProfScope ps(ACE_K_ZSTEP, st);
+            if (za.lean) launch_zlean(za, batch, st);
+            launch_zstep(p.variant, false, za, batch, st);
+        }
         q = 1 - q;
         if (wmode) {
             std::swap(Zc, Zo);

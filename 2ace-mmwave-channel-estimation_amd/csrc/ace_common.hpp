@@ -44,8 +44,58 @@ struct RealState {
     // where opt_Y lives (gyk_kernel, like optsrc for opt_X): 0 the opt_Y buffer; 1 / 2 the Y[0] /
     // Y[1] ping-pong buffer holding the best Y_new, copied only before that buffer is overwritten
     int32_t optysrc;
+    // Perturbation certificate of the lean Z-step (ace_zprox1w.hip::zlean_kernel).  When the
+    // one-wave Z-step's Ky Fan certificate passes with Z' = E (N' = 0), it records for every
+    // rank-profile entry p kf[p] = sqrt(sum of the r_p largest row norms^2 of Qprev^H E_ref), a
+    // norm of a fixed r_p-row projection of E_ref.  kfcum accumulates ||E_i - E_{i-1}|| over the
+    // later iterations, so kf[p] - kfcum bounds that projection of the current E from below
+    // (triangle inequality), and by Ky Fan the top-r_p eigenvalue sum of E E^H.  kfok: the bound
+    // is valid (the chain E_ref -> E_i has not been broken by a rescaling or N != 0).
+    double kf[4];
+    double kfcum;
+    int32_t kfok;
+    int32_t zit;   // iteration whose Z-step the lean kernel completed (the full kernel skips it)
+    // Lazy dual residual (ZArgs::lazy_dual): the convergence test (:372) needs res_dual and
+    // thresh_dual (the only consumers of A'*Y, :330/:366/:369) only when the primal test passes
+    // and the combined one fails.  The Z-step then sets dpend and keeps what dual_fixup needs to
+    // finish the test: dZ2 = ||Z - Z0||^2, nZ2 = ||Z||^2 and res_comb.
+    double pd_dZ2, pd_nZ2, pd_rc;
+    int32_t dpend, pad_;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
+
+// Parameters of the convergence test (inferLowRankV4_multi.m:364-381) that a deferred dual
+// residual needs (ZArgs / GykArgs carry one).
+struct DualCtl {
+    double tol_abs, tol_rel, rho;
+    int fixed_iters, n, r;
+    int* done_count;
+};
+// Finish a convergence test left pending by iter_control (RealState::dpend): res_dual and
+// thresh_dual (:366, :369) from dAtY = ||A^H (Y - Y0)||^2 and nAtY = ||A^H Y||^2, the test
+// (:372: the primal part held and the combined part failed, so it is the dual part), then the
+// stop or the mu update (:379-381).  Returns 1 when the realisation stopped.
+__device__ __forceinline__ int dual_finish(const DualCtl& c, RealState* st, double dAtY, double nAtY) {
+    const double mu = st->mu, rc = st->pd_rc;
+    const double res_dual = mu * sqrt(fmax(0.0, dAtY) + st->pd_dZ2);
+    const double t_dual = c.tol_abs * sqrt((double)c.n * c.r * 2) + c.tol_rel * sqrt(fmax(0.0, nAtY) + st->pd_nZ2);
+    st->dAtY = dAtY;
+    st->nAtY = nAtY;
+    st->dpend = 0;
+    bool stop = false;
+    if (res_dual < t_dual) {
+        st->status |= ACE_ST_CONVERGED;
+        if (!c.fixed_iters) stop = true;
+    }
+    if (stop) {
+        st->done = 1;
+        atomicAdd(c.done_count, 1);
+        return 1;
+    }
+    if (rc > st->last_res * 0.9) st->mu = mu * c.rho;
+    st->last_res = rc;
+    return 0;
+}
 
 // wave64 reduction of a double
 __device__ __forceinline__ double wave_sum(double v) {
@@ -160,6 +210,10 @@ struct GykArgs {
     const double* N;
     const double* zeros;
     int n;
+    // lazy dual residual: no K Y; a convergence test the previous Z-step left pending
+    // (RealState::dpend) is finished at the start from K Y_k and K (Y_k - Y_{k-1}) (Yo, Yn)
+    int lazy;
+    DualCtl dc;
 };
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
@@ -251,6 +305,12 @@ struct ZArgs {
     int yfused;
     const double* zeros;   // n zero complex entries (the N of realisations with nzero set)
     int nuclear;           // one-wave kernel: A2nuclear r = 1 prox Z = E max(0, |E| - 1/mu) / |E|
+    int lean;              // zlean_kernel ran before this launch: skip realisations with st->zit == it
+    // lazy dual residual (RealState::dpend): the dual terms are formed only when the convergence
+    // test needs them, from the f64 K = A A^H (shared, [m][m] c128) and Ynew, Yold
+    int lazy_dual;
+    const double* Kf;
+    int fixup_now;   // last iteration: finish a pending test here (dual_fixup), no later gyk_kernel
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {
@@ -291,6 +351,10 @@ __device__ __forceinline__ ZProfile z_profile(const ZArgs& a, int b) {
     return p;
 }
 void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st);  // A2only, one wave per realisation
+// steady-state A2only Z-step (wmode, ping-pong, N = 0 on entry) under the perturbation
+// certificate (RealState::kf); realisations it cannot certify are left to launch_zstep1w
+void launch_zlean(const ZArgs& a, int batch, hipStream_t st);
+bool zlean_enabled();
 void launch_pre(int n, int m, int batch, const double* Z, const double* N, const double* Y, const double* M, double* V,
                 double* S, const RealState* rs, hipStream_t st);
 void launch_ystep(int m, int batch, const double* S, const double* g, double* M, const double* B, const double* Yold,

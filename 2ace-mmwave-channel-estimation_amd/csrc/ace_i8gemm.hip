@@ -488,10 +488,9 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ double red[8][GRB][7];
     __shared__ double sc_s[GRB], p2_s[GRB];
-    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB];
-    __shared__ double imu0_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB];
+    __shared__ double imu0_s[GRB], mu_s[GRB];
     const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
-    const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
     d2* Ts = reinterpret_cast<d2*>(smem);               // [16][tst]: T, then Y_new
     int8_t* Ad = reinterpret_cast<int8_t*>(smem) + ((GRB * tst * 16 + 255) & ~255);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB;
@@ -502,10 +501,128 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         const bool lv = j < nb && !a.rs[j].done;
         live_s[t] = lv;
         avok_s[t] = lv && a.AX && a.rs[j].avok;
-        imu0_s[t] = lv ? 1.0 / a.rs[j].mu : 0.0;
+        mu_s[t] = lv ? a.rs[j].mu : 1.0;
+        imu0_s[t] = lv ? 1.0 / mu_s[t] : 0.0;
         oys_s[t] = lv ? a.rs[j].optysrc : 0;
+        pend_s[t] = lv && a.lazy && a.rs[j].dpend;
     }
     __syncthreads();
+    const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
+    // ---- lazy dual residual: the previous Z-step left some convergence tests pending (the primal
+    // part held, the combined part failed: inferLowRankV4_multi.m:372 needs res_dual).  They are
+    // finished here, before this iteration uses mu, from ||A^H Y_k||^2 = Y_k^H K Y_k and
+    // ||A^H (Y_k - Y_{k-1})||^2 (Y_k in Yo, Y_{k-1} still in Yn) on the int8 matrix cores (two
+    // passes of the K Y machinery below).  Rare: a few iterations per solve.
+    if (a.lazy && __syncthreads_or(t < GRB && pend_s[t])) {
+        const int bl = t >> 5, cp = t & 31, h = lane >> 5, ldo = 2 * m, ocb = NCB / 2, ncb = (ldo + ocb - 1) / ocb;
+        const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
+        const i4v* Bf = reinterpret_cast<const i4v*>(a.LK);
+        const int total = ncb * nksK;
+        const double* Ysd = reinterpret_cast<const double*>(Ts);
+        for (int pass = 0; pass < 2; ++pass) {
+            double mx = 0.0, sn = 0.0;
+            for (int i = cp; i < mp; i += 32) {   // half-wave bl: realisation bl
+                d2 v = make_double2(0.0, 0.0);
+                if (pend_s[bl] && i < m) {
+                    const long long o = (long long)(j0 + bl) * m + i;
+                    const d2 yk = reinterpret_cast<const d2*>(a.Yo)[o];
+                    v = pass ? csub(yk, reinterpret_cast<const d2*>(a.Yn)[o]) : yk;
+                }
+                Ts[bl * tst + i] = v;
+                mx = fmax(mx, fmax(fabs(v.x), fabs(v.y)));
+                sn += 0.0 * (fabs(v.x) + fabs(v.y));
+            }
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                mx = fmax(mx, __shfl_xor(mx, o, 64));
+                sn += __shfl_xor(sn, o, 64);
+            }
+            double p2, sc;
+            plane_scale(mx + sn, a.c8[1], p2, sc);
+            if (cp == 0) sc_s[bl] = sc;
+            __syncthreads();
+            for (int s = 0; s < nksK / KSC; ++s) {
+                d2 x[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int k = 64 * s + 2 * cp + u;
+                    x[u] = k < m ? Ts[bl * tst + k] : make_double2(0.0, 0.0);
+                }
+                const double v[4] = {x[0].x, x[0].y, x[1].x, x[1].y};
+                uint32_t d[8];
+                digits4(v, p2, d);
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt)
+                    *reinterpret_cast<uint32_t*>(&Ad[lds_row(bl, tt) * rst + KC * s + 4 * cp]) = d[tt];
+            }
+            __syncthreads();
+            auto bfl = [&](BSet& bs, int f0) {
+#pragma unroll
+                for (int kk = 0; kk < SK; ++kk) {
+                    const int f = min(f0 + kk, total - 1), cb = f / nksK, ks = f - cb * nksK;
+                    const i4v* pp = Bf + ((long long)(cb * (NCB / 32) + 2 * w) * nksK + ks) * 64 + lane;
+                    bs.f[kk][0] = pp[0];
+                    bs.f[kk][1] = pp[(long long)nksK * 64];
+                }
+            };
+            double pacc[4][2];
+#pragma unroll
+            for (int R = 0; R < 4; ++R) pacc[R][0] = pacc[R][1] = 0.0;
+            i16v acc[4][2];
+#pragma unroll
+            for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+            BSet bA, bB;
+            bfl(bA, 0);
+            for (int f = 0; f < total; f += 2 * SK) {
+                bfl(bB, f + SK);
+                __builtin_amdgcn_sched_barrier(0);
+                stage_mma(arow + 32 * (f % nksK), rst, bA, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                bfl(bA, f + 2 * SK);
+                __builtin_amdgcn_sched_barrier(0);
+                stage_mma(arow + 32 * ((f + SK) % nksK), rst, bB, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                if ((f + 2 * SK) % nksK == 0) {   // v^H (K v) over this 32-column tile
+                    const int col = ((f / nksK) * (NCB / 64) + w) * 32 + (lane & 31);
+#pragma unroll
+                    for (int R = 0; R < 4; ++R)
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const int blo = 4 * R + 2 * q + h;
+                            if (pend_s[blo] && col < ldo) {
+                                i16v cmb;
+#pragma unroll
+                                for (int e = 0; e < 16; ++e) cmb[e] = acc[R][0][e] + 128 * acc[R][1][e];
+                                pacc[R][q] += Ysd[2 * blo * tst + col] * (sc_s[blo] * recombine(cmb, q));
+                            }
+                        }
+#pragma unroll
+                    for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+                }
+            }
+#pragma unroll
+            for (int R = 0; R < 4; ++R)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+#pragma unroll
+                    for (int o = 1; o < 32; o <<= 1) pacc[R][q] += __shfl_xor(pacc[R][q], o, 64);
+                    if ((lane & 31) == 0) red[w][4 * R + 2 * q + h][pass] = pacc[R][q];
+                }
+            __syncthreads();
+        }
+        if (t < GRB && pend_s[t]) {
+            double nv = 0.0, dv = 0.0;
+            for (int q = 0; q < 8; ++q) {   // fixed order over the waves
+                nv += red[q][t][0];
+                dv += red[q][t][1];
+            }
+            RealState* rs = a.rs + j0 + t;
+            if (dual_finish(a.dc, rs, dv, nv)) live_s[t] = 0;   // stopped at the previous iteration
+            mu_s[t] = rs->mu;
+            imu0_s[t] = 1.0 / mu_s[t];
+        }
+        __syncthreads();
+    }
     // deferred opt_Y (RealState::optysrc): the best Y_new still lives in the buffer this iteration's
     // Y-step is about to overwrite -- save it first (rare: no better iterate in the last iteration)
     if (a.yn_id)
@@ -616,7 +733,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int jl = (lane >> 4) + 4 * r;
-        muv[r] = a.rs[live_s[jl] ? j0 + jl : j0].mu;
+        muv[r] = mu_s[jl];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int i = min(16 * (2 * w + c) + (lane & 15), m - 1);
@@ -737,6 +854,7 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         if (!a.yn_id && live_s[jl] && imp_s[jl])
             reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
     }
+    if (a.lazy) return;   // no K Y: the Z-step forms the dual terms when the test needs them
 #ifdef ACE_GYK_PROBE_P3
     return;
 #endif

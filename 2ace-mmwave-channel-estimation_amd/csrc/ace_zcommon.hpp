@@ -78,12 +78,120 @@ __device__ __forceinline__ int circ_next(int n, int p) {
 // Z-step reductions: best-objective bookkeeping (inferLowRankV4_multi.m:344-351),
 // residuals (:364-366), thresholds (:368-370), stop test (:372), mu update (:379-381).
 // Sums: nX2 = ||X||^2, nZ2 = ||Z||^2, jn2 = ||X - Z||^2, dZ2 = ||Z - Z0||^2,
-// dAtY = ||A^H (Y - Y0)||^2, nAtY = ||A^H Y||^2.  Returns 1 when the objective improved.
+// dAtY = ||A^H (Y - Y0)||^2, nAtY = ||A^H Y||^2.  Returns bit 0: the objective improved, bit 1:
+// the convergence test is pending (ZArgs::lazy_dual; the caller runs dual_fixup on the wave).
 // Sum the fused Y-step partials of realisation b (fixed tile order) into v[5].
 __device__ __forceinline__ void ystep_sums(const ZArgs& a, int b, double* v) {
     for (int k = 0; k < 5; ++k) v[k] = 0.0;
     for (int t = 0; t < a.ytiles; ++t)
         for (int k = 0; k < 5; ++k) v[k] += a.ypart[((long long)b * a.ytiles + t) * 5 + k];
+}
+
+// The inputs iter_control reads from RealState, loaded as one batch (the lean Z-step reads them
+// with its other loads: a load issued after the kernel's stores would wait for them to retire).
+struct IterIn {
+    double obj2, nAX2, nY2, nJM2, dY2, opt_obj, last_res;
+    int32_t status;
+};
+__device__ __forceinline__ IterIn iter_in(const RealState* st) {
+    return IterIn{st->obj2, st->nAX2, st->nY2, st->nJM2, st->dY2, st->opt_obj, st->last_res, st->status};
+}
+__device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, const IterIn& in, double mu, double nX2,
+                                               double nZ2, double jn2, double dZ2, double dAtY, double nAtY) {
+    const int m = a.m, n = a.n;
+    const double nX = sqrt(nX2), nZ = sqrt(nZ2);
+    const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
+    const double obj = sqrt(in.obj2);
+    const double nAX = sqrt(in.nAX2), nY = sqrt(in.nY2);
+    const double r = (double)a.r;  // columns per realisation
+    int improved = 0;
+    if (obj < in.opt_obj) {
+        st->opt_obj = obj;
+        improved = 1;
+    }
+    const double res_prim = sqrt(in.nJM2 + jn2);
+    const double res_comb = sqrt(res_prim * res_prim + in.dY2 + dZ2);
+    if (a.lazy_dual) {
+        // (P && D) || C: D is needed only when P holds and C does not (dual_fixup finishes then)
+        const double mx1 = fmax(nAX, nY), mx2 = fmax(nX, nZ);
+        const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
+        const double t_comb =
+            a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
+        st->iters = a.it;
+        if (res_prim < t_prim && !(res_comb < t_comb)) {
+            st->dpend = 1;
+            st->pd_dZ2 = dZ2;
+            st->pd_nZ2 = nZ * nZ;
+            st->pd_rc = res_comb;
+            return improved | 2;   // bit 1: the test is pending (dual_fixup)
+        }
+        const bool conv = res_comb < t_comb;
+        bool stop = false;
+        if (conv) {
+            st->status = in.status | ACE_ST_CONVERGED;
+            if (!a.fixed_iters) stop = true;
+        }
+        if (stop) {
+            st->done = 1;
+            atomicAdd(a.done_count, 1);
+        } else {
+            if (res_comb > in.last_res * 0.9) st->mu = mu * a.rho;
+            st->last_res = res_comb;
+        }
+        return improved;
+    }
+    const double res_dual = mu * sqrt(dAtY2 + dZ2);
+    const double mx1 = fmax(nAX, nY), mx2 = fmax(nX, nZ);
+    const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
+    const double t_dual = a.tol_abs * sqrt((double)n * r * 2) + a.tol_rel * sqrt(nAtY2 + nZ * nZ);
+    const double t_comb =
+        a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
+    st->iters = a.it;
+    const bool conv = (res_prim < t_prim && res_dual < t_dual) || (res_comb < t_comb);
+    bool stop = false;
+    if (conv) {
+        st->status = in.status | ACE_ST_CONVERGED;
+        if (!a.fixed_iters) stop = true;
+    }
+    if (stop) {
+        st->done = 1;
+        atomicAdd(a.done_count, 1);
+    } else {
+        if (res_comb > in.last_res * 0.9) st->mu = mu * a.rho;
+        st->last_res = res_comb;
+    }
+    return improved;
+}
+// Finish a pending convergence test (RealState::dpend) on one wave, for the last iteration
+// (ZArgs::fixup_now; before it, gyk_kernel of the next iteration finishes it on the int8
+// matrix cores): ||A^H (Y - Y0)||^2 = dY^H K dY and ||A^H Y||^2 = Y^H K Y from the f64 K (rows
+// of K^H = K read coalesced), then dual_finish.
+__device__ __forceinline__ void dual_fixup(const ZArgs& a, int b, RealState* st) {
+    const int lane = threadIdx.x & 63, m = a.m;
+    const d2* Yn = reinterpret_cast<const d2*>(a.Ynew) + (long long)b * m;
+    const d2* Yo = reinterpret_cast<const d2*>(a.Yold) + (long long)b * m;
+    const d2* K = reinterpret_cast<const d2*>(a.Kf);
+    double dacc = 0.0, nacc = 0.0;
+    for (int i0 = 0; i0 < m; i0 += 64) {
+        const int i = i0 + lane, ic = min(i, m - 1);
+        double kyr = 0.0, kyi = 0.0, kdr = 0.0, kdi = 0.0;
+        for (int k = 0; k < m; ++k) {
+            const d2 y = Yn[k], yo = Yo[k], kk = K[(long long)k * m + ic];   // K[ic][k] = conj(kk)
+            const double dyr = y.x - yo.x, dyi = y.y - yo.y;
+            kyr += kk.x * y.x + kk.y * y.y;
+            kyi += kk.x * y.y - kk.y * y.x;
+            kdr += kk.x * dyr + kk.y * dyi;
+            kdi += kk.x * dyi - kk.y * dyr;
+        }
+        if (i < m) {
+            const d2 y = Yn[i], yo = Yo[i];
+            const double dyr = y.x - yo.x, dyi = y.y - yo.y;
+            nacc += y.x * kyr + y.y * kyi;
+            dacc += dyr * kdr + dyi * kdi;
+        }
+    }
+    const double dAtY = wave_sum(dacc), nAtY = wave_sum(nacc);
+    if (lane == 0) dual_finish(DualCtl{a.tol_abs, a.tol_rel, a.rho, a.fixed_iters, a.n, a.r, a.done_count}, st, dAtY, nAtY);
 }
 
 __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, double mu, double nX2, double nZ2,
@@ -97,40 +205,7 @@ __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, doubl
         st->nJM2 = v[3];
         st->dY2 = v[4];
     }
-    const int m = a.m, n = a.n;
-    const double nX = sqrt(nX2), nZ = sqrt(nZ2);
-    const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
-    const double obj = sqrt(st->obj2);
-    const double nAX = sqrt(st->nAX2), nY = sqrt(st->nY2);
-    const double r = (double)a.r;  // columns per realisation
-    int improved = 0;
-    if (obj < st->opt_obj) {
-        st->opt_obj = obj;
-        improved = 1;
-    }
-    const double res_prim = sqrt(st->nJM2 + jn2);
-    const double res_dual = mu * sqrt(dAtY2 + dZ2);
-    const double res_comb = sqrt(res_prim * res_prim + st->dY2 + dZ2);
-    const double mx1 = fmax(nAX, nY), mx2 = fmax(nX, nZ);
-    const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
-    const double t_dual = a.tol_abs * sqrt((double)n * r * 2) + a.tol_rel * sqrt(nAtY2 + nZ * nZ);
-    const double t_comb =
-        a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
-    st->iters = a.it;
-    const bool conv = (res_prim < t_prim && res_dual < t_dual) || (res_comb < t_comb);
-    bool stop = false;
-    if (conv) {
-        st->status |= ACE_ST_CONVERGED;
-        if (!a.fixed_iters) stop = true;
-    }
-    if (stop) {
-        st->done = 1;
-        atomicAdd(a.done_count, 1);
-    } else {
-        if (res_comb > st->last_res * 0.9) st->mu = mu * a.rho;
-        st->last_res = res_comb;
-    }
-    return improved;
+    return iter_control_in(a, st, iter_in(st), mu, nX2, nZ2, jn2, dZ2, dAtY, nAtY);
 }
 
 }  // namespace

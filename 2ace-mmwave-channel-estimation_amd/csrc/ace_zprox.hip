@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
     }
     block_sum<6>(v6, red);
-    if (t == 0) flag_improved = iter_control(a, st, mu, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]);
+    if (t == 0) flag_improved = iter_control(a, st, mu, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]) & 1;   // (no lazy_dual here)
     write_vbound();
     __syncthreads();
     if (flag_improved) {  // best-objective iterate (:344-361): all columns, or the argmin column

@@ -57,6 +57,12 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->allow_i8 = true;
 }
 
+// ACE_FUSE=0 runs the lean Z-step as its own launch instead of in apply_AH's epilogue.
+static bool fuse_enabled() {
+    const char* e = getenv("ACE_FUSE");
+    return !(e && e[0] == '0');
+}
+
 // ACE_LAZY_DUAL=0 keeps K Y in gyk_kernel every iteration (A/B comparisons); read per solve.
 static bool lazy_dual_enabled() {
     const char* e = getenv("ACE_LAZY_DUAL");
@@ -87,7 +93,7 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipMemcpyAsync(c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
     ACE_HIP(hipStreamSynchronize(st));
-    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= 160 * 1024 - 256;
+    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= 160 * 1024 - 8192;
     if (!L.i8ok) return ACE_OK;
     c[1] = c[0] * c[0];
     ACE_HIP(hipMemcpyAsync(L.c8 + 1, c + 1, sizeof(double), hipMemcpyHostToDevice, st));
@@ -297,11 +303,6 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
                 launch_gyk(nb[h], m, ga, sh);
             }
             ACE_HIP(stagger_mark(h, it, 2));
-            {
-                ProfScope ps(ACE_K_APPLY_AH, sh);
-                launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh);
-            }
-            ACE_HIP(stagger_mark(h, it, 3));
             ZArgs za = za0;
             za.it = it;
             za.wmode = 1;
@@ -322,9 +323,17 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.fixup_now = it == p.maxiter;
             za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
             za.lean = lean;
+            // the steady-state Z-step in apply_AH's epilogue (not at the last iteration, whose
+            // pending convergence tests the one-wave kernels finish)
+            za.xfuse = lean && it != p.maxiter && fuse_enabled();
+            {
+                ProfScope ps(ACE_K_APPLY_AH, sh);
+                launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh, za.xfuse ? &za : nullptr);
+            }
+            ACE_HIP(stagger_mark(h, it, 3));
             {
                 ProfScope ps(ACE_K_ZSTEP, sh);
-                if (lean) launch_zlean(za, nb[h], sh);
+                if (lean && !za.xfuse) launch_zlean(za, nb[h], sh);
                 launch_zstep(p.variant, false, za, nb[h], sh);
             }
         }
@@ -481,7 +490,19 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         }
         if (!pc) {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
-            if (wmode) launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st);
+            if (wmode) {
+                za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled() &&
+                           it != p.maxiter && fuse_enabled();
+                if (za.xfuse) {   // the fused kernel needs this iteration's Z-step arguments
+                    za.it = it;
+                    za.wmode = 1;
+                    za.Z = Zc;
+                    za.N = Nc;
+                    za.Zn = Zo;
+                    za.Nn = No;
+                }
+                launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st, za.xfuse ? &za : nullptr);
+            }
             else if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
             else applyAH(w.g, w.X, w.V);
         }
@@ -504,7 +525,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.fixup_now = it == p.maxiter;
         {
             ProfScope ps(ACE_K_ZSTEP, st);
-            if (za.lean) launch_zlean(za, batch, st);
+            if (za.lean && !za.xfuse) launch_zlean(za, batch, st);
             launch_zstep(p.variant, false, za, batch, st);
         }
         q = 1 - q;

@@ -60,7 +60,11 @@ struct RealState {
     // and the combined one fails.  The Z-step then sets dpend and keeps what dual_fixup needs to
     // finish the test: dZ2 = ||Z - Z0||^2, nZ2 = ||Z||^2 and res_comb.
     double pd_dZ2, pd_nZ2, pd_rc;
-    int32_t dpend, pad_;
+    int32_t dpend;
+    // the fused apply_AH (ace_i8gemm.hip, i8ah_kernel<false, true>) formed X = Z' of iteration fzit
+    // and left ||X||^2 and ||X - Z||^2 for zstep1w_kernel's certificate and iteration control
+    int32_t fzit;
+    double fs0, fs3;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -176,8 +180,10 @@ void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, 
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
                        const double* AX, hipStream_t st);
 // W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
+// fuse != nullptr: the steady-state Z-step runs in the epilogue (i8ah_kernel<false, true>)
+struct ZArgs;
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
-                        const RealState* rs, hipStream_t st);
+                        const RealState* rs, hipStream_t st, const ZArgs* fuse = nullptr);
 size_t i8ah_lds_bytes(int kc);
 // Fused g = G T (3M f64 MFMA), Y-step, K Y (int8 digit planes), dual terms and opt_Y for
 // 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
@@ -311,6 +317,7 @@ struct ZArgs {
     int lazy_dual;
     const double* Kf;
     int fixup_now;   // last iteration: finish a pending test here (dual_fixup), no later gyk_kernel
+    int xfuse;       // the fused apply_AH ran: realisations with st->fzit == it have X in Zn and their sums
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

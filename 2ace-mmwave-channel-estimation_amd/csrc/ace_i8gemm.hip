@@ -34,6 +34,7 @@
 // realisation's m entries in a pre-pass.  A non-finite bound yields NaN outputs for that
 // realisation (the f64 product would not be finite either).
 #include "ace_i8.hpp"
+#include "ace_zcommon.hpp"
 
 namespace ace {
 
@@ -289,14 +290,27 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
 // two accumulator tiles are the two planes of the same 32 output columns; they are combined
 // exactly in int32 (acc_lo + 128 acc_hi) before the recombination.  A work-group then covers
 // 256 output columns per block.
-template <bool KY>
+//
+// FUSE (unit path, from r02): the steady-state Z-step's data pass runs in the epilogue.  For a
+// realisation with N = 0 and a valid perturbation certificate (RealState::kfok, nzero) the
+// epilogue forms X = Z + W (xw with N = 0) and stores it as Z' = E = X instead of storing W, and
+// reduces ||X||^2 and ||X - Z||^2; W then never goes through HBM.  The sums go to RealState
+// (fs0, fs3, fzit) and zstep1w_kernel, one wave per realisation, checks the bound and runs the
+// iteration control (or, if the bound fails, the full Z-step with X read from Z').  An
+// ineligible realisation gets W as before.
+struct FuseState {   // per realisation, loaded in the prologue
+    int el, keep_cur, optsrc;
+};
+template <bool KY, bool FUSE>
 __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
                                                      const double* __restrict__ Gp, double* __restrict__ Wp,
                                                      const double* __restrict__ cptr,
-                                                     const RealState* __restrict__ rs) {
+                                                     const RealState* __restrict__ rs, ZArgs za) {
     extern __shared__ __attribute__((aligned(16))) int8_t Ad[];
     __shared__ double sc_s[RB];
     __shared__ int live_s[RB];
+    __shared__ FuseState fs_s[FUSE ? RB : 1];
+    __shared__ double fred[FUSE ? 8 : 1][RB][2];
     const int rst = 32 * nks + 16;   // LDS row stride (bytes)
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -305,6 +319,24 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     STAMP_DECL;
     STAMP(0);
     const bool live = jb < nb && !rs[jb].done;
+    const int zn_id = 1 + (za.it & 1);
+    if constexpr (FUSE) {
+        if (t < RB) {
+            const int j = j0 + t;
+            FuseState f{};
+            if (j < nb && !rs[j].done) {
+                const RealState& r = rs[j];
+                f.el = r.kfok && r.nzero;
+                const bool improved_pre = sqrt(r.obj2) < r.opt_obj;   // (as the Z-step decides it)
+                f.keep_cur = !improved_pre && !(r.opt_obj < INFINITY);
+                f.optsrc = r.optsrc;
+            }
+            fs_s[t] = f;
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                for (int q = 0; q < 8; ++q) fred[q][t][k] = 0.0;
+        }
+    }
     const d2* g = reinterpret_cast<const d2*>(Gp) + (long long)jb * Kc;
 
     // g of this realisation: 2 complex entries per 128-real block per thread, one batch of
@@ -367,6 +399,17 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     }
     __syncthreads();
     STAMP(1);
+    if constexpr (FUSE) {
+        // deferred opt_X: the Z' buffer of an eligible realisation holds its best iterate -- keep
+        // it before the epilogue overwrites it (rare; fs_s is visible after the staging barrier)
+        for (int r = 0; r < RB; ++r)
+            if (fs_s[r].el && fs_s[r].optsrc == zn_id) {
+                const long long o = (long long)(j0 + r) * 2 * Mc;
+                for (int i = t; i < 2 * Mc; i += NT) za.optX[o + i] = za.Zn[o + i];
+                __syncthreads();
+                if (t == 0) za.st[j0 + r].optsrc = 0;
+            }
+    }
 
     const int h = lane >> 5, ldo = 2 * Mc, ocb = KY ? NCB / 2 : NCB, ncb = (ldo + ocb - 1) / ocb;
     const int8_t* arow = &Ad[(lane & 31) * rst + 16 * (lane >> 5)];
@@ -380,7 +423,22 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
             b.f[kk][1] = p[(long long)nks * 64];
         }
     };
-    auto epilogue = [&](int cbk, i16v (&acc)[4][2]) {
+    // FUSE: Z at this lane's 16 epilogue outputs of block cbk (eligible realisations)
+    auto zload = [&](int cbk, double (&zv)[4][2][2]) {
+        const int ct0 = cbk * (NCB / 32) + 2 * w;
+#pragma unroll
+        for (int R = 0; R < 4; ++R)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int blo = 4 * R + 2 * q + (lane >> 5), j = min(j0 + blo, nb - 1);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int col = min((ct0 + c) * 32 + (lane & 31), 2 * Mc - 1);
+                    zv[R][q][c] = fs_s[blo].el ? za.Z[(long long)j * 2 * Mc + col] : 0.0;
+                }
+            }
+    };
+    auto epilogue = [&](int cbk, i16v (&acc)[4][2], const double (&zv)[4][2][2]) {
         if constexpr (KY) {   // one 32-column output tile per wave: low + 128 x high digit plane
             const int col = (cbk * (NCB / 64) + w) * 32 + (lane & 31);
 #pragma unroll
@@ -399,6 +457,46 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
             return;
         }
         const int ct0 = cbk * (NCB / 32) + 2 * w;
+        if constexpr (FUSE) {   // zv: requested two stages ahead by the sweep (zload)
+#pragma unroll
+            for (int R = 0; R < 4; ++R)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                    const bool el = fs_s[blo].el, kc = fs_s[blo].keep_cur;
+                    double p0 = 0.0, p3 = 0.0;
+                    if (j < nb && live_s[blo]) {
+                        const double scb = sc_s[blo];
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const int col = (ct0 + c) * 32 + (lane & 31);
+                            if (col >= ldo) continue;
+                            const long long off = (long long)j * ldo + col;
+                            const double wv = scb * recombine(acc[R][c], q);
+                            if (el) {
+                                const double x = zv[R][q][c] + wv, d = x - zv[R][q][c];
+                                za.Zn[off] = x;
+                                if (kc) za.Xcur[off] = x;
+                                p0 += x * x;
+                                p3 += d * d;
+                            } else {
+                                Wp[off] = wv;
+                            }
+                        }
+                    }
+                    if (el) {   // half-wave reduction, then this wave's slot (fixed order over blocks)
+#pragma unroll
+                        for (int o = 1; o < 32; o <<= 1) {
+                            p0 += __shfl_xor(p0, o, 64);
+                            p3 += __shfl_xor(p3, o, 64);
+                        }
+                        if ((lane & 31) == 0) {
+                            fred[w][blo][0] += p0;
+                            fred[w][blo][1] += p3;
+                        }
+                    }
+                }
+        } else {
 #pragma unroll
         for (int R = 0; R < 4; ++R)
 #pragma unroll
@@ -412,6 +510,7 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
                     if (col < ldo) Wp[(long long)j * ldo + col] = scb * recombine(acc[R][c], q);
                 }
             }
+        }
 #pragma unroll
         for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
     };
@@ -420,19 +519,69 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
     BSet bA, bB;
     bfl(bA, 0);
-    for (int f = 0; f < total; f += 2 * SK) {
-        bfl(bB, f + SK);
-        __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
-        stage_mma(arow + 32 * (f % nks), rst, bA, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        bfl(bA, f + 2 * SK);
-        __builtin_amdgcn_sched_barrier(0);
-        stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc);
+    if constexpr (FUSE) {
+        // the last loop step of every block is peeled: its Z loads go out right after the stage's
+        // codebook loads, so no wait before the epilogue's own waits for them (vmcnt retires in
+        // order: a load issued under a branch would make every wait a full drain)
+        double zv[4][2][2];
+        const int per = nks / (2 * SK);
+        for (int cbk = 0; cbk < ncb; ++cbk) {
+            const int f0 = cbk * nks;
+            for (int i = 0; i < per - 1; ++i) {
+                const int f = f0 + 2 * SK * i;
+                bfl(bB, f + SK);
+                __builtin_amdgcn_sched_barrier(0);
+                stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                bfl(bA, f + 2 * SK);
+                __builtin_amdgcn_sched_barrier(0);
+                stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const int f = f0 + 2 * SK * (per - 1);
+            bfl(bB, f + SK);
+            zload(cbk, zv);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            bfl(bA, f + 2 * SK);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            epilogue(cbk, acc, zv);
+        }
+    } else {
+        const double zv0[4][2][2] = {};
+        for (int f = 0; f < total; f += 2 * SK) {
+            bfl(bB, f + SK);
+            __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
+            stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            bfl(bA, f + 2 * SK);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc, zv0);
+        }
     }
     STAMP(2);
-    if (!KY) STAMP_PRINT("i8ah prologue|sweep:", 3);
+    if (!KY && !FUSE) STAMP_PRINT("i8ah prologue|sweep:", 3);
+    if constexpr (FUSE) {
+        __syncthreads();
+        if (t < RB && fs_s[t].el && live_s[t]) {
+            double s0 = 0.0, s3 = 0.0;
+            for (int q = 0; q < 8; ++q) {   // fixed order over the waves
+                s0 += fred[q][t][0];
+                s3 += fred[q][t][1];
+            }
+            RealState* st = za.st + j0 + t;
+            st->fs0 = s0;   // ||E||^2 = ||X||^2
+            st->fs3 = s3;   // ||E - E_prev||^2 = ||X - Z||^2
+            st->fzit = za.it;
+        }
+        STAMP(3);
+        STAMP_PRINT("i8ah-fused prologue|sweep|post:", 4);
+    }
 }
 
 // Codebook check and expansion.  cmax = max |component| of A (device scalar).  Each
@@ -1047,13 +1196,13 @@ void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, i
 void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
                        const RealState* rs, hipStream_t st) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<true>),
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<true, false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
     }();
     (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
-    hipLaunchKernelGGL(i8ah_kernel<true>, grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
-                       reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs);
+    hipLaunchKernelGGL((i8ah_kernel<true, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
+                       reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs, ZArgs{});
 }
 size_t gyk_gfrag_bytes(int m) { return (size_t)gyk_mp(m) * gyk_mp(m) * 16; }
 size_t gyk_lds_bytes(int m) {   // Ts, then the Ad region: K Y digit planes, or apply_A's digit stages
@@ -1076,15 +1225,24 @@ void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(gyk_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyk_lds_bytes(m), st, nb, m, a);
 }
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
-                        const RealState* rs, hipStream_t st) {
+                        const RealState* rs, hipStream_t st, const ZArgs* fuse) {
     static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
+        // dynamic + static (FUSE: 7.3 KiB of per-realisation state and partial sums) <= 160 KiB
+        const bool a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false, false>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192) == hipSuccess;
+        const bool a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false, true>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192) == hipSuccess;
+        (void)hipGetLastError();
+        return a0 && a1;
     }();
     (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
-    hipLaunchKernelGGL(i8ah_kernel<false>, grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
-                       reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs);
+    if (fuse)
+        hipLaunchKernelGGL((i8ah_kernel<false, true>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+                           reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, *fuse);
+    else
+        hipLaunchKernelGGL((i8ah_kernel<false, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+                           reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, ZArgs{});
 }
 
 }  // namespace ace

@@ -64,6 +64,37 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     RealState* st = a.st + b;
     if (!INIT && st->done) return;
     if (!INIT && a.lean && st->zit == a.it) return;   // zlean_kernel completed this iteration
+    // The fused apply_AH formed X = Z + W of this iteration in Z' with its sums: the perturbation
+    // certificate of zlean_kernel, then the iteration control; if the bound fails, the full
+    // Z-step below runs on X read from Z'.
+    const bool xin = !INIT && a.xfuse && st->fzit == a.it;
+    if (xin) {
+        int ok = 0;
+        if (threadIdx.x == 0) {
+            const double s0 = st->fs0, s3 = st->fs3;
+            const double cum = (st->kfcum + sqrt(s3)) * (1.0 + 0x1p-40);
+            bool pass = s0 > 0.0;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                if (p >= pf.np) break;
+                const double lb = st->kf[p] * (1.0 - 1e-12) - cum;
+                pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
+            }
+            if (pass) {
+                const bool improved_pre = sqrt(st->obj2) < st->opt_obj;
+                const int optsrc = st->optsrc;   // (the fused kernel kept a best iterate in Z')
+                iter_control(a, st, st->mu, s0, s0, 0.0, s3, st->dAtY, st->nAtY);
+                st->vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
+                st->nzero = 1;
+                st->avok = 1;
+                st->optsrc = improved_pre ? 1 + (a.it & 1) : optsrc;   // deferred opt_X: X = Z' bit for bit
+                st->kfcum = cum;
+                st->zit = a.it;
+                ok = 1;
+            }
+        }
+        if (__shfl(ok, 0, 64)) return;
+    }
     __shared__ __attribute__((aligned(16))) d2 T0[ZT * ZHS];
     __shared__ double4 RotS[16];
     __shared__ double wv[ZT], scl[ZT], rs2[ZT];
@@ -71,7 +102,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     __shared__ int flag_any, flag_fast;
 
     const double mu = INIT ? 1.0 : st->mu;
-    const d2* X = reinterpret_cast<const d2*>(a.X) + (long long)b * n;
+    const d2* X = reinterpret_cast<const d2*>(xin ? a.Zn : a.X) + (long long)b * n;
     // wmode + ping-pong: N may be the exact zero vector (RealState::nzero), and in the common case
     // Z = E the new N is stored as exact zero (see RealState::nzero)
     const bool flushN = !INIT && a.wmode && a.Zn && a.Zn != a.Z && a.zeros;
@@ -86,7 +117,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const bool warm = (!INIT) && a.warm && !nuc;
     const double imu = 1.0 / mu;
     // wmode: the X buffer holds W = A^H g and X = (Z - N/mu) + W is formed here
-    const bool wm = !INIT && a.wmode;
+    const bool wm = !INIT && a.wmode && !xin;
     auto loadx = [&](int k, d2 nn, d2 zo) -> d2 {
         const d2 v = X[k];
         return wm ? xw(zo, nn, v, imu) : v;

@@ -281,15 +281,39 @@ def test_lean_zstep_bit_identical(gpu, monkeypatch, a_shared, batch):
     """The steady-state Z-step under the perturbation certificate (zlean_kernel) produces exactly
     what the full one-wave Z-step produces (same element order and sums at 32 antennas); it only
     replaces the Ky Fan certificate by a bound that implies it.  ACE_LEAN=0 runs the full kernel
-    every iteration.  Shared (split sub-batches and one batch) and private phase-code codebooks."""
+    every iteration.  Shared (split sub-batches and one batch) and private phase-code codebooks.
+    The same Z-step fused into apply_AH's epilogue (ACE_FUSE, shared codebooks) reduces its sums
+    in another order: equal to rounding, same iteration counts."""
     import torch
     from ace_amd import infer_admm_batch, synth_problem
     A, B, X0, _ = synth_problem(41, 0, batch, 256, 32, 32, a_shared=a_shared)
     out = {}
-    for lean in ("0", "1"):
+    for lean, fuse in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("ACE_LEAN", lean)
+        monkeypatch.setenv("ACE_FUSE", fuse)
         r = infer_admm_batch(A, B, X0, 32, 32, maxiter=200, fixed_iters=True)
         torch.cuda.synchronize()
-        out[lean] = (r.X.cpu().numpy(), r.Y.cpu().numpy(), r.iters.cpu().numpy())
-    for a, b in zip(out["0"], out["1"]):
+        out[lean + fuse] = (r.X.cpu().numpy(), r.Y.cpu().numpy(), r.iters.cpu().numpy())
+    for a, b in zip(out["00"], out["10"]):
         assert np.array_equal(a, b)
+    assert _errs(out["11"][0], out["00"][0]).max() <= 1e-12
+    assert np.array_equal(out["11"][2], out["00"][2])
+
+
+@pytest.mark.parametrize("batch", [64, 1024])
+def test_fused_zstep_convergence_mode(gpu, monkeypatch, batch):
+    """Convergence mode through the fused apply_AH Z-step and the lazy dual residual: iteration
+    counts and the converged flags equal the oracle's (a sample of the batch)."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(43, 0, batch, 256, 32, 32)
+    monkeypatch.setenv("ACE_LEAN", "1")
+    monkeypatch.setenv("ACE_FUSE", "1")
+    r = infer_admm_batch(A, B, X0, 32, 32, maxiter=500)
+    torch.cuda.synchronize()
+    idx = [0, batch // 2, batch - 1]
+    Ah, Bh, X0h = A.cpu().numpy(), B.cpu().numpy()[idx], X0.cpu().numpy()[idx]
+    Xo, _, ito, cvo, _ = _oracle(Ah, Bh, X0h, 32, variant=0, maxiter=500)
+    assert _errs(r.X.cpu().numpy()[idx], Xo).max() <= TOL
+    assert np.array_equal(r.iters.cpu().numpy()[idx], ito)
+    assert np.array_equal(r.converged.cpu().numpy()[idx], cvo)

@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r2e
 mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread -k "lean or split or fixed or convergence" > $O/tests_gpu.log 2>&1 || { echo gpu tests failed; tail -30 $O/tests_gpu.log; exit 1; }
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread  > $O/tests_gpu.log 2>&1 || { echo gpu tests failed; tail -30 $O/tests_gpu.log; exit 1; }
 tail -1 $O/tests_gpu.log
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-regime-p > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));print('value', d['value'], d['kernels_ms'])"

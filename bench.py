@@ -280,29 +280,28 @@ def unit_flops(m, n, tx, rx):
 
 def unit_i8_ops(m, n):
     """int8 matrix-core ops executed per realisation per launch by the digit-plane applies
-    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC;
-    gyk_kernel's K Y: 8 digit planes of Y x 2 base-128 planes of K_int x (2m x 2m) x 2."""
-    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m),
-            "apply_G": 2.0 * 8 * 2 * (2 * m) * (2 * m)}
+    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC.
+    gyk_kernel runs no K Y in the steady state (lazy dual residual, from r02): its int8 work is the
+    rare pending-test resolution, not counted."""
+    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m), "apply_G": 0.0}
 
 
 def unit_bytes(m, n, tx, rx):
     """Algorithmic HBM bytes per realisation per iteration of the steady-state unit path
     (complex128 = 16 B, each array read or written once):
-      zstep (wmode):  read W = A^H g, Z, the top-16 columns of Q (tx x 16); write Z'.  N is the exact
-                      zero vector (RealState::nzero) and is neither read nor written, opt_X is deferred
-                      to the Z' ping-pong buffer (RealState::optsrc), and the dual terms / opt_Y come
-                      from gyk_kernel's RealState fields
-      apply_A (i8):   read Z, Y, M; write T (N = 0 is read from a shared zero page); in the steady
-                      state (RealState::avok) it only checks the block and gyk forms T
-      apply_G (gyk):  read Y, M, AX (T), M, Y0, B (f64), Y0 and K Y0 (dual terms); write g, M, Y, AX,
-                      K Y, opt_Y
-      apply_AH (i8):  read g; write W"""
+      apply_G (gyk):  read Y, M, AX (T = Y - M/mu - AX, the Y-step re-reads M and Y) and B (f64);
+                      write g, AX, M, Y_new.  No K Y and no dual-term reads (lazy dual residual);
+                      opt_Y is deferred to the Y ping-pong buffer (RealState::optysrc)
+      apply_AH (fused i8ah_kernel<false, true>): read g and Z; write Z' = X = Z + A^H g (W stays
+                      on chip); N is the exact zero vector and is neither read nor written
+      zstep:          certificate and iteration control from RealState (no vector traffic in the
+                      steady state; the full Z-step only for realisations the bound cannot certify)
+      apply_A (i8):   read Z, Y, M; write T -- cold iterations only (A V = AX in the steady state)"""
     return {
-        "zstep": 16.0 * 3 * n + 16.0 * 16 * tx,
-        "apply_G": 16.0 * (3 + 2 + 2) * m + 8.0 * m + 16.0 * 6 * m,
+        "zstep": 0.0,
+        "apply_G": 16.0 * 7 * m + 8.0 * m,
         "apply_A": 16.0 * (n + 3 * m),
-        "apply_AH": 16.0 * (m + n),
+        "apply_AH": 16.0 * (m + 2 * n),
     }
 
 
@@ -357,7 +356,7 @@ def cpu_baseline(args, n_samples, private):
                        f"{_cpu_model()}; {setup_note}; solve {t_solve:.2f}s")}
 
 
-PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false>",
+PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false, true>",
               "apply_G": "gyk_kernel"}
 
 
@@ -539,41 +538,48 @@ def unit_bench(args, private, dev, rank, world):
                                         "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "flops_per_launch": f}},
                             "bytes_note": "per realisation: G_b lower triangle (c128) + A_b^H as 2-bit codes + "
                                           "Y, M, AX, B in and AX, M, Y out + W = A^H g out (bench.private_bytes)"}
-                if k == "apply_G" and gyk:   # f64 G T + int8 K Y + the Y-step's HBM traffic, phase after phase
-                    f, o, b = uf[k] * per_launch, io[k] * per_launch, ub[k] * per_launch
-                    tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
+                if k == "apply_G" and gyk:   # f64 G T + the Y-step's HBM traffic, phase after phase
+                    f, b = uf[k] * per_launch, ub[k] * per_launch
+                    tf, tb = f / (PEAK_FP64_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
                     res = {
                         "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
                                 "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
                                 "flops_per_launch": f},
-                        "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
-                                 "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
-                                 "ops_per_launch": o},
                         "hbm": {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
                                 "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
                     }
-                    # the bound is the resource that needs the most time at its peak
-                    main = max((("f64", tf), ("int8", to), ("hbm", tb)), key=lambda x: x[1])[0]
+                    main = "f64" if tf >= tb else "hbm"   # the resource that needs the most time at its peak
                     out = dict(res[main])
                     out.update({"traffic": None, "kernel": k, "resource": main,
                                 "other_resources": {r: v for r, v in res.items() if r != main},
-                                "serial_frac": round((tf + to + tb) / avg_s, 4),
-                                "flop_note": "gyk_kernel runs g = G T (f64 3M; f64 achieved counts 8 flops per complex "
-                                             "MAC), the Y-step (HBM) and K Y (int8 digit planes) one after the other in "
-                                             "each work-group; bound = the resource with the largest time at peak; "
-                                             "serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"})
+                                "serial_frac": round((tf + tb) / avg_s, 4),
+                                "flop_note": "gyk_kernel runs g = G T (f64 3M; achieved counts 8 flops per complex "
+                                             "MAC) and the Y-step (HBM) one after the other in each work-group; "
+                                             "bound = the resource with the largest time at peak; "
+                                             "serial_frac = (t_f64 + t_hbm at peak) / launch time"})
                     return out
-                if k in io and i8:   # exact int8 digit planes on the matrix cores
+                if k in io and i8:   # exact int8 digit planes on the matrix cores (+ apply_AH: the fused Z-step pass)
                     per, pb = io[k] * per_launch, ub[k] * per_launch
-                    return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
-                            "unit": "TOP/s", "frac": round(per / avg_s / 1e12 / PEAK_I8_TOPS, 4), "traffic": None,
-                            "kernel": k, "ops_per_launch": per,
-                            "hbm": {"achieved": round(pb / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                    "frac": round(pb / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": pb},
-                            "f64_equiv_tflops": round(uf[k] * bsz / avg_s / 1e12, 1),
-                            "op_note": "int8 x int8 -> int32 ops of the 8 digit planes x the 2x2 real expansion "
-                                       "(exact: the codebook is a phase code); f64_equiv_tflops counts the same "
-                                       "product as 8 flops per complex MAC"}
+                    to, tb = per / (PEAK_I8_TOPS * 1e12), pb / (PEAK_HBM_GBS * 1e9)
+                    res = {
+                        "int8": {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
+                                 "unit": "TOP/s", "frac": round(per / avg_s / 1e12 / PEAK_I8_TOPS, 4),
+                                 "ops_per_launch": per},
+                        "hbm": {"bound": "hbm", "achieved": round(pb / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": round(pb / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                                "bytes_per_launch": pb},
+                    }
+                    main = "int8" if to >= tb else "hbm"
+                    out = dict(res[main])
+                    out.update({"traffic": None, "kernel": k, "resource": main,
+                                "other_resources": {r: v for r, v in res.items() if r != main},
+                                "serial_frac": round((to + tb) / avg_s, 4),
+                                "f64_equiv_tflops": round(uf[k] * per_launch / avg_s / 1e12, 1),
+                                "op_note": "int8 x int8 -> int32 ops of the 8 digit planes x the 2x2 real expansion "
+                                           "(exact: the codebook is a phase code); f64_equiv_tflops counts the same "
+                                           "product as 8 flops per complex MAC; apply_AH also streams Z in and Z' out "
+                                           "(the steady-state Z-step pass fused into its epilogue)"})
+                    return out
                 if k in uf:   # MFMA-bound complex f64 GEMM
                     per = uf[k] * per_launch
                     # algorithmic = conventional 8 flops per complex MAC; the 3M kernel executes 6

@@ -43,7 +43,10 @@ namespace {
 #ifdef ACE_PHASE_STAMPS
 #define STAMP_DECL unsigned long long ts_[12] = {}
 #define STAMP(i) do { if (blockIdx.x == 5 && threadIdx.x == 0) ts_[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define STAMP_PRINT(name, k) do { if (blockIdx.x == 5 && threadIdx.x == 0) { printf("%s", name); for (int i_ = 1; i_ < k; ++i_) printf(" %llu", ts_[i_] - ts_[i_ - 1]); printf("\n"); } } while (0)
+#define STAMP_D(i) (i < k_ ? ts_[i] - ts_[i - 1] : 0ull)
+#define STAMP_PRINT(name, k) do { if (blockIdx.x == 5 && threadIdx.x == 0) { const int k_ = (k); \
+    printf("%s %llu %llu %llu %llu %llu %llu %llu\n", name, STAMP_D(1), STAMP_D(2), STAMP_D(3), STAMP_D(4), \
+           STAMP_D(5), STAMP_D(6), STAMP_D(7)); } } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i)
@@ -645,6 +648,22 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB;
     STAMP_DECL;
     STAMP(0);
+    // The inputs of T = (Y - M/mu) - AX (the steady state: every realisation has avok) are requested
+    // before the realisations' state, so the two round trips overlap (unconditional, clamped
+    // addresses; mp <= 256 gives at most 8 elements per thread)
+    constexpr int TU = 8;
+    d2 tyv[TU], tmv[TU], txv[TU];
+    const bool early = a.LA && a.AX;
+    if (early) {
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+            const int idx = min(t + NT * u, GRB * mp - 1), jl = idx / mp, k = min(idx - jl * mp, m - 1);
+            const long long o = (long long)min(j0 + jl, nb - 1) * m + k;
+            tyv[u] = reinterpret_cast<const d2*>(a.Yo)[o];
+            tmv[u] = reinterpret_cast<const d2*>(a.M)[o];
+            txv[u] = reinterpret_cast<const d2*>(a.AX)[o];
+        }
+    }
     if (t < GRB) {
         const int j = j0 + t;
         const bool lv = j < nb && !a.rs[j].done;
@@ -656,6 +675,23 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         pend_s[t] = lv && a.lazy && a.rs[j].dpend;
     }
     __syncthreads();
+    // T of the avok realisations from the early loads (a block that needs apply_A or finishes a
+    // pending test rewrites Ts below)
+    auto t_from = [&](const d2 (&yv)[TU], const d2 (&mv)[TU], const d2 (&xv)[TU]) {
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+            const int idx = t + NT * u;
+            if (idx >= GRB * mp) continue;
+            const int jl = idx / mp, k = idx - jl * mp;
+            d2 v = make_double2(0.0, 0.0);
+            if (live_s[jl] && avok_s[jl] && k < m) {
+                const double im = imu0_s[jl];
+                v = make_double2(fma(-mv[u].x, im, yv[u].x) - xv[u].x, fma(-mv[u].y, im, yv[u].y) - xv[u].y);
+            }
+            Ts[jl * tst + k] = v;
+        }
+    };
+    if (early) t_from(tyv, tmv, txv);
     const int nksK = i8_nks_dev(m), rst = 32 * nksK + 16;
     // ---- lazy dual residual: the previous Z-step left some convergence tests pending (the primal
     // part held, the combined part failed: inferLowRankV4_multi.m:372 needs res_dual).  They are
@@ -771,6 +807,17 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             imu0_s[t] = 1.0 / mu_s[t];
         }
         __syncthreads();
+        if (early) {   // Ts was scratch here, and mu may have changed: T again (rare)
+#pragma unroll
+            for (int u = 0; u < TU; ++u) {
+                const int idx = min(t + NT * u, GRB * mp - 1), jl = idx / mp, k = min(idx - jl * mp, m - 1);
+                const long long o = (long long)min(j0 + jl, nb - 1) * m + k;
+                tyv[u] = reinterpret_cast<const d2*>(a.Yo)[o];
+                tmv[u] = reinterpret_cast<const d2*>(a.M)[o];
+                txv[u] = reinterpret_cast<const d2*>(a.AX)[o];
+            }
+            t_from(tyv, tmv, txv);
+        }
     }
     // deferred opt_Y (RealState::optysrc): the best Y_new still lives in the buffer this iteration's
     // Y-step is about to overwrite -- save it first (rare: no better iterate in the last iteration)
@@ -792,6 +839,8 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         i8a_block<true>(nb, a.n, m, i8_nks_dev(a.n), reinterpret_cast<const i4v*>(a.LA), a.Z, a.N, a.Yo, a.M,
                         reinterpret_cast<double*>(Ts), 2 * tst, a.c8, a.rs, a.zeros, a.AX,
                         reinterpret_cast<int8_t(*)[ROWS * RSA]>(Ad), sc_s, p2_s, live_s, avok_s, j0, 0);
+    } else if (early) {
+        // T formed from the early loads above
     } else
     for (int idx = t; idx < GRB * mp; idx += NT) {
         const int jl = idx / mp, k = idx - jl * mp, j = j0 + jl;
@@ -1003,7 +1052,11 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
         if (!a.yn_id && live_s[jl] && imp_s[jl])
             reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
     }
-    if (a.lazy) return;   // no K Y: the Z-step forms the dual terms when the test needs them
+    if (a.lazy) {   // no K Y: the Z-step forms the dual terms when the test needs them
+        STAMP(5);
+        STAMP_PRINT("gyk-lazy T|GT|Ystep+shfl|red+RS|optY:", 6);
+        return;
+    }
 #ifdef ACE_GYK_PROBE_P3
     return;
 #endif

@@ -185,6 +185,7 @@ struct ZArgs;
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st, const ZArgs* fuse = nullptr);
 size_t i8ah_lds_bytes(int kc);
+size_t i8ah_fuse_lds_bytes();
 // Fused g = G T (3M f64 MFMA), Y-step, K Y (int8 digit planes), dual terms and opt_Y for
 // 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
 // fragment order (launch_gyk_gfrag at setup).

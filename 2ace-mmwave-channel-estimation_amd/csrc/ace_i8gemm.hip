@@ -313,7 +313,10 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     __shared__ double sc_s[RB];
     __shared__ int live_s[RB];
     __shared__ FuseState fs_s[FUSE ? RB : 1];
-    __shared__ double fred[FUSE ? 8 : 1][RB][2];
+    // FUSE: per-lane partial sums ||X||^2, ||X - Z||^2 of each (wave, realisation pair slot), one
+    // slot per lane accumulated over the column blocks (no shuffles in the epilogue): after the
+    // digit planes in the dynamic LDS, [8 waves][8 (R, q)][2][64 lanes] doubles = 64 KiB
+    double* zsum = reinterpret_cast<double*>(Ad + ((ROWS * (32 * nks + 16) + 255) & ~255));
     const int rst = 32 * nks + 16;   // LDS row stride (bytes)
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -335,9 +338,6 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
                 f.optsrc = r.optsrc;
             }
             fs_s[t] = f;
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-                for (int q = 0; q < 8; ++q) fred[q][t][k] = 0.0;
         }
     }
     const d2* g = reinterpret_cast<const d2*>(Gp) + (long long)jb * Kc;
@@ -487,16 +487,10 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
                             }
                         }
                     }
-                    if (el) {   // half-wave reduction, then this wave's slot (fixed order over blocks)
-#pragma unroll
-                        for (int o = 1; o < 32; o <<= 1) {
-                            p0 += __shfl_xor(p0, o, 64);
-                            p3 += __shfl_xor(p3, o, 64);
-                        }
-                        if ((lane & 31) == 0) {
-                            fred[w][blo][0] += p0;
-                            fred[w][blo][1] += p3;
-                        }
+                    if (el) {   // this lane's slots (fixed order over the blocks)
+                        double* zs = zsum + ((w * 8 + 2 * R + q) * 2) * 64 + lane;
+                        zs[0] = cbk == 0 ? p0 : zs[0] + p0;
+                        zs[64] = cbk == 0 ? p3 : zs[64] + p3;
                     }
                 }
         } else {
@@ -571,16 +565,26 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     if (!KY && !FUSE) STAMP_PRINT("i8ah prologue|sweep:", 3);
     if constexpr (FUSE) {
         __syncthreads();
-        if (t < RB && fs_s[t].el && live_s[t]) {
+        {   // half-wave t >> 5 = realisation blo: its 8 waves x 32 lanes of slots, fixed order
+            const int blo = t >> 5, sub = t & 31, R = blo >> 2, q = (blo >> 1) & 1, hh = blo & 1;
             double s0 = 0.0, s3 = 0.0;
-            for (int q = 0; q < 8; ++q) {   // fixed order over the waves
-                s0 += fred[q][t][0];
-                s3 += fred[q][t][1];
+            if (fs_s[blo].el && live_s[blo])
+                for (int ww = 0; ww < 8; ++ww) {
+                    const double* zs = zsum + ((ww * 8 + 2 * R + q) * 2) * 64 + 32 * hh + sub;
+                    s0 += zs[0];
+                    s3 += zs[64];
+                }
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                s0 += __shfl_xor(s0, o, 64);
+                s3 += __shfl_xor(s3, o, 64);
             }
-            RealState* st = za.st + j0 + t;
-            st->fs0 = s0;   // ||E||^2 = ||X||^2
-            st->fs3 = s3;   // ||E - E_prev||^2 = ||X - Z||^2
-            st->fzit = za.it;
+            if (sub == 0 && fs_s[blo].el && live_s[blo]) {
+                RealState* st = za.st + j0 + blo;
+                st->fs0 = s0;   // ||E||^2 = ||X||^2
+                st->fs3 = s3;   // ||E - E_prev||^2 = ||X - Z||^2
+                st->fzit = za.it;
+            }
         }
         STAMP(3);
         STAMP_PRINT("i8ah-fused prologue|sweep|post:", 4);
@@ -1231,7 +1235,8 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
                        i8_nks(n), LH, i8_nks(m), flag);
 }
 
-size_t i8ah_lds_bytes(int kc) { return (size_t)ROWS * (32 * i8_nks(kc) + 16); }
+size_t i8ah_lds_bytes(int kc) { return ((size_t)ROWS * (32 * i8_nks(kc) + 16) + 255) & ~(size_t)255; }
+size_t i8ah_fuse_lds_bytes() { return (size_t)8 * 8 * 2 * 64 * sizeof(double); }   // FUSE partial-sum slots
 
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
@@ -1291,7 +1296,8 @@ void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g
     (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
     if (fuse)
-        hipLaunchKernelGGL((i8ah_kernel<false, true>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+        hipLaunchKernelGGL((i8ah_kernel<false, true>), grid, block, i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes(), st, nb,
+                           m, n, i8_nks(m),
                            reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, *fuse);
     else
         hipLaunchKernelGGL((i8ah_kernel<false, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),

@@ -57,6 +57,18 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->allow_i8 = true;
 }
 
+// From this iteration on the Z-step launches in its compact form (zstep1w_compact_kernel): the
+// cold start (eigendecompositions, exact certificates) is over by then in the benchmark solves;
+// a later fallback is still handled, one per wave and realisation group.  ACE_ZCOMPACT=<it>
+// (0 = never).
+static int zcompact_after() {
+    static const int v = [] {
+        const char* e = getenv("ACE_ZCOMPACT");
+        return e ? atoi(e) : 40;
+    }();
+    return v;
+}
+
 // ACE_FUSE=0 runs the lean Z-step as its own launch instead of in apply_AH's epilogue.
 static bool fuse_enabled() {
     const char* e = getenv("ACE_FUSE");
@@ -323,6 +335,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.fixup_now = it == p.maxiter;
             za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
             za.lean = lean;
+            za.compact = lean && zcompact_after() > 0 && it > zcompact_after();
             // the steady-state Z-step in apply_AH's epilogue (not at the last iteration, whose
             // pending convergence tests the one-wave kernels finish)
             za.xfuse = lean && it != p.maxiter && fuse_enabled();
@@ -523,6 +536,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.KYold = w.KY[q];
         za.lean = wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled();
         za.fixup_now = it == p.maxiter;
+        za.compact = za.lean && zcompact_after() > 0 && it > zcompact_after();
         {
             ProfScope ps(ACE_K_ZSTEP, st);
             if (za.lean && !za.xfuse) launch_zlean(za, batch, st);

@@ -319,6 +319,7 @@ struct ZArgs {
     const double* Kf;
     int fixup_now;   // last iteration: finish a pending test here (dual_fixup), no later gyk_kernel
     int xfuse;       // the fused apply_AH ran: realisations with st->fzit == it have X in Zn and their sums
+    int compact;     // steady state: zstep1w_compact_kernel (one wave per 8 realisations)
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

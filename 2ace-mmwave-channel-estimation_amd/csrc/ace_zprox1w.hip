@@ -56,6 +56,35 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
     }
 }
 
+// Certificate and iteration control of a realisation whose X the fused apply_AH formed in Z'
+// with its sums (RealState::fzit, fs0 = ||X||^2, fs3 = ||X - Z||^2), on one lane: the
+// perturbation bound of zlean_kernel; if it holds, Z' = E = X stands, N' = 0, and the control
+// runs.  Returns 0 (nothing written) when the bound fails: the full Z-step must run.
+__device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
+    RealState s = *st;   // one batch of loads (the chain below then runs on registers)
+    const double s0 = s.fs0, s3 = s.fs3;
+    const double cum = (s.kfcum + sqrt(s3)) * (1.0 + 0x1p-40);
+    bool pass = s0 > 0.0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        if (p >= pf.np) break;
+        const double lb = s.kf[p] * (1.0 - 1e-12) - cum;
+        pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
+    }
+    if (!pass) return 0;
+    const bool improved_pre = sqrt(s.obj2) < s.opt_obj;
+    const int optsrc = s.optsrc;   // (the fused kernel kept a best iterate in Z')
+    iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY);
+    s.vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
+    s.nzero = 1;
+    s.avok = 1;
+    s.optsrc = improved_pre ? 1 + (a.it & 1) : optsrc;   // deferred opt_X: X = Z' bit for bit
+    s.kfcum = cum;
+    s.zit = a.it;
+    *st = s;
+    return 1;
+}
+
 template <bool INIT>
 __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const int lane = threadIdx.x;
@@ -70,29 +99,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const bool xin = !INIT && a.xfuse && st->fzit == a.it;
     if (xin) {
         int ok = 0;
-        if (threadIdx.x == 0) {
-            const double s0 = st->fs0, s3 = st->fs3;
-            const double cum = (st->kfcum + sqrt(s3)) * (1.0 + 0x1p-40);
-            bool pass = s0 > 0.0;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                if (p >= pf.np) break;
-                const double lb = st->kf[p] * (1.0 - 1e-12) - cum;
-                pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
-            }
-            if (pass) {
-                const bool improved_pre = sqrt(st->obj2) < st->opt_obj;
-                const int optsrc = st->optsrc;   // (the fused kernel kept a best iterate in Z')
-                iter_control(a, st, st->mu, s0, s0, 0.0, s3, st->dAtY, st->nAtY);
-                st->vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
-                st->nzero = 1;
-                st->avok = 1;
-                st->optsrc = improved_pre ? 1 + (a.it & 1) : optsrc;   // deferred opt_X: X = Z' bit for bit
-                st->kfcum = cum;
-                st->zit = a.it;
-                ok = 1;
-            }
-        }
+        if (threadIdx.x == 0) ok = fused_control(a, st, pf);
         if (__shfl(ok, 0, 64)) return;
     }
     __shared__ __attribute__((aligned(16))) d2 T0[ZT * ZHS];
@@ -847,6 +854,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     zstep1w_body<INIT>(a, blockIdx.x);
 }
 
+// Steady-state form (ZArgs::compact): one wave per ZC realisations.  Lane i settles realisation
+// b0 + i when the lean kernel or the fused apply_AH left it certifiable (the control runs on the
+// lanes in parallel); the wave then runs the full one-wave Z-step for the others, one after
+// another.  A launch of nb / ZC waves instead of nb: in the steady state every realisation is
+// settled on its lane, and a fallback (rare after the cold start) costs a sequential step.
+constexpr int ZC = 8;
+__device__ __noinline__ void zstep1w_body_call(const ZArgs& a, int b) { zstep1w_body<false>(a, b); }
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zstep1w_compact_kernel(ZArgs a, int nb) {
+    const int lane = threadIdx.x, b0 = blockIdx.x * ZC;
+    int full = 0;
+    if (lane < ZC && b0 + lane < nb) {
+        const int b = b0 + lane;
+        RealState* st = a.st + b;
+        if (!st->done && !(a.lean && st->zit == a.it)) {
+            full = 1;
+            if (a.xfuse && st->fzit == a.it) full = !fused_control(a, st, z_profile(a, b));
+        }
+    }
+    unsigned long long m = __ballot(full);
+    while (m) {
+        const int i = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        zstep1w_body_call(a, b0 + i);   // (re-checks the fused bound: it fails again, X from Z')
+        __syncthreads();
+    }
+}
+
 // ---- lean steady-state Z-step (A2only, wmode, ping-pong, N = 0 on entry).
 // In the steady state of the unit solve N = 0, so E = X = Z + W and the reference's Z-prox
 // leaves Z = E unless its tail rescaling fires (:469-484).  The full kernel above proves that
@@ -990,6 +1024,7 @@ void launch_zlean(const ZArgs& a, int batch, hipStream_t st) {
 
 void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st) {
     if (init) hipLaunchKernelGGL(zstep1w_kernel<true>, dim3(batch), dim3(64), 0, st, a);
+    else if (a.compact) hipLaunchKernelGGL(zstep1w_compact_kernel, dim3((batch + ZC - 1) / ZC), dim3(64), 0, st, a, batch);
     else hipLaunchKernelGGL(zstep1w_kernel<false>, dim3(batch), dim3(64), 0, st, a);
 }
 

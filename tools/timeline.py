@@ -4,14 +4,14 @@ import csv
 import statistics as S
 import sys
 
-KEYS = {"zstep1w_kernel<false>": "Z", "gyk_kernel": "G", "i8a_kernel": "A", "i8ah_kernel<false, false>": "H", "i8ah_kernel<false, true>": "F", "zlean_kernel": "L", "dual_fix_kernel": "D"}
+KEYS = {"zstep1w_kernel<false>": "Z", "zstep1w_compact_kernel": "C", "gyk_kernel": "G", "i8a_kernel": "A", "i8ah_kernel<false, false>": "H", "i8ah_kernel<false, true>": "F", "zlean_kernel": "L", "dual_fix_kernel": "D"}
 ev = []
 for r in csv.DictReader(open(sys.argv[1])):
     for k, c in KEYS.items():
         if k in r["Kernel_Name"]:
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), c, r["Stream_Id"]))
 ev.sort()
-for c in "AGHFZLD":
+for c in "AGHFZCLD":
     d = sorted(e - s for s, e, k, _ in ev if k == c)
     if d:
         print(f"{c} n={len(d)} median {S.median(d) / 1e3:.1f} us  p10 {d[len(d) // 10] / 1e3:.1f}  p90 {d[9 * len(d) // 10] / 1e3:.1f}")

@@ -57,14 +57,14 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->allow_i8 = true;
 }
 
-// From this iteration on the Z-step launches in its compact form (zstep1w_compact_kernel): the
-// cold start (eigendecompositions, exact certificates) is over by then in the benchmark solves;
-// a later fallback is still handled, one per wave and realisation group.  ACE_ZCOMPACT=<it>
-// (0 = never).
+// ACE_ZCOMPACT=<it>: from that iteration on the Z-step launches in its compact form
+// (zstep1w_compact_kernel: one wave per 8 realisations, the control on the lanes, fallbacks one
+// after another).  Measured neutral against one wave per realisation (r02: the launch is bound by
+// its dependent state round trips, not by the wave count), so off by default (0).
 static int zcompact_after() {
     static const int v = [] {
         const char* e = getenv("ACE_ZCOMPACT");
-        return e ? atoi(e) : 40;
+        return e ? atoi(e) : 0;
     }();
     return v;
 }

@@ -61,12 +61,9 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 // (zstep1w_compact_kernel: one wave per 8 realisations, the control on the lanes, fallbacks one
 // after another).  Measured neutral against one wave per realisation (r02: the launch is bound by
 // its dependent state round trips, not by the wave count), so off by default (0).
-static int zcompact_after() {
-    static const int v = [] {
-        const char* e = getenv("ACE_ZCOMPACT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
+static int zcompact_after() {   // (read per call: tests switch it within one process)
+    const char* e = getenv("ACE_ZCOMPACT");
+    return e ? atoi(e) : 0;
 }
 
 // ACE_FUSE=0 runs the lean Z-step as its own launch instead of in apply_AH's epilogue.

@@ -67,9 +67,14 @@ static int zcompact_after() {   // (read per call: tests switch it within one pr
 }
 
 // ACE_FUSE=0 runs the lean Z-step as its own launch instead of in apply_AH's epilogue.
-static bool fuse_enabled() {
+static bool fuse_enabled(int m) {
     const char* e = getenv("ACE_FUSE");
-    return !(e && e[0] == '0');
+    return !(e && e[0] == '0') && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192;
+}
+// ACE_GYF=0 runs gyk_kernel and the fused apply_AH as two launches instead of gyf_kernel.
+static bool gyf_enabled(int m) {
+    const char* e = getenv("ACE_GYF");
+    return !(e && e[0] == '0') && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN;
 }
 
 // ACE_LAZY_DUAL=0 keeps K Y in gyk_kernel every iteration (A/B comparisons); read per solve.
@@ -305,13 +310,6 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             double* Zc = (it & 1) ? wh.Z : wh.Z2;   // Z, N of the previous iterate (ping-pong)
             double* Nc = (it & 1) ? wh.N : wh.N2;
             ACE_HIP(stagger_mark(h, it, 1));
-            {
-                ProfScope ps(ACE_K_APPLY_G, sh);
-                const GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                                 L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc};
-                launch_gyk(nb[h], m, ga, sh);
-            }
-            ACE_HIP(stagger_mark(h, it, 2));
             ZArgs za = za0;
             za.it = it;
             za.wmode = 1;
@@ -335,8 +333,20 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.compact = lean && zcompact_after() > 0 && it > zcompact_after();
             // the steady-state Z-step in apply_AH's epilogue (not at the last iteration, whose
             // pending convergence tests the one-wave kernels finish)
-            za.xfuse = lean && it != p.maxiter && fuse_enabled();
-            {
+            za.xfuse = lean && it != p.maxiter && fuse_enabled(m);
+            // and apply_AH in the same launch as gyk (g stays on chip)
+            const bool gyf = za.xfuse && za0.lazy_dual && gyf_enabled(m);
+            GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
+                       L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0};
+            if (gyf) {
+                ProfScope ps(ACE_K_APPLY_G, sh);
+                launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, sh);
+            } else {
+                {
+                    ProfScope ps(ACE_K_APPLY_G, sh);
+                    launch_gyk(nb[h], m, ga, sh);
+                }
+                ACE_HIP(stagger_mark(h, it, 2));
                 ProfScope ps(ACE_K_APPLY_AH, sh);
                 launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh, za.xfuse ? &za : nullptr);
             }
@@ -502,7 +512,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
             if (wmode) {
                 za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled() &&
-                           it != p.maxiter && fuse_enabled();
+                           it != p.maxiter && fuse_enabled(m);
                 if (za.xfuse) {   // the fused kernel needs this iteration's Z-step arguments
                     za.it = it;
                     za.wmode = 1;

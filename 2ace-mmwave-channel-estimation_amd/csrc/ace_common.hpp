@@ -221,8 +221,12 @@ struct GykArgs {
     // (RealState::dpend) is finished at the start from K Y_k and K (Y_k - Y_{k-1}) (Yo, Yn)
     int lazy;
     DualCtl dc;
+    int glds;           // (gyf_kernel) g stays in LDS for the fused apply_AH instead of going to a.g
 };
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
+// gyk + the fused apply_AH (Z-step pass) in one launch; needs a.lazy and a.glds
+size_t gyf_lds_bytes(int m);
+void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);

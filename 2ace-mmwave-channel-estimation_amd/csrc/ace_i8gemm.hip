@@ -304,19 +304,19 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
 struct FuseState {   // per realisation, loaded in the prologue
     int el, keep_cur, optsrc;
 };
-template <bool KY, bool FUSE>
-__global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
-                                                     const double* __restrict__ Gp, double* __restrict__ Wp,
-                                                     const double* __restrict__ cptr,
-                                                     const RealState* __restrict__ rs, ZArgs za) {
-    extern __shared__ __attribute__((aligned(16))) int8_t Ad[];
+// The block body.  Ad: the digit planes (ROWS x (32 nks + 16) bytes of LDS); zsum (FUSE): the
+// per-lane partial sums ||X||^2, ||X - Z||^2 of each (wave, realisation pair slot), one slot per
+// lane accumulated over the column blocks (no shuffles in the epilogue), [8 waves][8 (R, q)][2]
+// [64 lanes] doubles = 64 KiB.  gl (GLDS): g of the block's realisations in LDS rows of gst
+// complex (the fused g / Y-step / apply_AH kernel), instead of Gp in global memory.
+template <bool KY, bool FUSE, bool GLDS>
+__device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                          const double* __restrict__ Gp, double* __restrict__ Wp,
+                                          const double* __restrict__ cptr, const RealState* __restrict__ rs,
+                                          const ZArgs& za, int8_t* Ad, double* zsum, const d2* gl, int gst) {
     __shared__ double sc_s[RB];
     __shared__ int live_s[RB];
     __shared__ FuseState fs_s[FUSE ? RB : 1];
-    // FUSE: per-lane partial sums ||X||^2, ||X - Z||^2 of each (wave, realisation pair slot), one
-    // slot per lane accumulated over the column blocks (no shuffles in the epilogue): after the
-    // digit planes in the dynamic LDS, [8 waves][8 (R, q)][2][64 lanes] doubles = 64 KiB
-    double* zsum = reinterpret_cast<double*>(Ad + ((ROWS * (32 * nks + 16) + 255) & ~255));
     const int rst = 32 * nks + 16;   // LDS row stride (bytes)
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -350,6 +350,7 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
     double mx = 0.0, sn = 0.0;   // max |g| of the realisation over this half-wave
     auto gat = [&](int s, int u) -> d2 {
         const int k = 64 * s + 2 * cp + u;
+        if constexpr (GLDS) return (live && k < Kc) ? gl[bl * gst + k] : make_double2(0.0, 0.0);
         return (live && k < Kc) ? g[k] : make_double2(0.0, 0.0);
     };
 #pragma unroll
@@ -590,6 +591,15 @@ __global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int
         STAMP_PRINT("i8ah-fused prologue|sweep|post:", 4);
     }
 }
+template <bool KY, bool FUSE>
+__global__ __launch_bounds__(NT, 1) void i8ah_kernel(int nb, int Kc, int Mc, int nks, const i4v* __restrict__ Bf,
+                                                     const double* __restrict__ Gp, double* __restrict__ Wp,
+                                                     const double* __restrict__ cptr,
+                                                     const RealState* __restrict__ rs, ZArgs za) {
+    extern __shared__ __attribute__((aligned(16))) int8_t Ad[];
+    double* zsum = reinterpret_cast<double*>(Ad + ((ROWS * (32 * nks + 16) + 255) & ~255));
+    i8ah_body<KY, FUSE, false>(nb, Kc, Mc, nks, Bf, Gp, Wp, cptr, rs, za, Ad, zsum, nullptr, 0);
+}
 
 // Codebook check and expansion.  cmax = max |component| of A (device scalar).  Each
 // complex entry A[i][k] = c (p + j q) must have p, q in {-1, 0, 1}; flag is set otherwise.
@@ -640,8 +650,8 @@ struct GSet {
     d2 f[GSK][2];
 };
 
-__global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+template <bool GLDS>   // g stays in the LDS rows of T for the fused apply_AH (gyf_kernel) instead of a.g
+__device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem) {
     __shared__ double red[8][GRB][7];
     __shared__ double sc_s[GRB], p2_s[GRB];
     __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB];
@@ -986,11 +996,12 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
             const double f = (Bi / d + mu) / (1.0 + mu);
             const d2 y = cscale(cc, f);
             const d2 jv = csub(ax, y);
-            reinterpret_cast<d2*>(a.g)[off] = gv;
+            if constexpr (!GLDS) reinterpret_cast<d2*>(a.g)[off] = gv;
             if (a.AX) reinterpret_cast<d2*>(a.AX)[off] = ax;
             reinterpret_cast<d2*>(a.M)[off] = cadd(mii, cscale(jv, mu));
             reinterpret_cast<d2*>(a.Yn)[off] = y;
-            Ts[jl * tst + i] = y;
+            if constexpr (GLDS) Ts[jl * tst + i] = gv;   // g stays on chip for the fused apply_AH
+            else Ts[jl * tst + i] = y;
             const double aax = sqrt(cabs2(ax)) - Bi;
             v7[r][0] += aax * aax;
             v7[r][1] += cabs2(ax);
@@ -1180,6 +1191,27 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     STAMP(7);
     STAMP_PRINT("gyk T|GT|Ystep+shfl|red+RS|optY+digits|KY|dual:", 8);
 }
+__global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    gyk_body<false>(nb, m, a, smem);
+}
+// One iteration's matrix work in one launch (unit path, lazy dual residual, fused Z-step pass):
+// gyk_body (T, g = G T, the Y-step; g left in the LDS rows of T), then the fused apply_AH body
+// on the same 16 realisations with its digit planes staged from LDS.  The g round trip through
+// HBM, apply_AH's g loads and one launch boundary go away.  LDS: [T / g rows | digit planes]
+// and the 64 KiB of Z-step partial sums over the T rows when they are large enough, else after.
+__host__ __device__ __forceinline__ size_t gyf_ts_bytes(int m) { return ((size_t)GRB * (gyk_mp(m) + 1) * 16 + 255) & ~(size_t)255; }
+__global__ __launch_bounds__(NT, 1) void gyf_kernel(int nb, int m, int n, GykArgs a, const i4v* __restrict__ LAH,
+                                                    double* __restrict__ Wp, ZArgs za, size_t ad_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    gyk_body<true>(nb, m, a, smem);
+    __syncthreads();
+    const size_t ts = gyf_ts_bytes(m);
+    int8_t* Ad = reinterpret_cast<int8_t*>(smem + ts);
+    double* zsum = reinterpret_cast<double*>(ts >= (size_t)8 * 8 * 2 * 64 * sizeof(double) ? smem : smem + ts + ad_bytes);
+    i8ah_body<false, true, true>(nb, m, n, i8_nks_dev(m), LAH, nullptr, Wp, a.c8, a.rs, za, Ad, zsum,
+                                 reinterpret_cast<const d2*>(smem), gyk_mp(m) + 1);
+}
 
 // G [m][m] c128 -> f64 MFMA B-operand fragments: ((ks * (mp/16) + ct) * 64 + lane) holds
 // G[16 ct + (lane & 15)][4 ks + (lane >> 4)] (zero padded to mp = m rounded up to 32).
@@ -1281,6 +1313,22 @@ void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st) {
     }();
     (void)attr;
     hipLaunchKernelGGL(gyk_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyk_lds_bytes(m), st, nb, m, a);
+}
+size_t gyf_lds_bytes(int m) {
+    const size_t ts = gyf_ts_bytes(m), ad = gyk_lds_bytes(m) - ts, zs = i8ah_fuse_lds_bytes();
+    return ts + ad + (ts >= zs ? 0 : zs);
+}
+void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, hipStream_t st) {
+    static const bool attr = [] {
+        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gyf_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, GYK_MAXDYN) == hipSuccess;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    (void)attr;
+    const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
+    hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
+                       reinterpret_cast<const i4v*>(LAH), W, za, ad);
 }
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st, const ZArgs* fuse) {

@@ -286,6 +286,12 @@ def unit_i8_ops(m, n):
     return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m), "apply_G": 0.0}
 
 
+def gyf_bytes(m, n):
+    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel (gyk + the fused apply_AH in
+    one launch, g on chip): read Y, M, AX (c128), B (f64) and Z; write AX, M, Y_new and Z' = X."""
+    return 16.0 * 6 * m + 8.0 * m + 16.0 * 2 * n
+
+
 def unit_bytes(m, n, tx, rx):
     """Algorithmic HBM bytes per realisation per iteration of the steady-state unit path
     (complex128 = 16 B, each array read or written once):
@@ -357,7 +363,7 @@ def cpu_baseline(args, n_samples, private):
 
 
 PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false, true>",
-              "apply_G": "gyk_kernel"}
+              "apply_G": "gyf_kernel"}
 
 
 PMC_KERNEL_PRIVATE = {"zstep": "zstep1w_kernel<false>", "apply_G": "pgk_kernel"}
@@ -518,6 +524,9 @@ def unit_bench(args, private, dev, rank, world):
             per_launch = -(-bsz // nsplit)
 
             gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
+            # with concurrent sub-batches apply_G is gyf_kernel: gyk and the fused apply_AH in one launch
+            env_on = lambda k: os.environ.get(k) != "0"
+            gyf = gyk and nsplit > 1 and all(env_on(k) for k in ("ACE_GYF", "ACE_FUSE", "ACE_LAZY_DUAL", "ACE_LEAN"))
             # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
             pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
 
@@ -538,6 +547,30 @@ def unit_bench(args, private, dev, rank, world):
                                         "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "flops_per_launch": f}},
                             "bytes_note": "per realisation: G_b lower triangle (c128) + A_b^H as 2-bit codes + "
                                           "Y, M, AX, B in and AX, M, Y out + W = A^H g out (bench.private_bytes)"}
+                if k == "apply_G" and gyf:   # f64 G T, int8 A^H g, HBM (T, Y-step, Z pass), phase after phase
+                    f, o, b = uf[k] * per_launch, io["apply_AH"] * per_launch, gyf_bytes(m, n) * per_launch
+                    tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
+                    res = {
+                        "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
+                                "flops_per_launch": f},
+                        "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
+                                 "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
+                                 "ops_per_launch": o},
+                        "hbm": {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
+                    }
+                    main = max((("f64", tf), ("int8", to), ("hbm", tb)), key=lambda x: x[1])[0]
+                    out = dict(res[main])
+                    out.update({"traffic": None, "kernel": "apply_G (gyf_kernel)", "resource": main,
+                                "other_resources": {r: v for r, v in res.items() if r != main},
+                                "serial_frac": round((tf + to + tb) / avg_s, 4),
+                                "flop_note": "gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per "
+                                             "complex MAC), the Y-step, then W = A^H g (int8 digit planes) with the "
+                                             "certified Z-step pass (Z in, Z' out) in its epilogue, one phase after "
+                                             "another in each work-group; bound = the resource with the largest time "
+                                             "at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"})
+                    return out
                 if k == "apply_G" and gyk:   # f64 G T + the Y-step's HBM traffic, phase after phase
                     f, b = uf[k] * per_launch, ub[k] * per_launch
                     tf, tb = f / (PEAK_FP64_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)

@@ -26,6 +26,13 @@ def test_unit_bytes_match_design():
     assert ub["apply_AH"] == 16 * (m + 2 * n)
 
 
+def test_gyf_bytes():
+    b = _bench()
+    m, n = 256, 1024
+    # gyk + fused apply_AH in one launch: read Y, M, AX, B, Z; write AX, M, Y, Z' (g stays on chip)
+    assert b.gyf_bytes(m, n) == 16 * 6 * m + 8 * m + 32 * n == 58 * 1024
+
+
 def test_int8_ops_and_flops():
     b = _bench()
     io = b.unit_i8_ops(256, 1024)

@@ -233,7 +233,7 @@ void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, i
 void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
                        const RealState* rs, hipStream_t st);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
-void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st);
+void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st, double* bnd);
 // out[0] = max |x_i| over n doubles
 void launch_max_abs(long long n, const double* x, double* out, hipStream_t st);
 

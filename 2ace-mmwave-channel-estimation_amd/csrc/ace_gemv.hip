@@ -9,6 +9,8 @@
 // A never needs a transposed copy.
 #include "ace_common.hpp"
 
+#include <algorithm>
+
 namespace ace {
 
 namespace {
@@ -141,56 +143,62 @@ __global__ __launch_bounds__(1024) void inv_ipk_kernel(int m, double* __restrict
         __syncthreads();
     }
 }
-__global__ __launch_bounds__(1024) void ns_prep_kernel(int m, const d2* __restrict__ K, d2* __restrict__ Ap,
-                                                       d2* __restrict__ Id, d2* __restrict__ X0) {
-    __shared__ double part[1024];
-    double b = 0.0;
-    for (int i = threadIdx.x; i < m; i += blockDim.x) {  // Gershgorin row sums of I + K
-        double rs = 0.0;
-        for (int j = 0; j < m; ++j) {
-            d2 v = K[(long long)i * m + j];
-            if (i == j) v.x += 1.0;
-            rs += sqrt(v.x * v.x + v.y * v.y);
-        }
-        b = fmax(b, rs);
-    }
-    part[threadIdx.x] = b;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) part[threadIdx.x] = fmax(part[threadIdx.x], part[threadIdx.x + s]);
-        __syncthreads();
-    }
-    const double alpha = 2.0 / (1.0 + part[0]);
-    for (long long e = threadIdx.x; e < (long long)m * m; e += blockDim.x) {
-        const bool diag = (e / m) == (e % m);
-        d2 v = K[e];
-        if (diag) v.x += 1.0;
-        Ap[e] = v;
-        Id[e] = make_double2(diag ? 1.0 : 0.0, 0.0);
-        X0[e] = make_double2(diag ? alpha : 0.0, 0.0);
-    }
-}
-
-__global__ __launch_bounds__(1024) void max_abs_kernel(long long n, const double* __restrict__ x, double* out) {
-    __shared__ double part[1024];
+// max |x_i| over the grid: per-block maxima combined with a 64-bit atomic max on the bit patterns
+// (for non-negative doubles the unsigned order of the patterns is the numeric order); *out must be
+// zeroed first (launch_max_abs does it).  NaNs are dropped (fmax), as before.
+__global__ __launch_bounds__(256) void max_abs_kernel(long long n, const double* __restrict__ x, double* out) {
+    __shared__ double part[256];
     double v = 0.0;
-    for (long long i = threadIdx.x; i < n; i += blockDim.x) v = fmax(v, fabs(x[i]));
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += 256LL * gridDim.x) v = fmax(v, fabs(x[i]));
     part[threadIdx.x] = v;
     __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) part[threadIdx.x] = fmax(part[threadIdx.x], part[threadIdx.x + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[0] = part[0];
+    if (threadIdx.x == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(part[0]));
+}
+// Newton-Schulz start for the HPD matrix I + K, one row per block: Ap = I + K, Id = I, and the
+// Gershgorin bound b = max_i sum_j |(I + K)_ij| into *bnd (atomic max; zeroed first).
+__global__ __launch_bounds__(256) void ns_rows_kernel(int m, const d2* __restrict__ K, d2* __restrict__ Ap,
+                                                      d2* __restrict__ Id, double* bnd) {
+    __shared__ double part[256];
+    const int i = blockIdx.x;
+    double rs = 0.0;
+    for (int j = threadIdx.x; j < m; j += 256) {
+        d2 v = K[(long long)i * m + j];
+        if (i == j) v.x += 1.0;
+        rs += sqrt(v.x * v.x + v.y * v.y);
+        Ap[(long long)i * m + j] = v;
+        Id[(long long)i * m + j] = make_double2(i == j ? 1.0 : 0.0, 0.0);
+    }
+    part[threadIdx.x] = rs;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned long long*>(bnd), (unsigned long long)__double_as_longlong(part[0]));
+}
+__global__ __launch_bounds__(256) void ns_x0_kernel(int m, const double* __restrict__ bnd, d2* __restrict__ X0) {
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= (long long)m * m) return;
+    const double alpha = 2.0 / (1.0 + *bnd);
+    X0[e] = make_double2((e / m) == (e % m) ? alpha : 0.0, 0.0);
 }
 }  // namespace
 
-void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st) {
-    hipLaunchKernelGGL(ns_prep_kernel, dim3(1), dim3(1024), 0, st, m, (const d2*)K, (d2*)Ap, (d2*)Id, (d2*)X0);
+void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st, double* bnd) {
+    (void)hipMemsetAsync(bnd, 0, sizeof(double), st);
+    hipLaunchKernelGGL(ns_rows_kernel, dim3(m), dim3(256), 0, st, m, (const d2*)K, (d2*)Ap, (d2*)Id, bnd);
+    hipLaunchKernelGGL(ns_x0_kernel, dim3((unsigned)(((long long)m * m + 255) / 256)), dim3(256), 0, st, m, bnd, (d2*)X0);
 }
 
 void launch_max_abs(long long n, const double* x, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(max_abs_kernel, dim3(1), dim3(1024), 0, st, n, x, out);
+    (void)hipMemsetAsync(out, 0, sizeof(double), st);
+    const long long blocks = std::min<long long>(1024, (n + 2047) / 2048);
+    hipLaunchKernelGGL(max_abs_kernel, dim3((unsigned)std::max<long long>(1, blocks)), dim3(256), 0, st, n, x, out);
 }
 
 void launch_zgemv_rows(int mode, int M, int K, int nb, const double* L, long long strideL, const double* V,

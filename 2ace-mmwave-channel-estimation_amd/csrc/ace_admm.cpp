@@ -269,8 +269,11 @@ static int split_count(int batch) {
     return k;
 }
 
-// AdmmState of realisations [ob, ob + ...) of w (r = 1 layout)
-static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n) {
+// AdmmState of realisations [ob, ob + ...) of w (r = 1 layout).  Q is indexed by the Z-step
+// kernels with a stride of tx * tx complex per realisation (not the allocation's 32 x 32): the
+// warm-start basis must be the one the init Z-step wrote for the same realisation, since the
+// perturbation certificate pairs it with that realisation's RealState::kf.
+static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n, int tx) {
     AdmmState h = w;
     const long long on = 2 * ob * n, om = 2 * ob * m;
     h.X = w.X + on;
@@ -281,7 +284,7 @@ static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n) {
     h.AX = w.AX + om;
     h.V = w.V + on;
     h.optX = w.optX + on;
-    h.Q = w.Q + 2 * ob * 32 * 32;
+    h.Q = w.Q + 2 * ob * tx * tx;
     for (int i = 0; i < 2; ++i) {
         h.Y[i] = w.Y[i] + om;
         h.KY[i] = w.KY[i] + om;
@@ -337,7 +340,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     for (int h = 0; h < nsplit; ++h) {
         const long long ob = (long long)h * chunk;
         nb[h] = (int)std::max(0LL, std::min((long long)chunk, batch - ob));
-        ws[h] = state_slice(w, ob, m, n);
+        ws[h] = state_slice(w, ob, m, n, za0.tx);
     }
     // Stagger: sub-batch h >= 1 starts its first iteration once sub-batch 0 has issued `stg`
     // kernels of it, so that the sub-batches run different kernels (HBM- vs matrix-core-bound)

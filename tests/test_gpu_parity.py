@@ -337,3 +337,25 @@ def test_compact_zstep_bit_identical(gpu, monkeypatch, fixed):
         out[zc] = (r.X.cpu().numpy(), r.iters.cpu().numpy(), r.status.cpu().numpy())
     for a, b in zip(out["0"], out["3"]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("batch,m,tx", [(1000, 256, 32), (1024, 121, 16), (1040, 243, 32)])
+def test_gyf_ragged_batches_and_sizes(gpu, batch, m, tx):
+    """gyf_kernel (gyk + fused apply_AH, concurrent sub-batches) on ragged sub-batches (not a
+    multiple of the 16-realisation work-group), m not a multiple of the tiles (the T rows then too
+    small to hold the Z-step's partial sums), 16 antennas: a sample matches the oracle and its own
+    result in a small batch (batch invariance)."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(53, 0, batch, m, tx, tx)
+    r = infer_admm_batch(A, B, X0, tx, tx, maxiter=200, fixed_iters=True)
+    torch.cuda.synchronize()
+    X = r.X.cpu().numpy()
+    idx = [0, batch // 2 + 7, batch - 1]
+    Ah, Bh, X0h = A.cpu().numpy(), B.cpu().numpy()[idx], X0.cpu().numpy()[idx]
+    Xo, _, _, _, _ = _oracle(Ah, Bh, X0h, tx, variant=0, maxiter=200, fixed_iters=True)
+    assert _errs(X[idx], Xo).max() <= TOL
+    small = infer_admm_batch(A, B[batch - 16:].contiguous(), X0[batch - 16:].contiguous(), tx, tx, maxiter=200,
+                             fixed_iters=True)
+    torch.cuda.synchronize()
+    assert _errs(small.X.cpu().numpy(), X[batch - 16:]).max() <= 1e-12

@@ -79,6 +79,19 @@ static bool gyf_enabled(int m) {
     return !(e && e[0] == '0') && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN;
 }
 
+// ACE_MSPACE=0 keeps Z in memory through the steady state (no m-space steps, RealState::msp).
+static bool mspace_enabled() {
+    const char* e = getenv("ACE_MSPACE");
+    return !(e && e[0] == '0');
+}
+
+// ACE_MSP_FAIL_IT=<it> (tests): the perturbation bound of every m-space iterate fails at that
+// iteration, so the Z-step materialises Z, Z' and opt_X from the implicit form.
+static int msp_fail_it() {
+    const char* e = getenv("ACE_MSP_FAIL_IT");
+    return e ? atoi(e) : -1;
+}
+
 // ACE_LAZY_DUAL=0 keeps K Y in gyk_kernel every iteration (A/B comparisons); read per solve.
 static bool lazy_dual_enabled() {
     const char* e = getenv("ACE_LAZY_DUAL");
@@ -253,6 +266,8 @@ void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s) 
     s->st = cv.take<RealState>(sizeof(RealState) * (size_t)batch);
     s->done = cv.take<int>(256);
     s->zeros = cv.take(16 * (size_t)n);
+    for (int i = 0; i < 2; ++i) s->Sg[i] = cv.take(cz * bm);
+    s->optS = cv.take(cz * bm);
 }
 
 // ---- the unit path split into independent sub-batches on concurrent streams.  Each of the four
@@ -294,6 +309,9 @@ static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n, int
     h.T = w.T + om;
     h.g = w.g + om;
     h.optY = w.optY + om;
+    h.Sg[0] = w.Sg[0] + om;
+    h.Sg[1] = w.Sg[1] + om;
+    h.optS = w.optS + om;
     h.st = w.st + ob;
     return h;
 }
@@ -356,6 +374,8 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     };
     // steady-state Z-steps under the perturbation certificate (zlean_kernel), A2only only
     const bool lean = p.variant != ACE_VARIANT_NUCLEAR && za0.warm && za0.Q && zlean_enabled();
+    // m-space steady state (RealState::msp): needs the fused gyf iteration at every iteration
+    const bool msp = lean && za0.lazy_dual && fuse_enabled(m) && gyf_enabled(m) && mspace_enabled();
     const DualCtl dc{za0.tol_abs, za0.tol_rel, za0.rho, za0.fixed_iters, n, 1, w.done};
     int q = 0, rc = ACE_OK;
     for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
@@ -388,14 +408,23 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.fixup_now = it == p.maxiter;
             za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
             za.lean = lean;
-            za.compact = lean && zcompact_after() > 0 && it > zcompact_after();
+            za.compact = lean && zcompact_after() > 0 && it > zcompact_after() && it != p.maxiter;
             // the steady-state Z-step in apply_AH's epilogue (not at the last iteration, whose
-            // pending convergence tests the one-wave kernels finish)
-            za.xfuse = lean && it != p.maxiter && fuse_enabled(m);
+            // pending convergence tests the one-wave kernels finish, unless m-space steps are on:
+            // their realisations have no Z in memory, and the fused control runs dual_fixup)
+            za.xfuse = lean && (it != p.maxiter || msp) && fuse_enabled(m);
+            za.msp = msp;
+            za.Af = L.A;
+            za.Sold = wh.Sg[(it + 1) & 1];
+            za.Snew = wh.Sg[it & 1];
+            za.optS = wh.optS;
+            za.msp_fail_it = msp_fail_it();
             // and apply_AH in the same launch as gyk (g stays on chip)
             const bool gyf = za.xfuse && za0.lazy_dual && gyf_enabled(m);
             GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
-                       L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0};
+                       L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0,
+                       gyf && msp ? 1 : 0, it, za.Sold, wh.Sg[it & 1], wh.optS, za0.np,
+                       {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one};
             if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, sh);
@@ -430,6 +459,8 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     ACE_HIP(hipGetLastError());
     {
         ProfScope ps(ACE_K_FINAL, st);
+        // best iterates still in m-space form (RealState::optsrc 3): opt_X = Z0 + A^H opt_S
+        if (msp) launch_i8_msp_optx(batch, m, n, L.LAH8, w.optS, w.optX, L.c8, w.st, w.Z, w.Z2, st);
         launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st, w.Z,
                           w.Z2, w.Y[0], w.Y[1]);
     }
@@ -518,7 +549,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     int q = 0;
     const int poll = 8;
     const int nsplit = gyk ? split_count(batch) : 1;
-    if (nsplit > 1) return admm_iterate_split(L, p, w, za, batch, B, nsplit, Xo, Yo, iters, status, mu_out, st);
+    if (nsplit > 1 || (gyk && mspace_enabled() && p.variant != ACE_VARIANT_NUCLEAR)) return admm_iterate_split(L, p, w, za, batch, B, nsplit, Xo, Yo, iters, status, mu_out, st);
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {

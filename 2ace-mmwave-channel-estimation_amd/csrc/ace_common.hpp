@@ -65,6 +65,15 @@ struct RealState {
     // and left ||X||^2 and ||X - Z||^2 for zstep1w_kernel's certificate and iteration control
     int32_t fzit;
     double fs0, fs3;
+    // m-space steady state (GykArgs::msp, ace_i8gemm.hip::gyk_body): from iteration it0 on, a
+    // certified realisation keeps Z implicit as Z = Z0 + A^H S with S = sum of its g since it0 (Z0
+    // the Z buffer z0id = 1 (Z) / 2 (Z2) as it stood at it0).  With N = 0 the fused pass's sums follow
+    // from m-space quantities: ||X - Z||^2 = ||A^H g||^2 = g^H K g = Re g^H (T - g) ((I + K) g = T),
+    // ||X||^2 = ||Z||^2 + 2 Re (A Z)^H g + ||A^H g||^2 (A Z = A V, the T input), so apply_AH and the
+    // Z / Z' traffic drop out of the iteration.  mzit: the iteration gyk_kernel settled that way;
+    // msp: the implicit form is live (cleared when the Z-step materialises Z for a full step).
+    // optsrc = 3: opt_X = Z0 + A^H opt_S.
+    int32_t msp, mzit, z0id, msp_pad;   // msp_pad: the entry iteration it0
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -183,9 +192,14 @@ void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, 
 // fuse != nullptr: the steady-state Z-step runs in the epilogue (i8ah_kernel<false, true>)
 struct ZArgs;
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
-                        const RealState* rs, hipStream_t st, const ZArgs* fuse = nullptr);
+                        const RealState* rs, hipStream_t st, const ZArgs* fuse = nullptr,
+                        const ZArgs* plain = nullptr);
 size_t i8ah_lds_bytes(int kc);
 size_t i8ah_fuse_lds_bytes();
+// opt_X = Z0 + A^H opt_S for the realisations whose best iterate is in m-space form (optsrc 3;
+// Z0 in Zb1 / Zb2 by RealState::z0id), done or not; sets optsrc = 0
+void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* optS, double* optX, const double* cmax,
+                        RealState* rs, const double* Zb1, const double* Zb2, hipStream_t st);
 // Fused g = G T (3M f64 MFMA), Y-step, K Y (int8 digit planes), dual terms and opt_Y for
 // 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
 // fragment order (launch_gyk_gfrag at setup).
@@ -222,7 +236,20 @@ struct GykArgs {
     int lazy;
     DualCtl dc;
     int glds;           // (gyf_kernel) g stays in LDS for the fused apply_AH instead of going to a.g
+    // m-space steady state (RealState::msp; needs lazy and glds): S' = S + g into Snew (S from Sold,
+    // the ping-pong partner), opt_S = S' when the iterate improves, the fused sums into RealState
+    int msp;
+    int it;
+    const double* Sold;
+    double* Snew;
+    double* optS;
+    // the Z-step's rank profile (z_profile): a realisation enters the m-space form only while the
+    // perturbation bound has room for GYK_MSP_ROOM more steps of the current size
+    int np;
+    double fl[4];
+    const unsigned char* rank_one;
 };
+constexpr double GYK_MSP_ROOM = 32.0;
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // gyk + the fused apply_AH (Z-step pass) in one launch; needs a.lazy and a.glds
 size_t gyf_lds_bytes(int m);
@@ -324,6 +351,15 @@ struct ZArgs {
     int fixup_now;   // last iteration: finish a pending test here (dual_fixup), no later gyk_kernel
     int xfuse;       // the fused apply_AH ran: realisations with st->fzit == it have X in Zn and their sums
     int compact;     // steady state: zstep1w_compact_kernel (one wave per 8 realisations)
+    // m-space steady state (RealState::msp): realisations with st->mzit == it were settled by
+    // gyk_kernel (no apply_AH pass); a failed bound materialises Z, Z' (and opt_X) from Af, S
+    int msp;
+    const double* Af;      // A [m][n] c128
+    const double* Sold;
+    const double* Snew;
+    const double* optS;
+    int matz;              // (launch_i8_msp_optx) the apply_AH launch forms opt_X = Z0 + A^H opt_S
+    int msp_fail_it;       // (tests: ACE_MSP_FAIL_IT) the bound of m-space iterates fails at this iteration
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

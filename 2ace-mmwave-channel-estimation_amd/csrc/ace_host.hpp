@@ -153,6 +153,7 @@ struct AdmmState {
     RealState* st;
     int* done;
     double* zeros;  // [n] c128 zeros (N of realisations with RealState::nzero)
+    double *Sg[2], *optS;  // r = 1 m-space steady state (RealState::msp): S ping-pong, opt_S ([batch][m])
 };
 void admm_state_carve(Carver& cv, int batch, int m, int n, int r, AdmmState* s);
 // Runs init (:296-310), the iterations (:318-383) and returns the best-objective iterate

@@ -317,6 +317,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     __shared__ double sc_s[RB];
     __shared__ int live_s[RB];
     __shared__ FuseState fs_s[FUSE ? RB : 1];
+    __shared__ int z0_s[(!FUSE && !KY) ? RB : 1];
     const int rst = 32 * nks + 16;   // LDS row stride (bytes)
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -324,13 +325,22 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     const int bl = t >> 5, cp = t & 31, jb = j0 + bl;
     STAMP_DECL;
     STAMP(0);
-    const bool live = jb < nb && !rs[jb].done;
+    // m-space realisations (RealState::mzit, set by gyk_body of this launch) need no pass; the
+    // matz launch (launch_i8_msp_optx) takes exactly the realisations with opt_X in m-space form
+    const bool matz = !FUSE && !KY && za.matz;
+    const bool live = jb < nb && (matz ? rs[jb].optsrc == 3 : (!rs[jb].done && !(za.msp && rs[jb].mzit == za.it)));
+    // a block none of whose realisations needs the pass (all settled in m-space, done, or past nb)
+    // skips it whole (uniform across the work-group)
+    if (!__syncthreads_or(live)) return;
     const int zn_id = 1 + (za.it & 1);
+    if constexpr (!FUSE && !KY) {
+        if (matz && t < RB) z0_s[t] = j0 + t < nb ? rs[j0 + t].z0id : 0;
+    }
     if constexpr (FUSE) {
         if (t < RB) {
             const int j = j0 + t;
             FuseState f{};
-            if (j < nb && !rs[j].done) {
+            if (j < nb && !rs[j].done && !(za.msp && rs[j].mzit == za.it)) {
                 const RealState& r = rs[j];
                 f.el = r.kfok && r.nzero;
                 const bool improved_pre = sqrt(r.obj2) < r.opt_obj;   // (as the Z-step decides it)
@@ -505,7 +515,11 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const int col = (ct0 + c) * 32 + (lane & 31);
-                    if (col < ldo) Wp[(long long)j * ldo + col] = scb * recombine(acc[R][c], q);
+                    if (col >= ldo) continue;
+                    const long long off = (long long)j * ldo + col;
+                    const double wv = scb * recombine(acc[R][c], q);
+                    if (matz) Wp[off] = (z0_s[blo] == 1 ? za.Z : za.Zn)[off] + wv;   // Z0 + A^H opt_S
+                    else Wp[off] = wv;
                 }
             }
         }
@@ -564,6 +578,9 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     }
     STAMP(2);
     if (!KY && !FUSE) STAMP_PRINT("i8ah prologue|sweep:", 3);
+    if constexpr (!FUSE && !KY) {
+        if (matz && (t & 31) == 0 && live) za.st[jb].optsrc = 0;
+    }
     if constexpr (FUSE) {
         __syncthreads();
         {   // half-wave t >> 5 = realisation blo: its 8 waves x 32 lanes of slots, fixed order
@@ -652,9 +669,9 @@ struct GSet {
 
 template <bool GLDS>   // g stays in the LDS rows of T for the fused apply_AH (gyf_kernel) instead of a.g
 __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem) {
-    __shared__ double red[8][GRB][7];
+    __shared__ double red[8][GRB][9];
     __shared__ double sc_s[GRB], p2_s[GRB];
-    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB], msp_s[GRB], ent_s[GRB];
     __shared__ double imu0_s[GRB], mu_s[GRB];
     const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
     d2* Ts = reinterpret_cast<d2*>(smem);               // [16][tst]: T, then Y_new
@@ -687,6 +704,20 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
         imu0_s[t] = lv ? 1.0 / mu_s[t] : 0.0;
         oys_s[t] = lv ? a.rs[j].optysrc : 0;
         pend_s[t] = lv && a.lazy && a.rs[j].dpend;
+        // m-space step candidate (RealState::msp): certified, N = 0, V = the previous X, an opt_X
+        // recorded, and the previous iteration left ||Z||^2 in fs0 (fused pass or m-space step).
+        // A realisation already in the form stays in it; a new one enters after the Y-step only if
+        // the bound has room (below), else it takes the fused apply_AH pass as before.
+        int ms = 0, en = 0;
+        if (GLDS && a.msp && lv && a.it >= 2) {
+            const RealState& r = a.rs[j];
+            // (Z of a realisation in the form is not in memory: it stays in it; a failed bound
+            // materialises it in the Z-step)
+            ms = r.msp || (avok_s[t] && r.kfok && r.nzero && r.opt_obj < INFINITY && r.fzit == a.it - 1);
+            en = ms && !r.msp;
+        }
+        msp_s[t] = ms;
+        ent_s[t] = en;
     }
     __syncthreads();
     // T of the avok realisations from the early loads (a block that needs apply_A or finishes a
@@ -968,11 +999,11 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
 #endif
 
     // ---- Y-step on this lane's 2 x 4 outputs: realisation (lane >> 4) + 4 r, output 16 ct + (lane & 15)
-    double v7[4][7];
+    double v7[4][9];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int k = 0; k < 7; ++k) v7[r][k] = 0.0;
+        for (int k = 0; k < 9; ++k) v7[r][k] = 0.0;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int ct = 2 * w + c;
@@ -1000,8 +1031,19 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             if (a.AX) reinterpret_cast<d2*>(a.AX)[off] = ax;
             reinterpret_cast<d2*>(a.M)[off] = cadd(mii, cscale(jv, mu));
             reinterpret_cast<d2*>(a.Yn)[off] = y;
-            if constexpr (GLDS) Ts[jl * tst + i] = gv;   // g stays on chip for the fused apply_AH
-            else Ts[jl * tst + i] = y;
+            if constexpr (GLDS) {
+                if (msp_s[jl]) {   // m-space candidate: Re (A Z)^H g, g^H K g = Re g^H (T - g), S' = S + g
+                    const d2 tv = Ts[jl * tst + i];
+                    const d2 av = csub(csub(yo, cscale(mii, imu)), tv);   // A V = A Z (T's input)
+                    v7[r][7] += av.x * gv.x + av.y * gv.y;
+                    v7[r][8] += gv.x * (tv.x - gv.x) + gv.y * (tv.y - gv.y);
+                    const d2 so = ent_s[jl] ? make_double2(0.0, 0.0) : reinterpret_cast<const d2*>(a.Sold)[off];
+                    reinterpret_cast<d2*>(a.Snew)[off] = cadd(so, gv);
+                }
+                Ts[jl * tst + i] = gv;   // g stays on chip for the fused apply_AH
+            } else {
+                Ts[jl * tst + i] = y;
+            }
             const double aax = sqrt(cabs2(ax)) - Bi;
             v7[r][0] += aax * aax;
             v7[r][1] += cabs2(ax);
@@ -1024,20 +1066,26 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             for (int k = 0; k < 5; ++k) v7[r][k] += __shfl_xor(v7[r][k], o, 64);
             v7[r][5] = fmax(v7[r][5], __shfl_xor(v7[r][5], o, 64));
             v7[r][6] += __shfl_xor(v7[r][6], o, 64);
+            if (GLDS && a.msp) {
+                v7[r][7] += __shfl_xor(v7[r][7], o, 64);
+                v7[r][8] += __shfl_xor(v7[r][8], o, 64);
+            }
         }
         if ((lane & 15) == 0)
 #pragma unroll
-            for (int k = 0; k < 7; ++k) red[w][(lane >> 4) + 4 * r][k] = v7[r][k];
+            for (int k = 0; k < 9; ++k) red[w][(lane >> 4) + 4 * r][k] = v7[r][k];
     }
     __syncthreads();
     STAMP(3);
     if (t < GRB) {
-        double v[7] = {0, 0, 0, 0, 0, 0, 0};
+        double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int q = 0; q < 8; ++q) {   // fixed order over the waves
 #pragma unroll
             for (int k = 0; k < 5; ++k) v[k] += red[q][t][k];
             v[5] = fmax(v[5], red[q][t][5]);
             v[6] += red[q][t][6];
+            v[7] += red[q][t][7];
+            v[8] += red[q][t][8];
         }
         int imp = 0;
         double p2 = 1.0, sc = 0.0;
@@ -1052,6 +1100,33 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             plane_scale(v[5] + v[6], a.c8[1], p2, sc);
             if (a.yn_id)   // opt_Y deferred: Y_new stays in Yn until that buffer comes round again
                 rs.optysrc = imp ? a.yn_id : (oys_s[t] == a.yn_id ? 0 : oys_s[t]);
+            if (msp_s[t]) {   // the fused pass's sums, from m-space (RealState::msp)
+                const double s0 = rs.fs0 + 2.0 * v[7] + v[8];   // ||Z + A^H g||^2
+                const double s3 = v[8];                         // ||A^H g||^2
+                bool take = !ent_s[t];
+                if (!take) {   // entry: the bound of fused_control with GYK_MSP_ROOM more steps like this one
+                    const bool r1 = a.rank_one && a.rank_one[j0 + t];
+                    const int np = r1 ? 1 : a.np;
+                    const double cum = rs.kfcum + GYK_MSP_ROOM * sqrt(s3);
+                    take = s0 > 0.0;
+                    for (int p = 0; p < 4 && p < np; ++p) {
+                        const double fl = r1 ? 0.95 : a.fl[p], lb = rs.kf[p] * (1.0 - 1e-12) - cum;
+                        take = take && lb > 0.0 && lb * lb > fl * s0 * (1.0 + 1e-9);
+                    }
+                }
+                if (take) {
+                    rs.fs0 = s0;
+                    rs.fs3 = s3;
+                    rs.fzit = a.it;
+                    rs.mzit = a.it;
+                    if (ent_s[t]) {
+                        rs.msp = 1;
+                        rs.z0id = (a.it & 1) ? 1 : 2;   // the Z buffer this iteration reads (Zc)
+                        rs.msp_pad = a.it;               // (entry iteration: no S before it)
+                    }
+                }
+                msp_s[t] = take;
+            }
         }
         imp_s[t] = imp;
         p2_s[t] = p2;
@@ -1067,6 +1142,13 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
         if (!a.yn_id && live_s[jl] && imp_s[jl])
             reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
     }
+    if (GLDS && a.msp)
+        for (int idx = t; idx < GRB * m; idx += NT) {   // opt_S of an improved m-space iterate
+            const int jl = idx / m, i = idx - jl * m;
+            if (live_s[jl] && msp_s[jl] && imp_s[jl])
+                reinterpret_cast<d2*>(a.optS)[(long long)(j0 + jl) * m + i] =
+                    reinterpret_cast<const d2*>(a.Snew)[(long long)(j0 + jl) * m + i];
+        }
     if (a.lazy) {   // no K Y: the Z-step forms the dual terms when the test needs them
         STAMP(5);
         STAMP_PRINT("gyk-lazy T|GT|Ystep+shfl|red+RS|optY:", 6);
@@ -1330,8 +1412,17 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad);
 }
+void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* optS, double* optX, const double* cmax,
+                        RealState* rs, const double* Zb1, const double* Zb2, hipStream_t st) {
+    ZArgs za{};
+    za.matz = 1;
+    za.st = rs;
+    za.Z = const_cast<double*>(Zb1);
+    za.Zn = const_cast<double*>(Zb2);
+    launch_i8_apply_AH(nb, m, n, LAH, optS, optX, cmax, rs, st, nullptr, &za);
+}
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
-                        const RealState* rs, hipStream_t st, const ZArgs* fuse) {
+                        const RealState* rs, hipStream_t st, const ZArgs* fuse, const ZArgs* plain) {
     static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
         // dynamic + static (FUSE: 7.3 KiB of per-realisation state and partial sums) <= 160 KiB
         const bool a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false, false>),
@@ -1349,7 +1440,7 @@ void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g
                            reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, *fuse);
     else
         hipLaunchKernelGGL((i8ah_kernel<false, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
-                           reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, ZArgs{});
+                           reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, plain ? *plain : ZArgs{});
 }
 
 }  // namespace ace

@@ -57,9 +57,11 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
 }
 
 // Certificate and iteration control of a realisation whose X the fused apply_AH formed in Z'
-// with its sums (RealState::fzit, fs0 = ||X||^2, fs3 = ||X - Z||^2), on one lane: the
-// perturbation bound of zlean_kernel; if it holds, Z' = E = X stands, N' = 0, and the control
-// runs.  Returns 0 (nothing written) when the bound fails: the full Z-step must run.
+// with its sums (RealState::fzit, fs0 = ||X||^2, fs3 = ||X - Z||^2), or whose sums gyk_kernel
+// formed in m-space (RealState::mzit == it, X implicit), on one lane: the perturbation bound of
+// zlean_kernel; if it holds, Z' = E = X stands, N' = 0, and the control runs.  Returns 0 (nothing
+// written) when the bound fails: the full Z-step must run; else 1, plus 2 when the convergence
+// test is left pending (ZArgs::lazy_dual: at the last iteration the wave runs dual_fixup).
 __device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
     RealState s = *st;   // one batch of loads (the chain below then runs on registers)
     const double s0 = s.fs0, s3 = s.fs3;
@@ -71,18 +73,81 @@ __device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, cons
         const double lb = s.kf[p] * (1.0 - 1e-12) - cum;
         pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
     }
+    pass &= !(a.msp && s.mzit == a.it && a.it == a.msp_fail_it);   // (tests: the fallback path)
     if (!pass) return 0;
     const bool improved_pre = sqrt(s.obj2) < s.opt_obj;
     const int optsrc = s.optsrc;   // (the fused kernel kept a best iterate in Z')
-    iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY);
+    const int ctl = iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY);
     s.vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
     s.nzero = 1;
     s.avok = 1;
-    s.optsrc = improved_pre ? 1 + (a.it & 1) : optsrc;   // deferred opt_X: X = Z' bit for bit
+    // deferred opt_X: X = Z' bit for bit, or (m-space) X = Z0 + A^H opt_S
+    s.optsrc = improved_pre ? (a.msp && s.mzit == a.it ? 3 : 1 + (a.it & 1)) : optsrc;
     s.kfcum = cum;
     s.zit = a.it;
     *st = s;
-    return 1;
+    return 1 | (ctl & 2);
+}
+
+// m-space fallback (RealState::msp): the bound failed for an iterate gyk_kernel settled in m-space,
+// so the full Z-step needs Z and X = Z' in memory.  One wave forms them from the implicit form,
+// out = base + A^H v with the f64 A (rare: the bound keeps holding once it holds), and opt_X if
+// it lives in m-space form or in a Z buffer about to be rewritten.
+__device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
+    const int lane = threadIdx.x, n = a.n, m = a.m;
+    RealState* st = a.st + b;
+    const int zc_id = (a.it & 1) ? 1 : 2, zn_id = 1 + (a.it & 1);
+    const int z0id = st->z0id, optsrc = st->optsrc, entered = st->msp_pad == a.it;
+    d2* Zc = reinterpret_cast<d2*>(a.Z) + (long long)b * n;
+    d2* Zn = reinterpret_cast<d2*>(a.Zn) + (long long)b * n;
+    d2* Z0 = z0id == zc_id ? Zc : Zn;
+    d2* oX = reinterpret_cast<d2*>(a.optX) + (long long)b * n;
+    const d2* Af = reinterpret_cast<const d2*>(a.Af);
+    const long long om = (long long)b * m;
+    auto gemv = [&](d2* out, const d2* base, const d2* v) {   // out[k] = base[k] + sum_i conj(A[i][k]) v[i]
+        for (int k0 = 0; k0 < n; k0 += 64 * 4) {
+            d2 acc[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = make_double2(0.0, 0.0);
+            for (int i = 0; i < m; ++i) {
+                const d2 vi = v[i];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = min(k0 + lane + 64 * u, n - 1);
+                    const d2 av = Af[(long long)i * n + k];
+                    acc[u].x = fma(av.x, vi.x, fma(av.y, vi.y, acc[u].x));
+                    acc[u].y = fma(av.x, vi.y, fma(-av.y, vi.x, acc[u].y));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + lane + 64 * u;
+                if (k < n) out[k] = cadd(base[k], acc[u]);
+            }
+        }
+        __syncthreads();   // (one wave) the stores are visible to every lane's later loads
+    };
+    if (optsrc == 3) {
+        gemv(oX, Z0, reinterpret_cast<const d2*>(a.optS) + om);
+    } else if (optsrc == zc_id || optsrc == zn_id) {
+        const d2* src = optsrc == zc_id ? Zc : Zn;
+        for (int k = lane; k < n; k += 64) oX[k] = src[k];
+        __syncthreads();
+    }
+    const d2* Sn = reinterpret_cast<const d2*>(a.Snew) + om;
+    const d2* So = reinterpret_cast<const d2*>(a.Sold) + om;
+    if (Z0 == Zc) {
+        gemv(Zn, Zc, Sn);
+        if (!entered) gemv(Zc, Zc, So);
+    } else {
+        gemv(Zc, Zn, So);   // (entered implies Z0 == Zc)
+        gemv(Zn, Zn, Sn);
+    }
+    if (lane == 0) {
+        if (optsrc == 3 || optsrc == zc_id || optsrc == zn_id) st->optsrc = 0;
+        st->msp = 0;
+    }
+    __syncthreads();
 }
 
 template <bool INIT>
@@ -100,7 +165,12 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     if (xin) {
         int ok = 0;
         if (threadIdx.x == 0) ok = fused_control(a, st, pf);
-        if (__shfl(ok, 0, 64)) return;
+        ok = __shfl(ok, 0, 64);
+        if (ok) {
+            if ((ok & 2) && a.fixup_now) dual_fixup(a, b, st);   // pending test at the last iteration
+            return;
+        }
+        if (a.msp && st->mzit == a.it) msp_materialise(a, b);
     }
     __shared__ __attribute__((aligned(16))) d2 T0[ZT * ZHS];
     __shared__ double4 RotS[16];

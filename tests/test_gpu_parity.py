@@ -248,13 +248,17 @@ def test_split_streams_match_single_batch(gpu):
         assert np.array_equal(sub.iters.cpu().numpy(), big.iters.cpu().numpy()[lo:lo + 64])
 
 
+@pytest.mark.parametrize("msp", ["1", "0"])
 @pytest.mark.parametrize("batch", [64, 1024])
-def test_unit_path_launches_three_kernels_per_iteration(gpu, batch):
+def test_unit_path_launches_three_kernels_per_iteration(gpu, monkeypatch, batch, msp):
     """The phase-code r = 1 iteration is gyk_kernel + apply_AH + Z-step: no apply_A, pre, Y-step
     or K Y launch (with and without concurrent sub-batches), one launch of each per iteration and
     sub-batch.  With concurrent sub-batches gyk and the fused apply_AH are one launch (gyf_kernel,
-    counted as apply_G) except at the last iteration."""
+    counted as apply_G) except at the last iteration.  With m-space steps (ACE_MSPACE, default on)
+    every iteration, the last included and one batch too, is gyf_kernel + Z-step, and one
+    apply_AH launch at the end forms the m-space best iterates (RealState::optsrc 3)."""
     import ctypes as C
+    monkeypatch.setenv("ACE_MSPACE", msp)
     import torch
     from ace_amd import infer_admm_batch, synth_problem
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
@@ -275,7 +279,10 @@ def test_unit_path_launches_three_kernels_per_iteration(gpu, batch):
         assert n[k] == 0, (k, n)
     for k in ("apply_G", "zstep"):
         assert n[k] == iters * subs, (k, n)
-    assert n["apply_AH"] == (subs if subs > 1 else iters), n
+    if msp == "1":
+        assert n["apply_AH"] == 0, n   # (the final opt_X launch runs under the finalize scope)
+    else:
+        assert n["apply_AH"] == (subs if subs > 1 else iters), n
 
 
 @pytest.mark.parametrize("a_shared,batch", [(True, 1024), (True, 64), (False, 64)])
@@ -337,6 +344,42 @@ def test_compact_zstep_bit_identical(gpu, monkeypatch, fixed):
         out[zc] = (r.X.cpu().numpy(), r.iters.cpu().numpy(), r.status.cpu().numpy())
     for a, b in zip(out["0"], out["3"]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("fail_it", [None, "40", "200"])
+@pytest.mark.parametrize("fixed", [True, False])
+@pytest.mark.parametrize("batch,m,tx", [(1024, 256, 32), (64, 256, 32), (600, 121, 16)])
+def test_mspace_steps(gpu, monkeypatch, batch, m, tx, fixed, fail_it):
+    """m-space steady state (RealState::msp, ACE_MSPACE): Z kept as Z0 + A^H S, the fused pass's
+    sums from m-space, no apply_AH pass for settled realisations, the best iterate materialised at
+    the end.  Against the memory form (ACE_MSPACE=0): equal to rounding (1e-10 relative), identical
+    iteration counts and flags; a sample against the oracle.  ACE_MSP_FAIL_IT forces the bound of
+    every m-space iterate to fail at one iteration (the Z-step then materialises Z, Z' and opt_X from
+    the implicit form and runs the full step): 40 = mid-solve, 200 = the last iteration."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(59, 0, batch, m, tx, tx)
+    out = {}
+    for msp in ("0", "1"):
+        monkeypatch.setenv("ACE_MSPACE", msp)
+        if fail_it and msp == "1":
+            monkeypatch.setenv("ACE_MSP_FAIL_IT", fail_it)
+        r = infer_admm_batch(A, B, X0, tx, tx, maxiter=200, fixed_iters=fixed)
+        torch.cuda.synchronize()
+        out[msp] = (r.X.cpu().numpy(), r.Y.cpu().numpy(), r.iters.cpu().numpy(), r.status.cpu().numpy())
+        monkeypatch.delenv("ACE_MSP_FAIL_IT", raising=False)
+    X0_, Y0_, it0, st0 = out["0"]
+    X1, Y1, it1, st1 = out["1"]
+    assert np.isfinite(X1).all() and np.isfinite(Y1).all()
+    assert _errs(X1, X0_).max() <= 1e-10
+    assert _errs(Y1, Y0_).max() <= 1e-10
+    assert np.array_equal(it1, it0)
+    assert np.array_equal(st1, st0)
+    idx = [0, batch // 3, batch - 1]
+    Ah, Bh, X0h = A.cpu().numpy(), B.cpu().numpy()[idx], X0.cpu().numpy()[idx]
+    Xo, _, ito, _, _ = _oracle(Ah, Bh, X0h, tx, variant=0, maxiter=200, fixed_iters=fixed)
+    assert _errs(X1[idx], Xo).max() <= TOL
+    assert np.array_equal(it1[idx], ito)
 
 
 @pytest.mark.parametrize("batch,m,tx", [(1000, 256, 32), (1024, 121, 16), (1040, 243, 32)])

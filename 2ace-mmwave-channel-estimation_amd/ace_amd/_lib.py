@@ -111,6 +111,8 @@ def _load():
     lib.ace_prof_sample.restype = C.c_int
     lib.ace_prof_stop.argtypes = [dp, ip]
     lib.ace_prof_stop.restype = C.c_int
+    lib.ace_prof_msp_steps.argtypes = [C.POINTER(C.c_longlong)]
+    lib.ace_prof_msp_steps.restype = C.c_int
     lib.ace_last_error.argtypes = []
     lib.ace_last_error.restype = C.c_char_p
     lib.ace_version.argtypes = []

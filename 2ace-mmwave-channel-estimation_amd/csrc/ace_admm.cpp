@@ -85,6 +85,14 @@ static bool mspace_enabled() {
     return !(e && e[0] == '0');
 }
 
+// ACE_MSP_ROOM=<k>: a realisation enters the m-space form only if the perturbation bound would
+// still hold after k more steps of the current size (default 32; entries that fail soon after
+// cost a materialisation in the Z-step).
+static double msp_room() {
+    const char* e = getenv("ACE_MSP_ROOM");
+    return e ? atof(e) : 32.0;
+}
+
 // ACE_MSP_FAIL_IT=<it> (tests): the perturbation bound of every m-space iterate fails at that
 // iteration, so the Z-step materialises Z, Z' and opt_X from the implicit form.
 static int msp_fail_it() {
@@ -424,7 +432,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
                        L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0,
                        gyf && msp ? 1 : 0, it, za.Sold, wh.Sg[it & 1], wh.optS, za0.np,
-                       {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one};
+                       {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one, msp_room()};
             if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, sh);
@@ -461,6 +469,9 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
         ProfScope ps(ACE_K_FINAL, st);
         // best iterates still in m-space form (RealState::optsrc 3): opt_X = Z0 + A^H opt_S
         if (msp) launch_i8_msp_optx(batch, m, n, L.LAH8, w.optS, w.optX, L.c8, w.st, w.Z, w.Z2, st);
+        if (msp && g_prof.on && g_prof.msp_used < g_prof.msp_cap)   // (ace_prof_msp_steps)
+            ACE_HIP(hipMemcpyAsync(g_prof.msp_slots + g_prof.msp_used++, w.done + 1, sizeof(int),
+                                   hipMemcpyDeviceToHost, st));
         launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st, w.Z,
                           w.Z2, w.Y[0], w.Y[1]);
     }

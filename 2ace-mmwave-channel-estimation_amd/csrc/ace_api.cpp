@@ -46,7 +46,19 @@ int ace_prof_start(int max_launches) {
     g_prof.cls.assign(max_launches, 0);
     g_prof.used = 0;
     for (int& c : g_prof.seen) c = 0;
+    if (!g_prof.msp_slots) {
+        g_prof.msp_cap = 4096;
+        ACE_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_prof.msp_slots), sizeof(int) * g_prof.msp_cap));
+    }
+    g_prof.msp_used = 0;
     g_prof.on = true;
+    return ACE_OK;
+}
+
+int ace_prof_msp_steps(long long* steps) {
+    g_err.clear();
+    if (!steps) return fail(ACE_ERR_ARG, "steps is NULL");
+    *steps = g_prof.msp_total;
     return ACE_OK;
 }
 
@@ -69,6 +81,10 @@ int ace_prof_stop(double* total_ms, int32_t* launches) {
     g_prof.ev.clear();
     g_prof.cls.clear();
     g_prof.used = 0;
+    ACE_HIP(hipDeviceSynchronize());   // (the m-space counters are copied after the last events)
+    g_prof.msp_total = 0;
+    for (int i = 0; i < g_prof.msp_used; ++i) g_prof.msp_total += g_prof.msp_slots[i];
+    g_prof.msp_used = 0;
     return ACE_OK;
 }
 

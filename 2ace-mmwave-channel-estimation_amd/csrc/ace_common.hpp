@@ -244,12 +244,12 @@ struct GykArgs {
     double* Snew;
     double* optS;
     // the Z-step's rank profile (z_profile): a realisation enters the m-space form only while the
-    // perturbation bound has room for GYK_MSP_ROOM more steps of the current size
+    // perturbation bound has room for `room` more steps of the current size (ACE_MSP_ROOM)
     int np;
     double fl[4];
     const unsigned char* rank_one;
+    double room;
 };
-constexpr double GYK_MSP_ROOM = 32.0;
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // gyk + the fused apply_AH (Z-step pass) in one launch; needs a.lazy and a.glds
 size_t gyf_lds_bytes(int m);

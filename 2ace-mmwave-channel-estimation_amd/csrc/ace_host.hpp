@@ -48,6 +48,11 @@ struct Prof {
     int stride = 1;               // record every stride-th launch of each class (ace_prof_sample) ...
     unsigned full = 0;            // ... except the classes in this mask, recorded on every launch
     int seen[ACE_NKCLASS] = {};
+    // m-space step counts of the solves in the session (ace_prof_msp_steps): one pinned slot per
+    // solve, filled from the device counter (AdmmState::done[1]) at the end of the solve
+    int* msp_slots = nullptr;
+    int msp_cap = 0, msp_used = 0;
+    long long msp_total = 0;
 };
 inline Prof g_prof;
 

@@ -1104,10 +1104,10 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                 const double s0 = rs.fs0 + 2.0 * v[7] + v[8];   // ||Z + A^H g||^2
                 const double s3 = v[8];                         // ||A^H g||^2
                 bool take = !ent_s[t];
-                if (!take) {   // entry: the bound of fused_control with GYK_MSP_ROOM more steps like this one
+                if (!take) {   // entry: the bound of fused_control with `room` more steps like this one
                     const bool r1 = a.rank_one && a.rank_one[j0 + t];
                     const int np = r1 ? 1 : a.np;
-                    const double cum = rs.kfcum + GYK_MSP_ROOM * sqrt(s3);
+                    const double cum = rs.kfcum + a.room * sqrt(s3);
                     take = s0 > 0.0;
                     for (int p = 0; p < 4 && p < np; ++p) {
                         const double fl = r1 ? 0.95 : a.fl[p], lb = rs.kf[p] * (1.0 - 1e-12) - cum;
@@ -1115,6 +1115,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                     }
                 }
                 if (take) {
+                    atomicAdd(a.dc.done_count + 1, 1);   // m-space step count (ace_prof_msp_steps)
                     rs.fs0 = s0;
                     rs.fs3 = s3;
                     rs.fzit = a.it;

@@ -292,6 +292,22 @@ def gyf_bytes(m, n):
     return 16.0 * 6 * m + 8.0 * m + 16.0 * 2 * n
 
 
+def msp_bytes(m):
+    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel for a realisation in m-space
+    form (RealState::msp: Z implicit as Z0 + A^H S, no apply_AH pass): read Y, M, AX, S (c128) and
+    B (f64); write AX, M, Y_new and S' = S + g.  (opt_S, copied when the iterate improves, is not
+    counted: a bookkeeping copy like the deferred opt_X / opt_Y.)"""
+    return 16.0 * 8 * m + 8.0 * m
+
+
+def msp_bytes(m):
+    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel for a realisation in m-space
+    form (RealState::msp: Z implicit as Z0 + A^H S, no apply_AH pass): read Y, M, AX, S (c128) and
+    B (f64); write AX, M, Y_new and S' = S + g.  (opt_S, copied when the iterate improves, is not
+    counted: a bookkeeping copy like the deferred opt_X / opt_Y.)"""
+    return 16.0 * 8 * m + 8.0 * m
+
+
 def unit_bytes(m, n, tx, rx):
     """Algorithmic HBM bytes per realisation per iteration of the steady-state unit path
     (complex128 = 16 B, each array read or written once):
@@ -490,8 +506,10 @@ def unit_bench(args, private, dev, rank, world):
     elapsed = time.perf_counter() - t0
     kt = (C.c_double * 10)()
     kn = (C.c_int32 * 10)()
+    msp_steps = C.c_longlong(0)
     if prof:
         check(LIB.ace_prof_stop(kt, kn))
+        check(LIB.ace_prof_msp_steps(C.byref(msp_steps)))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -526,7 +544,13 @@ def unit_bench(args, private, dev, rank, world):
             gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
             # with concurrent sub-batches apply_G is gyf_kernel: gyk and the fused apply_AH in one launch
             env_on = lambda k: os.environ.get(k) != "0"
-            gyf = gyk and nsplit > 1 and all(env_on(k) for k in ("ACE_GYF", "ACE_FUSE", "ACE_LAZY_DUAL", "ACE_LEAN"))
+            # (and with m-space steps, ACE_MSPACE, on one batch too, A2only)
+            msp_on = env_on("ACE_MSPACE") and args.variant == "A2only"
+            gyf = gyk and (nsplit > 1 or msp_on) and all(env_on(k) for k in ("ACE_GYF", "ACE_FUSE", "ACE_LAZY_DUAL",
+                                                                             "ACE_LEAN"))
+            # share of the realisation-iterations gyf_kernel settled in m-space form (no apply_AH
+            # pass, no Z traffic: ace_prof_msp_steps); the per-launch work below is averaged with it
+            msp_frac = msp_steps.value / float(args.steps * bsz * args.iters) if msp_on else 0.0
             # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
             pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
 
@@ -548,7 +572,9 @@ def unit_bench(args, private, dev, rank, world):
                             "bytes_note": "per realisation: G_b lower triangle (c128) + A_b^H as 2-bit codes + "
                                           "Y, M, AX, B in and AX, M, Y out + W = A^H g out (bench.private_bytes)"}
                 if k == "apply_G" and gyf:   # f64 G T, int8 A^H g, HBM (T, Y-step, Z pass), phase after phase
-                    f, o, b = uf[k] * per_launch, io["apply_AH"] * per_launch, gyf_bytes(m, n) * per_launch
+                    f = uf[k] * per_launch
+                    o = io["apply_AH"] * per_launch * (1.0 - msp_frac)
+                    b = (msp_frac * msp_bytes(m) + (1.0 - msp_frac) * gyf_bytes(m, n)) * per_launch
                     tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
                     res = {
                         "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
@@ -565,10 +591,14 @@ def unit_bench(args, private, dev, rank, world):
                     out.update({"traffic": None, "kernel": "apply_G (gyf_kernel)", "resource": main,
                                 "other_resources": {r: v for r, v in res.items() if r != main},
                                 "serial_frac": round((tf + to + tb) / avg_s, 4),
+                                "msp_frac": round(msp_frac, 4),
                                 "flop_note": "gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per "
                                              "complex MAC), the Y-step, then W = A^H g (int8 digit planes) with the "
                                              "certified Z-step pass (Z in, Z' out) in its epilogue, one phase after "
-                                             "another in each work-group; bound = the resource with the largest time "
+                                             "another in each work-group; a realisation in m-space form (msp_frac of "
+                                             "the realisation-iterations) skips the int8 pass and the Z traffic and "
+                                             "moves S in / S' out instead (bench.msp_bytes); int8 ops and bytes are "
+                                             "averaged with msp_frac; bound = the resource with the largest time "
                                              "at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"})
                     return out
                 if k == "apply_G" and gyk:   # f64 G T + the Y-step's HBM traffic, phase after phase

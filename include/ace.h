@@ -272,6 +272,10 @@ int ace_prof_start(int max_launches);
  * recorded on every launch: keeps the event overhead out of a throughput measurement. */
 int ace_prof_sample(int stride, uint32_t full_mask);
 int ace_prof_stop(double* total_ms, int32_t* launches);
+/* Realisation-iterations the unit solves between the last ace_prof_start / ace_prof_stop pair
+ * settled in m-space form (RealState::msp: no apply_AH pass, no Z traffic), for the bench's
+ * per-launch work accounting. */
+int ace_prof_msp_steps(long long* steps);
 
 /* Last error text for this thread ("" if none). */
 const char* ace_last_error(void);

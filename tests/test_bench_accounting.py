@@ -33,6 +33,12 @@ def test_gyf_bytes():
     assert b.gyf_bytes(m, n) == 16 * 6 * m + 8 * m + 32 * n == 58 * 1024
 
 
+def test_msp_bytes():
+    b = _bench()
+    # m-space form: read Y, M, AX, S, B; write AX, M, Y, S' (no Z, no apply_AH pass)
+    assert b.msp_bytes(256) == 16 * 8 * 256 + 8 * 256 == 34 * 1024
+
+
 def test_int8_ops_and_flops():
     b = _bench()
     io = b.unit_i8_ops(256, 1024)

@@ -468,7 +468,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     {
         ProfScope ps(ACE_K_FINAL, st);
         // best iterates still in m-space form (RealState::optsrc 3): opt_X = Z0 + A^H opt_S
-        if (msp) launch_i8_msp_optx(batch, m, n, L.LAH8, w.optS, w.optX, L.c8, w.st, w.Z, w.Z2, st);
+        if (msp) launch_i8_msp_optx(batch, m, n, L.LAH8, w.optS, w.optX, L.c8, w.st, w.Z, w.Z2, w.Sg[0], w.Sg[1], st);
         if (msp && g_prof.on && g_prof.msp_used < g_prof.msp_cap)   // (ace_prof_msp_steps)
             ACE_HIP(hipMemcpyAsync(g_prof.msp_slots + g_prof.msp_used++, w.done + 1, sizeof(int),
                                    hipMemcpyDeviceToHost, st));

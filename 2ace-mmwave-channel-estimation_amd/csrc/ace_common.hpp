@@ -72,7 +72,8 @@ struct RealState {
     // ||X||^2 = ||Z||^2 + 2 Re (A Z)^H g + ||A^H g||^2 (A Z = A V, the T input), so apply_AH and the
     // Z / Z' traffic drop out of the iteration.  mzit: the iteration gyk_kernel settled that way;
     // msp: the implicit form is live (cleared when the Z-step materialises Z for a full step).
-    // optsrc = 3: opt_X = Z0 + A^H opt_S.
+    // optsrc = 3: opt_X = Z0 + A^H opt_S; 4 / 5: the same with opt_S still in the S ping-pong
+    // buffer Sg[0] / Sg[1] (deferred like opt_Y: copied only before that buffer is overwritten).
     int32_t msp, mzit, z0id, msp_pad;   // msp_pad: the entry iteration it0
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
@@ -199,7 +200,8 @@ size_t i8ah_fuse_lds_bytes();
 // opt_X = Z0 + A^H opt_S for the realisations whose best iterate is in m-space form (optsrc 3;
 // Z0 in Zb1 / Zb2 by RealState::z0id), done or not; sets optsrc = 0
 void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* optS, double* optX, const double* cmax,
-                        RealState* rs, const double* Zb1, const double* Zb2, hipStream_t st);
+                        RealState* rs, const double* Zb1, const double* Zb2, const double* S0, const double* S1,
+                        hipStream_t st);
 // Fused g = G T (3M f64 MFMA), Y-step, K Y (int8 digit planes), dual terms and opt_Y for
 // 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
 // fragment order (launch_gyk_gfrag at setup).

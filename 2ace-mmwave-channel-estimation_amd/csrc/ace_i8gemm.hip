@@ -671,7 +671,7 @@ template <bool GLDS>   // g stays in the LDS rows of T for the fused apply_AH (g
 __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem) {
     __shared__ double red[8][GRB][9];
     __shared__ double sc_s[GRB], p2_s[GRB];
-    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB], msp_s[GRB], ent_s[GRB];
+    __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB], msp_s[GRB], ent_s[GRB], oss_s[GRB];
     __shared__ double imu0_s[GRB], mu_s[GRB];
     const int mp = gyk_mp(m), tst = mp + 1;            // LDS row stride (complex, odd)
     d2* Ts = reinterpret_cast<d2*>(smem);               // [16][tst]: T, then Y_new
@@ -718,6 +718,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
         }
         msp_s[t] = ms;
         ent_s[t] = en;
+        oss_s[t] = lv ? a.rs[j].optsrc : 0;
     }
     __syncthreads();
     // T of the avok realisations from the early loads (a block that needs apply_A or finishes a
@@ -971,8 +972,9 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
     // the Y-step inputs of the lane's 8 elements as one batch of loads (unconditional, clamped
     // addresses; per-element branches would serialise 8 memory round trips).  Issued after the
     // G T loop: held across it they would push the kernel past 256 VGPRs into scratch.
-    d2 mi[2][4], yov[2][4];
+    d2 mi[2][4], yov[2][4], sov[2][4];
     double biv[2][4], muv[4];
+    const bool mspl = GLDS && a.msp;   // (m-space: S of the lane's outputs in the same batch)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int jl = (lane >> 4) + 4 * r;
@@ -984,6 +986,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             mi[c][r] = reinterpret_cast<const d2*>(a.M)[off];
             yov[c][r] = reinterpret_cast<const d2*>(a.Yo)[off];
             biv[c][r] = a.B[off];
+            sov[c][r] = mspl ? reinterpret_cast<const d2*>(a.Sold)[off] : make_double2(0.0, 0.0);
         }
     }
     __syncthreads();   // every wave is done with T: Ts becomes Y_new
@@ -1037,8 +1040,12 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                     const d2 av = csub(csub(yo, cscale(mii, imu)), tv);   // A V = A Z (T's input)
                     v7[r][7] += av.x * gv.x + av.y * gv.y;
                     v7[r][8] += gv.x * (tv.x - gv.x) + gv.y * (tv.y - gv.y);
-                    const d2 so = ent_s[jl] ? make_double2(0.0, 0.0) : reinterpret_cast<const d2*>(a.Sold)[off];
-                    reinterpret_cast<d2*>(a.Snew)[off] = cadd(so, gv);
+                    const d2 so = ent_s[jl] ? make_double2(0.0, 0.0) : sov[c][r];
+                    d2* sn = reinterpret_cast<d2*>(a.Snew) + off;
+                    // deferred opt_S (RealState::optsrc 4 / 5): the best iterate's S is the one this
+                    // store overwrites -- keep it first (rare: no better iterate for two iterations)
+                    if (oss_s[jl] == 4 + (a.it & 1)) reinterpret_cast<d2*>(a.optS)[off] = *sn;
+                    *sn = cadd(so, gv);
                 }
                 Ts[jl * tst + i] = gv;   // g stays on chip for the fused apply_AH
             } else {
@@ -1126,6 +1133,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                         rs.msp_pad = a.it;               // (entry iteration: no S before it)
                     }
                 }
+                if (oss_s[t] == 4 + (a.it & 1)) rs.optsrc = 3;   // (saved to opt_S in the loop above)
                 msp_s[t] = take;
             }
         }
@@ -1143,13 +1151,6 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
         if (!a.yn_id && live_s[jl] && imp_s[jl])
             reinterpret_cast<d2*>(a.optY)[(long long)(j0 + jl) * m + i] = Ts[jl * tst + i];
     }
-    if (GLDS && a.msp)
-        for (int idx = t; idx < GRB * m; idx += NT) {   // opt_S of an improved m-space iterate
-            const int jl = idx / m, i = idx - jl * m;
-            if (live_s[jl] && msp_s[jl] && imp_s[jl])
-                reinterpret_cast<d2*>(a.optS)[(long long)(j0 + jl) * m + i] =
-                    reinterpret_cast<const d2*>(a.Snew)[(long long)(j0 + jl) * m + i];
-        }
     if (a.lazy) {   // no K Y: the Z-step forms the dual terms when the test needs them
         STAMP(5);
         STAMP_PRINT("gyk-lazy T|GT|Ystep+shfl|red+RS|optY:", 6);
@@ -1413,8 +1414,20 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad);
 }
+// best m-space iterates still in an S ping-pong buffer (optsrc 4 / 5) -> opt_S (optsrc 3)
+__global__ __launch_bounds__(256) void msp_opt_gather_kernel(int m, RealState* rs, const double* S0, const double* S1,
+                                                             double* optS) {
+    const int b = blockIdx.x, os = rs[b].optsrc;
+    if (os != 4 && os != 5) return;
+    const d2* src = reinterpret_cast<const d2*>(os == 4 ? S0 : S1) + (long long)b * m;
+    d2* dst = reinterpret_cast<d2*>(optS) + (long long)b * m;
+    for (int i = threadIdx.x; i < m; i += 256) dst[i] = src[i];
+    if (threadIdx.x == 0) rs[b].optsrc = 3;
+}
 void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* optS, double* optX, const double* cmax,
-                        RealState* rs, const double* Zb1, const double* Zb2, hipStream_t st) {
+                        RealState* rs, const double* Zb1, const double* Zb2, const double* S0, const double* S1,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(msp_opt_gather_kernel, dim3(nb), dim3(256), 0, st, m, rs, S0, S1, const_cast<double*>(optS));
     ZArgs za{};
     za.matz = 1;
     za.st = rs;

@@ -56,39 +56,6 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
     }
 }
 
-// Certificate and iteration control of a realisation whose X the fused apply_AH formed in Z'
-// with its sums (RealState::fzit, fs0 = ||X||^2, fs3 = ||X - Z||^2), or whose sums gyk_kernel
-// formed in m-space (RealState::mzit == it, X implicit), on one lane: the perturbation bound of
-// zlean_kernel; if it holds, Z' = E = X stands, N' = 0, and the control runs.  Returns 0 (nothing
-// written) when the bound fails: the full Z-step must run; else 1, plus 2 when the convergence
-// test is left pending (ZArgs::lazy_dual: at the last iteration the wave runs dual_fixup).
-__device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
-    RealState s = *st;   // one batch of loads (the chain below then runs on registers)
-    const double s0 = s.fs0, s3 = s.fs3;
-    const double cum = (s.kfcum + sqrt(s3)) * (1.0 + 0x1p-40);
-    bool pass = s0 > 0.0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        if (p >= pf.np) break;
-        const double lb = s.kf[p] * (1.0 - 1e-12) - cum;
-        pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
-    }
-    pass &= !(a.msp && s.mzit == a.it && a.it == a.msp_fail_it);   // (tests: the fallback path)
-    if (!pass) return 0;
-    const bool improved_pre = sqrt(s.obj2) < s.opt_obj;
-    const int optsrc = s.optsrc;   // (the fused kernel kept a best iterate in Z')
-    const int ctl = iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY);
-    s.vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
-    s.nzero = 1;
-    s.avok = 1;
-    // deferred opt_X: X = Z' bit for bit, or (m-space) X = Z0 + A^H opt_S
-    s.optsrc = improved_pre ? (a.msp && s.mzit == a.it ? 3 : 1 + (a.it & 1)) : optsrc;
-    s.kfcum = cum;
-    s.zit = a.it;
-    *st = s;
-    return 1 | (ctl & 2);
-}
-
 // m-space fallback (RealState::msp): the bound failed for an iterate gyk_kernel settled in m-space,
 // so the full Z-step needs Z and X = Z' in memory.  One wave forms them from the implicit form,
 // out = base + A^H v with the f64 A (rare: the bound keeps holding once it holds), and opt_X if
@@ -127,8 +94,9 @@ __device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
         }
         __syncthreads();   // (one wave) the stores are visible to every lane's later loads
     };
-    if (optsrc == 3) {
-        gemv(oX, Z0, reinterpret_cast<const d2*>(a.optS) + om);
+    if (optsrc >= 3 && optsrc <= 5) {   // opt_S, or still in the S buffer Sg[optsrc - 4]
+        const double* sp = optsrc == 3 ? a.optS : ((optsrc - 4) == (a.it & 1) ? a.Snew : a.Sold);
+        gemv(oX, Z0, reinterpret_cast<const d2*>(sp) + om);
     } else if (optsrc == zc_id || optsrc == zn_id) {
         const d2* src = optsrc == zc_id ? Zc : Zn;
         for (int k = lane; k < n; k += 64) oX[k] = src[k];
@@ -144,7 +112,7 @@ __device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
         gemv(Zn, Zn, Sn);
     }
     if (lane == 0) {
-        if (optsrc == 3 || optsrc == zc_id || optsrc == zn_id) st->optsrc = 0;
+        if ((optsrc >= 3 && optsrc <= 5) || optsrc == zc_id || optsrc == zn_id) st->optsrc = 0;
         st->msp = 0;
     }
     __syncthreads();

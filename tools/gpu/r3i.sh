@@ -1,7 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for room in 32 8 2 128; do
-ACE_MSP_ROOM=$room timeout -k 10 600 python3 bench.py --no-cpu-baseline --no-regime-p > gpurun_out/b_$room.json 2> gpurun_out/b.err || { tail -20 gpurun_out/b.err; exit 1; }
-python3 -c "import json;d=json.load(open('gpurun_out/b_$room.json'));print('room $room', d['value'], d['ms_per_step'], d['roofline']['msp_frac'])"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { grep -E "passed|failed|Error|assert" gpurun_out/gputests.log | tail -20; exit 1; }
+tail -1 gpurun_out/gputests.log
+for i in 1 2; do
+timeout -k 10 600 python3 bench.py --no-cpu-baseline --no-regime-p > gpurun_out/b.json 2> gpurun_out/b.err || { tail -20 gpurun_out/b.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/b.json'));print(d['value'], d['ms_per_step'], d['kernels_ms'], d['roofline']['msp_frac'])"
 done

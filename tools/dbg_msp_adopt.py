@@ -1,0 +1,21 @@
+"""m-space adoption: realisation-iterations in m-space form for solves of k iterations (bench unit)."""
+import ctypes as C, sys
+sys.path.insert(0, "2ace-mmwave-channel-estimation_amd")
+import torch
+from ace_amd import infer_admm_batch, synth_problem
+from ace_amd._lib import LIB, check
+batch = 4096
+A, B, X0, _ = synth_problem(7, 0, batch, 256, 32, 32)
+infer_admm_batch(A, B, X0, 32, 32, maxiter=10, fixed_iters=True)
+prev, prevk = 0, 0
+for k in [10, 20, 30, 40, 50, 60, 70, 80, 100, 150, 200]:
+    check(LIB.ace_prof_sample(1000000, 0))
+    check(LIB.ace_prof_start(16))
+    infer_admm_batch(A, B, X0, 32, 32, maxiter=k, fixed_iters=True)
+    torch.cuda.synchronize()
+    kt = (C.c_double * 10)(); kn = (C.c_int32 * 10)()
+    check(LIB.ace_prof_stop(kt, kn))
+    s = C.c_longlong(0)
+    check(LIB.ace_prof_msp_steps(C.byref(s)))
+    print(f"iters {k}: msp steps {s.value}  per-iteration share over ({prevk},{k}]: {(s.value - prev) / (batch * (k - prevk)):.3f}")
+    prev, prevk = s.value, k

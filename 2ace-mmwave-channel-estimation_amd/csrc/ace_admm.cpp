@@ -93,6 +93,13 @@ static double msp_room() {
     return e ? atof(e) : 32.0;
 }
 
+// ACE_COLD_SYNC=<k>: the first k iterations of a split solve run all sub-batches' g launches, then
+// all their Z-steps (cross-stream barriers), instead of each sub-batch's pair in turn.
+static int cold_sync_iters() {
+    const char* e = getenv("ACE_COLD_SYNC");
+    return e ? atoi(e) : 0;
+}
+
 // ACE_MSP_FAIL_IT=<it> (tests): the perturbation bound of every m-space iterate fails at that
 // iteration, so the Z-step materialises Z, Z' and opt_X from the implicit form.
 static int msp_fail_it() {
@@ -335,7 +342,7 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     // Keyed by (device, caller stream), so solves on different caller streams stay independent.
     struct SplitRes {
         hipStream_t s[4];
-        hipEvent_t e[4];
+        hipEvent_t e[4], c[4];
         bool ok;
     };
     static std::map<std::pair<int, hipStream_t>, SplitRes> res;
@@ -343,19 +350,21 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     int dev = 0;
     ACE_HIP(hipGetDevice(&dev));
     std::vector<hipStream_t> ss(nsplit, st);
-    std::vector<hipEvent_t> ev(nsplit);
+    std::vector<hipEvent_t> ev(nsplit), cev(nsplit);
     {
         std::lock_guard<std::mutex> lk(mtx);
         SplitRes& r = res[{dev, st}];
         if (!r.ok) {
             for (int h = 0; h < 4; ++h) {
                 ACE_HIP(hipEventCreateWithFlags(&r.e[h], hipEventDisableTiming));
+                ACE_HIP(hipEventCreateWithFlags(&r.c[h], hipEventDisableTiming));
                 ACE_HIP(hipStreamCreateWithFlags(&r.s[h], hipStreamNonBlocking));
             }
             r.ok = true;
         }
         for (int h = 0; h < nsplit; ++h) {
             ev[h] = r.e[h];
+            cev[h] = r.c[h];
             if (h > 0) ss[h] = r.s[h];
         }
     }
@@ -385,8 +394,22 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
     // m-space steady state (RealState::msp): needs the fused gyf iteration at every iteration
     const bool msp = lean && za0.lazy_dual && fuse_enabled(m) && gyf_enabled(m) && mspace_enabled();
     const DualCtl dc{za0.tol_abs, za0.tol_rel, za0.rho, za0.fixed_iters, n, 1, w.done};
+    // cold iterations (ACE_COLD_SYNC=k: it <= k): the g launches of all sub-batches, then all
+    // Z-steps, with a cross-stream barrier after each group, so that no g work-group waits for
+    // CUs held by another sub-batch's long cold Z-step
+    const int cold_sync = cold_sync_iters();
+    auto barrier = [&]() -> int {
+        for (int h = 0; h < nsplit; ++h) ACE_HIP(hipEventRecord(cev[h], ss[h]));
+        for (int h = 0; h < nsplit; ++h)
+            for (int k = 0; k < nsplit; ++k)
+                if (k != h) ACE_HIP(hipStreamWaitEvent(ss[h], cev[k], 0));
+        return ACE_OK;
+    };
     int q = 0, rc = ACE_OK;
     for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
+        const bool csync = nsplit > 1 && it <= cold_sync;
+      for (int phase = 0; phase < (csync ? 2 : 1); ++phase) {
+        const int pmask = csync ? (1 << phase) : 3;   // bit 0: the g launch, bit 1: the Z-step
         for (int h = 0; h < nsplit; ++h) {
             if (nb[h] == 0) continue;
             const AdmmState& wh = ws[h];
@@ -433,7 +456,8 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
                        L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0,
                        gyf && msp ? 1 : 0, it, za.Sold, wh.Sg[it & 1], wh.optS, za0.np,
                        {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one, msp_room()};
-            if (gyf) {
+            if (!(pmask & 1)) {
+            } else if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, sh);
             } else {
@@ -446,12 +470,14 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
                 launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh, za.xfuse ? &za : nullptr);
             }
             ACE_HIP(stagger_mark(h, it, 3));
-            {
+            if (pmask & 2) {
                 ProfScope ps(ACE_K_ZSTEP, sh);
                 if (lean && !za.xfuse) launch_zlean(za, nb[h], sh);
                 launch_zstep(p.variant, false, za, nb[h], sh);
             }
         }
+        if (csync) ACE_TRY(barrier());
+      }
         q = 1 - q;
         if (!p.fixed_iters && (it % 8 == 0) && it < p.maxiter) {
             for (int h = 0; h < nsplit; ++h) ACE_HIP(hipStreamSynchronize(ss[h]));

@@ -388,9 +388,9 @@ struct ZProfile {
     int rl[4];
     double fl[4];
 };
-__device__ __forceinline__ ZProfile z_profile(const ZArgs& a, int b) {
+__device__ __forceinline__ ZProfile z_profile_flag(const ZArgs& a, int rank_one_b) {   // rank_one[b] given
     ZProfile p;
-    if (a.rank_one && a.rank_one[b]) {
+    if (rank_one_b) {
         p.np = 1;
         p.rl[0] = 1;
         p.fl[0] = 0.95;
@@ -400,6 +400,9 @@ __device__ __forceinline__ ZProfile z_profile(const ZArgs& a, int b) {
         for (int i = 0; i < 4; ++i) { p.rl[i] = a.rl[i]; p.fl[i] = a.fl[i]; }
     }
     return p;
+}
+__device__ __forceinline__ ZProfile z_profile(const ZArgs& a, int b) {
+    return z_profile_flag(a, a.rank_one ? (int)a.rank_one[b] : 0);
 }
 void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st);  // A2only, one wave per realisation
 // steady-state A2only Z-step (wmode, ping-pong, N = 0 on entry) under the perturbation

@@ -121,15 +121,27 @@ __device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
 template <bool INIT>
 __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const int lane = threadIdx.x;
-    const ZProfile pf = z_profile(a, b);
     const int n = a.n, m = a.m, tx = a.tx, rx = a.rx;
     RealState* st = a.st + b;
-    if (!INIT && st->done) return;
-    if (!INIT && a.lean && st->zit == a.it) return;   // zlean_kernel completed this iteration
+    // the three state words the steady state decides on, requested together (one round trip
+    // instead of a chain of dependent loads before the common early exits)
+    // (the empty asm consumes all of them before the first branch, so that the compiler cannot
+    // sink each load below the branch before it: one memory round trip, not four)
+    int s_done = 0, s_zit = 0, s_fzit = 0;
+    if (!INIT) {
+        s_done = st->done;
+        s_zit = st->zit;
+        s_fzit = st->fzit;
+    }
+    const int r1 = a.rank_one ? (int)a.rank_one[b] : 0;
+    asm volatile("" ::"s"(s_done), "s"(s_zit), "s"(s_fzit), "v"(r1));
+    const ZProfile pf = z_profile_flag(a, r1);
+    if (!INIT && s_done) return;
+    if (!INIT && a.lean && s_zit == a.it) return;   // zlean_kernel completed this iteration
     // The fused apply_AH formed X = Z + W of this iteration in Z' with its sums: the perturbation
     // certificate of zlean_kernel, then the iteration control; if the bound fails, the full
     // Z-step below runs on X read from Z'.
-    const bool xin = !INIT && a.xfuse && st->fzit == a.it;
+    const bool xin = !INIT && a.xfuse && s_fzit == a.it;
     if (xin) {
         int ok = 0;
         if (threadIdx.x == 0) ok = fused_control(a, st, pf);

@@ -668,7 +668,8 @@ struct GSet {
 };
 
 template <bool GLDS>   // g stays in the LDS rows of T for the fused apply_AH (gyf_kernel) instead of a.g
-__device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem) {
+__device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem, const ZArgs& za,
+                                         int za_ctl) {
     __shared__ double red[8][GRB][9];
     __shared__ double sc_s[GRB], p2_s[GRB];
     __shared__ int live_s[GRB], imp_s[GRB], avok_s[GRB], oys_s[GRB], pend_s[GRB], msp_s[GRB], ent_s[GRB], oss_s[GRB];
@@ -1134,6 +1135,12 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                     }
                 }
                 if (oss_s[t] == 4 + (a.it & 1)) rs.optsrc = 3;   // (saved to opt_S in the loop above)
+                // the Z-step's certificate and control right here, on the state in place (the
+                // Z-step launch then returns at once for this realisation, RealState::zit); not at
+                // the last iteration, whose pending tests need the one-wave dual_fixup
+                if constexpr (GLDS) {
+                    if (take && za_ctl && !za.fixup_now) fused_control<false>(za, &rs, z_profile(za, j0 + t));
+                }
                 msp_s[t] = take;
             }
         }
@@ -1277,7 +1284,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
 }
 __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    gyk_body<false>(nb, m, a, smem);
+    gyk_body<false>(nb, m, a, smem, ZArgs{}, 0);
 }
 // One iteration's matrix work in one launch (unit path, lazy dual residual, fused Z-step pass):
 // gyk_body (T, g = G T, the Y-step; g left in the LDS rows of T), then the fused apply_AH body
@@ -1286,9 +1293,9 @@ __global__ __launch_bounds__(NT, 1) void gyk_kernel(int nb, int m, GykArgs a) {
 // and the 64 KiB of Z-step partial sums over the T rows when they are large enough, else after.
 __host__ __device__ __forceinline__ size_t gyf_ts_bytes(int m) { return ((size_t)GRB * (gyk_mp(m) + 1) * 16 + 255) & ~(size_t)255; }
 __global__ __launch_bounds__(NT, 1) void gyf_kernel(int nb, int m, int n, GykArgs a, const i4v* __restrict__ LAH,
-                                                    double* __restrict__ Wp, ZArgs za, size_t ad_bytes) {
+                                                    double* __restrict__ Wp, ZArgs za, size_t ad_bytes, int za_ctl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    gyk_body<true>(nb, m, a, smem);
+    gyk_body<true>(nb, m, a, smem, za, za_ctl);
     __syncthreads();
     const size_t ts = gyf_ts_bytes(m);
     int8_t* Ad = reinterpret_cast<int8_t*>(smem + ts);
@@ -1411,8 +1418,12 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     }();
     (void)attr;
     const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
+    static const int ctl = [] {   // ACE_GYF_CTL=0: the Z-step launch runs the m-space control
+        const char* e = getenv("ACE_GYF_CTL");
+        return e ? atoi(e) : 1;
+    }();
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
-                       reinterpret_cast<const i4v*>(LAH), W, za, ad);
+                       reinterpret_cast<const i4v*>(LAH), W, za, ad, ctl);
 }
 // best m-space iterates still in an S ping-pong buffer (optsrc 4 / 5) -> opt_S (optsrc 3)
 __global__ __launch_bounds__(256) void msp_opt_gather_kernel(int m, RealState* rs, const double* S0, const double* S1,

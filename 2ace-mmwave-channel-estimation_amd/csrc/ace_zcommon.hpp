@@ -214,8 +214,13 @@ __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, doubl
 // zlean_kernel; if it holds, Z' = E = X stands, N' = 0, and the control runs.  Returns 0 (nothing
 // written) when the bound fails: the full Z-step must run; else 1, plus 2 when the convergence
 // test is left pending (ZArgs::lazy_dual: at the last iteration the wave runs dual_fixup).
+// COPY: the state is copied to registers in one batch of loads and written back (the one-wave
+// Z-step, scalar loads); otherwise the fields are used in place (gyf_kernel's m-space steps).
+template <bool COPY = true>
 __device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
-    RealState s = *st;   // one batch of loads (the chain below then runs on registers)
+    RealState sc;
+    if constexpr (COPY) sc = *st;
+    RealState& s = COPY ? sc : *st;
     const double s0 = s.fs0, s3 = s.fs3;
     const double cum = (s.kfcum + sqrt(s3)) * (1.0 + 0x1p-40);
     bool pass = s0 > 0.0;
@@ -237,7 +242,7 @@ __device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, cons
     s.optsrc = improved_pre ? (a.msp && s.mzit == a.it ? 4 + (a.it & 1) : 1 + (a.it & 1)) : optsrc;
     s.kfcum = cum;
     s.zit = a.it;
-    *st = s;
+    if constexpr (COPY) *st = sc;
     return 1 | (ctl & 2);
 }
 

@@ -1418,10 +1418,8 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     }();
     (void)attr;
     const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
-    static const int ctl = [] {   // ACE_GYF_CTL=0: the Z-step launch runs the m-space control
-        const char* e = getenv("ACE_GYF_CTL");
-        return e ? atoi(e) : 1;
-    }();
+    const char* ce = getenv("ACE_GYF_CTL");   // 0: the Z-step launch runs the m-space control (read per call)
+    const int ctl = ce ? atoi(ce) : 1;
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad, ctl);
 }

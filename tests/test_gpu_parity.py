@@ -382,6 +382,23 @@ def test_mspace_steps(gpu, monkeypatch, batch, m, tx, fixed, fail_it):
     assert np.array_equal(it1[idx], ito)
 
 
+@pytest.mark.parametrize("fixed", [True, False])
+def test_gyf_control_bit_identical(gpu, monkeypatch, fixed):
+    """The certificate and iteration control of m-space iterates run inside gyf_kernel (default) or
+    in the Z-step launch (ACE_GYF_CTL=0): the same code on the same state, bit-identical results."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(61, 0, 1024, 256, 32, 32)
+    out = {}
+    for c in ("1", "0"):
+        monkeypatch.setenv("ACE_GYF_CTL", c)
+        r = infer_admm_batch(A, B, X0, 32, 32, maxiter=200, fixed_iters=fixed)
+        torch.cuda.synchronize()
+        out[c] = (r.X.cpu().numpy(), r.Y.cpu().numpy(), r.iters.cpu().numpy(), r.status.cpu().numpy())
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("batch,m,tx", [(1000, 256, 32), (1024, 121, 16), (1040, 243, 32)])
 def test_gyf_ragged_batches_and_sizes(gpu, batch, m, tx):
     """gyf_kernel (gyk + fused apply_AH, concurrent sub-batches) on ragged sub-batches (not a

@@ -1,4 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-ACE_LIB=$PWD/tools/libace_dbg.so timeout -k 10 300 python3 tools/dbg_msp1.py 4096 256 32 12 1 > gpurun_out/sweeps.log 2>&1 || { tail gpurun_out/sweeps.log; exit 1; }
-grep -c cold gpurun_out/sweeps.log
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -q -x -k "control_bit or mspace" --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { grep -E "passed|failed|Error|assert" gpurun_out/t.log | tail; exit 1; }
+tail -1 gpurun_out/t.log

@@ -660,7 +660,10 @@ __global__ __launch_bounds__(256) void i8_expand_kernel(int m, int n, const doub
 //   K Y_new on the int8 matrix cores (digit planes of Y_new from LDS, as i8ah_kernel<true>)
 //   the dual terms dY^H (K Y - K Y0), Y^H K Y and the opt_Y copy
 // so that neither the Z-step nor a separate K Y launch touches Y or K Y again.
-constexpr int GSK = 4;          // f64 K-steps (4 complex each) per pipeline stage
+#ifndef ACE_GSK
+#define ACE_GSK 4
+#endif
+constexpr int GSK = ACE_GSK;          // f64 K-steps (4 complex each) per pipeline stage
 constexpr int GRB = 16;         // realisations per work-group (one f64 MFMA row tile)
 __host__ __device__ __forceinline__ int gyk_mp(int m) { return (m + 31) & ~31; }
 struct GSet {

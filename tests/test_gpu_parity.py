@@ -383,6 +383,29 @@ def test_mspace_steps(gpu, monkeypatch, batch, m, tx, fixed, fail_it):
 
 
 @pytest.mark.parametrize("fixed", [True, False])
+def test_mspace_frequent_fallbacks(gpu, monkeypatch, fixed):
+    """m-space entry with almost no margin (ACE_MSP_ROOM=1): realisations enter the implicit form
+    as soon as the bound holds and many fall back soon after, so the Z-step materialises Z, Z' and
+    opt_X (from opt_S, or from an S ping-pong buffer) at many different iterations.  Against the
+    memory form: equal to rounding, identical iteration counts and flags."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(67, 0, 512, 256, 32, 32)
+    out = {}
+    for msp in ("0", "1"):
+        monkeypatch.setenv("ACE_MSPACE", msp)
+        monkeypatch.setenv("ACE_MSP_ROOM", "1")
+        r = infer_admm_batch(A, B, X0, 32, 32, maxiter=200, fixed_iters=fixed)
+        torch.cuda.synchronize()
+        out[msp] = (r.X.cpu().numpy(), r.Y.cpu().numpy(), r.iters.cpu().numpy(), r.status.cpu().numpy())
+    assert np.isfinite(out["1"][0]).all()
+    assert _errs(out["1"][0], out["0"][0]).max() <= 1e-10
+    assert _errs(out["1"][1], out["0"][1]).max() <= 1e-10
+    assert np.array_equal(out["1"][2], out["0"][2])
+    assert np.array_equal(out["1"][3], out["0"][3])
+
+
+@pytest.mark.parametrize("fixed", [True, False])
 def test_gyf_control_bit_identical(gpu, monkeypatch, fixed):
     """The certificate and iteration control of m-space iterates run inside gyf_kernel (default) or
     in the Z-step launch (ACE_GYF_CTL=0): the same code on the same state, bit-identical results."""

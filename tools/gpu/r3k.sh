@@ -1,6 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-for L in 2ace-mmwave-channel-estimation_amd/ace_amd/libace.so tools/libace_gsk2.so 2ace-mmwave-channel-estimation_amd/ace_amd/libace.so tools/libace_gsk2.so; do
-ACE_LIB=$PWD/$L timeout -k 10 600 python3 bench.py --no-cpu-baseline --no-regime-p > gpurun_out/b.json 2> gpurun_out/b.err || { tail -20 gpurun_out/b.err; exit 1; }
-python3 -c "import json;d=json.load(open('gpurun_out/b.json'));print('$L', d['value'], d['ms_per_step'], d['kernels_ms']['apply_G'])"
-done
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -q -x -k "frequent or mspace" --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 || { grep -E "passed|failed|Error|assert" gpurun_out/t.log | tail; exit 1; }
+tail -1 gpurun_out/t.log

@@ -6,7 +6,9 @@ not been built (there is no CPU fallback on the product path).
 from ._lib import LIB, AceError, AdmmCfg, default_cfg  # noqa: F401
 from ._lib import (ACE_VARIANT_A2ONLY, ACE_VARIANT_NUCLEAR, ACE_ST_CONVERGED, ACE_ST_NO_OPT,  # noqa: F401
                    ACE_ST_EIG_NOCONV, ACE_ST_ROLLBACK, PipelineCfg, pipeline_cfg)
-from .solver import InferADMM, infer_admm_batch, infer_admm_host, synth_problem, BatchResult  # noqa: F401
+from .solver import (InferADMM, infer_admm_batch, infer_admm_host, synth_problem, BatchResult,  # noqa: F401
+                     nuclear_prox_batch)
+from ._lib import path_counts  # noqa: F401
 from .pipeline import (inferLowRankV4_multi, inferLowRankV4, inferLowRank_Nuclear,  # noqa: F401
                        infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, draw_partitions,
                        PipelineResult)

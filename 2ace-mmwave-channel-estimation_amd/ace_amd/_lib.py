@@ -113,6 +113,10 @@ def _load():
     lib.ace_prof_stop.restype = C.c_int
     lib.ace_prof_msp_steps.argtypes = [C.POINTER(C.c_longlong)]
     lib.ace_prof_msp_steps.restype = C.c_int
+    lib.ace_nuclear_prox_batch.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]
+    lib.ace_nuclear_prox_batch.restype = C.c_int
+    lib.ace_path_counts.argtypes = [C.POINTER(C.c_int64), C.c_int]
+    lib.ace_path_counts.restype = C.c_int
     lib.ace_last_error.argtypes = []
     lib.ace_last_error.restype = C.c_char_p
     lib.ace_version.argtypes = []
@@ -127,6 +131,16 @@ def check(rc):
     if rc != ACE_OK:
         raise AceError(rc, LIB.ace_last_error().decode())
     return rc
+
+
+PATHS = ("int8_shared", "codes_private", "f64_shared", "f64_private")
+
+
+def path_counts(reset=False):
+    """InferADMM solves per apply path since the last reset (ace_path_counts)."""
+    v = (C.c_int64 * 4)()
+    check(LIB.ace_path_counts(v, int(bool(reset))))
+    return dict(zip(PATHS, v))
 
 
 def default_cfg(**kw) -> AdmmCfg:

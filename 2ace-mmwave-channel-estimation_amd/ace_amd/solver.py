@@ -166,6 +166,23 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
     return out
 
 
+def nuclear_prox_batch(E, tau, *, out=None, stream=None):
+    """Z_b = U Shrink(S, tau) V^H of each n x r matrix E_b (inferLowRank_Nuclear.m:411-439, the
+    A2nuclear Z-prox) on the GPU.  E: torch complex128 device tensor [batch][r][n] (column j of
+    realisation b contiguous, the solver's state layout), r <= 32."""
+    import torch
+    if not E.is_cuda or E.dtype != torch.complex128 or E.dim() != 3:
+        raise TypeError("E must be a complex128 device tensor [batch][r][n]")
+    E = E.contiguous()
+    batch, r, n = E.shape
+    if out is None:
+        out = torch.empty_like(E)
+    if stream is None:
+        stream = torch.cuda.current_stream(E.device)
+    check(LIB.ace_nuclear_prox_batch(batch, n, r, E.data_ptr(), float(tau), out.data_ptr(), stream.cuda_stream))
+    return out
+
+
 def synth_problem(seed, first, count, m, tx, rx, *, a_shared=True, L=3, snr_db=30.0, x0_noise=0.5,
                   device="cuda", stream=None):
     """Generate a synthetic batch directly in HBM (ace_synth_codebook/ace_synth_channels)."""

@@ -59,59 +59,51 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->allow_i8 = true;
 }
 
-// ACE_ZCOMPACT=<it>: from that iteration on the Z-step launches in its compact form
-// (zstep1w_compact_kernel: one wave per 8 realisations, the control on the lanes, fallbacks one
-// after another).  Measured neutral against one wave per realisation (r02: the launch is bound by
-// its dependent state round trips, not by the wave count), so off by default (0).
-static int zcompact_after() {   // (read per call: tests switch it within one process)
-    const char* e = getenv("ACE_ZCOMPACT");
-    return e ? atoi(e) : 0;
+// A/B and test switches, read from the environment once per solve (tests change them between
+// solves in one process; nothing on the iteration path calls getenv):
+//   ACE_ZCOMPACT=<it>   from that iteration on the Z-step launches in its compact form
+//                       (zstep1w_compact_kernel: one wave per 8 realisations; measured neutral, off)
+//   ACE_FUSE=0          the lean Z-step as its own launch instead of in apply_AH's epilogue
+//   ACE_GYF=0           gyk_kernel and the fused apply_AH as two launches instead of gyf_kernel
+//   ACE_GYF_CTL=0       the Z-step launch, not gyf_kernel, runs the m-space control
+//   ACE_MSPACE=0        Z stays in memory through the steady state (no m-space steps, RealState::msp)
+//   ACE_MSP_ROOM=<k>    a realisation enters the m-space form only if the perturbation bound would
+//                       still hold after k more steps of the current size (default 32)
+//   ACE_COLD_SYNC=<k>   the first k iterations of a split solve run all sub-batches' g launches, then
+//                       all their Z-steps (cross-stream barriers)
+//   ACE_MSP_FAIL_IT=<i> (tests) the perturbation bound of every m-space iterate fails at iteration i,
+//                       so the Z-step materialises Z, Z' and opt_X from the implicit form
+//   ACE_LAZY_DUAL=0     K Y in gyk_kernel every iteration
+//   ACE_LEAN=0          the full one-wave Z-step every iteration (no zlean / certified pass)
+struct Knobs {
+    int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1;
+    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true;
+    double msp_room = 32.0;
+};
+static Knobs read_knobs() {
+    Knobs k;
+    const auto on = [](const char* name) {
+        const char* e = getenv(name);
+        return !(e && e[0] == '0');
+    };
+    const auto num = [](const char* name, double dflt) {
+        const char* e = getenv(name);
+        return e ? atof(e) : dflt;
+    };
+    k.zcompact = (int)num("ACE_ZCOMPACT", 0);
+    k.cold_sync = (int)num("ACE_COLD_SYNC", 0);
+    k.msp_fail_it = (int)num("ACE_MSP_FAIL_IT", -1);
+    k.gyf_ctl = (int)num("ACE_GYF_CTL", 1);
+    k.msp_room = num("ACE_MSP_ROOM", 32.0);
+    k.fuse = on("ACE_FUSE");
+    k.gyf = on("ACE_GYF");
+    k.mspace = on("ACE_MSPACE");
+    k.lazy_dual = on("ACE_LAZY_DUAL");
+    k.lean = on("ACE_LEAN");
+    return k;
 }
-
-// ACE_FUSE=0 runs the lean Z-step as its own launch instead of in apply_AH's epilogue.
-static bool fuse_enabled(int m) {
-    const char* e = getenv("ACE_FUSE");
-    return !(e && e[0] == '0') && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192;
-}
-// ACE_GYF=0 runs gyk_kernel and the fused apply_AH as two launches instead of gyf_kernel.
-static bool gyf_enabled(int m) {
-    const char* e = getenv("ACE_GYF");
-    return !(e && e[0] == '0') && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN;
-}
-
-// ACE_MSPACE=0 keeps Z in memory through the steady state (no m-space steps, RealState::msp).
-static bool mspace_enabled() {
-    const char* e = getenv("ACE_MSPACE");
-    return !(e && e[0] == '0');
-}
-
-// ACE_MSP_ROOM=<k>: a realisation enters the m-space form only if the perturbation bound would
-// still hold after k more steps of the current size (default 32; entries that fail soon after
-// cost a materialisation in the Z-step).
-static double msp_room() {
-    const char* e = getenv("ACE_MSP_ROOM");
-    return e ? atof(e) : 32.0;
-}
-
-// ACE_COLD_SYNC=<k>: the first k iterations of a split solve run all sub-batches' g launches, then
-// all their Z-steps (cross-stream barriers), instead of each sub-batch's pair in turn.
-static int cold_sync_iters() {
-    const char* e = getenv("ACE_COLD_SYNC");
-    return e ? atoi(e) : 0;
-}
-
-// ACE_MSP_FAIL_IT=<it> (tests): the perturbation bound of every m-space iterate fails at that
-// iteration, so the Z-step materialises Z, Z' and opt_X from the implicit form.
-static int msp_fail_it() {
-    const char* e = getenv("ACE_MSP_FAIL_IT");
-    return e ? atoi(e) : -1;
-}
-
-// ACE_LAZY_DUAL=0 keeps K Y in gyk_kernel every iteration (A/B comparisons); read per solve.
-static bool lazy_dual_enabled() {
-    const char* e = getenv("ACE_LAZY_DUAL");
-    return !(e && e[0] == '0');
-}
+static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192; }
+static bool gyf_ok(const Knobs& k, int m) { return k.gyf && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN; }
 
 // ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
 static bool i8_disabled() {
@@ -221,7 +213,11 @@ int ns_inverse(LinOps& L, hipStream_t st) {
 static int pc_setup(LinOps& L, int batch, hipStream_t st) {
     const int m = L.m, n = L.n;
     L.pc_ok = false;
-    if (L.shared || !L.pcodes || !L.allow_i8 || i8_disabled() || !pc_supported(m, n) || batch != L.batch) return ACE_OK;
+    // (the code-image iteration needs the one-wave Z-step that forms X from W = A^H g; the four-wave
+    // A/B kernel would make admm_run take the generic path, which reads K and G as matrices)
+    if (L.shared || !L.pcodes || !L.allow_i8 || i8_disabled() || !pc_supported(m, n) || batch != L.batch ||
+        !zstep_takes_w(ACE_VARIANT_A2ONLY, 1))
+        return ACE_OK;
     ACE_HIP(hipMemsetAsync(L.pcflag, 0, sizeof(int), st));
     launch_pc_pack(batch, m, n, L.A, L.pcb, L.pcodes, L.pcflag, st);
     int flag = 1;
@@ -331,37 +327,66 @@ static AdmmState state_slice(const AdmmState& w, long long ob, int m, int n, int
     return h;
 }
 
-int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w, const ZArgs& za0, int batch,
-                       const double* B, int nsplit, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
-                       double* mu_out, hipStream_t st) {
+static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w, const ZArgs& za0, int batch,
+                              const double* B, int nsplit, const Knobs& kn, double* Xo, double* Yo, int32_t* iters,
+                              uint32_t* status, double* mu_out, hipStream_t st) {
     const int m = L.m, n = L.n;
     const int chunk = (batch / nsplit + 15) & ~15;
-    // The sub-batch streams and fork / join events live as long as the process (one set per device):
-    // destroying a stream waits for its work, which would make every solve block the host until the
-    // GPU finishes it (measured: a 0.7 ms idle gap before the next solve's first kernel).
-    // Keyed by (device, caller stream), so solves on different caller streams stay independent.
+    // The sub-batch streams and fork / join events outlive the solve (one set per device and caller
+    // stream): destroying a stream waits for its work, which would make every solve block the host
+    // until the GPU finishes it (measured: a 0.7 ms idle gap before the next solve's first kernel).
+    // Keyed by (device, caller stream), so solves on different caller streams stay independent; at
+    // most kSplitSets sets are kept, the least recently used one is released when a new caller
+    // stream needs a set (a caller that makes a stream per solve recycles them).  A set only holds
+    // library-owned streams, so a caller stream handle that is destroyed and reused stays correct.
     struct SplitRes {
-        hipStream_t s[4];
-        hipEvent_t e[4], c[4];
-        bool ok;
+        hipStream_t s[4] = {};
+        hipEvent_t e[4] = {}, c[4] = {};
+        unsigned long long used = 0;
     };
+    constexpr size_t kSplitSets = 8;
     static std::map<std::pair<int, hipStream_t>, SplitRes> res;
+    static unsigned long long tick = 0;
     static std::mutex mtx;
+    const auto release = [](SplitRes& r) {
+        for (int h = 0; h < 4; ++h) {
+            if (r.s[h]) (void)hipStreamDestroy(r.s[h]);
+            if (r.e[h]) (void)hipEventDestroy(r.e[h]);
+            if (r.c[h]) (void)hipEventDestroy(r.c[h]);
+        }
+        r = SplitRes{};
+    };
     int dev = 0;
     ACE_HIP(hipGetDevice(&dev));
     std::vector<hipStream_t> ss(nsplit, st);
     std::vector<hipEvent_t> ev(nsplit), cev(nsplit);
     {
         std::lock_guard<std::mutex> lk(mtx);
-        SplitRes& r = res[{dev, st}];
-        if (!r.ok) {
-            for (int h = 0; h < 4; ++h) {
-                ACE_HIP(hipEventCreateWithFlags(&r.e[h], hipEventDisableTiming));
-                ACE_HIP(hipEventCreateWithFlags(&r.c[h], hipEventDisableTiming));
-                ACE_HIP(hipStreamCreateWithFlags(&r.s[h], hipStreamNonBlocking));
+        const auto key = std::make_pair(dev, st);
+        auto it = res.find(key);
+        if (it == res.end()) {
+            if (res.size() >= kSplitSets) {
+                auto lru = res.begin();
+                for (auto i = res.begin(); i != res.end(); ++i)
+                    if (i->second.used < lru->second.used) lru = i;
+                release(lru->second);
+                res.erase(lru);
             }
-            r.ok = true;
+            SplitRes r;
+            hipError_t e = hipSuccess;
+            for (int h = 0; h < 4 && e == hipSuccess; ++h) {
+                e = hipEventCreateWithFlags(&r.e[h], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&r.c[h], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipStreamCreateWithFlags(&r.s[h], hipStreamNonBlocking);
+            }
+            if (e != hipSuccess) {
+                release(r);
+                return fail(ACE_ERR_HIP, "sub-batch streams: %s", hipGetErrorString(e));
+            }
+            it = res.emplace(key, r).first;
         }
+        SplitRes& r = it->second;
+        r.used = ++tick;
         for (int h = 0; h < nsplit; ++h) {
             ev[h] = r.e[h];
             cev[h] = r.c[h];
@@ -390,14 +415,14 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
         return (evs && h == 0 && it == 1 && k == stg) ? hipEventRecord(evs, ss[0]) : hipSuccess;
     };
     // steady-state Z-steps under the perturbation certificate (zlean_kernel), A2only only
-    const bool lean = p.variant != ACE_VARIANT_NUCLEAR && za0.warm && za0.Q && zlean_enabled();
+    const bool lean = p.variant != ACE_VARIANT_NUCLEAR && za0.warm && za0.Q && kn.lean;
     // m-space steady state (RealState::msp): needs the fused gyf iteration at every iteration
-    const bool msp = lean && za0.lazy_dual && fuse_enabled(m) && gyf_enabled(m) && mspace_enabled();
+    const bool msp = lean && za0.lazy_dual && fuse_ok(kn, m) && gyf_ok(kn, m) && kn.mspace;
     const DualCtl dc{za0.tol_abs, za0.tol_rel, za0.rho, za0.fixed_iters, n, 1, w.done};
     // cold iterations (ACE_COLD_SYNC=k: it <= k): the g launches of all sub-batches, then all
     // Z-steps, with a cross-stream barrier after each group, so that no g work-group waits for
     // CUs held by another sub-batch's long cold Z-step
-    const int cold_sync = cold_sync_iters();
+    const int cold_sync = kn.cold_sync;
     auto barrier = [&]() -> int {
         for (int h = 0; h < nsplit; ++h) ACE_HIP(hipEventRecord(cev[h], ss[h]));
         for (int h = 0; h < nsplit; ++h)
@@ -439,27 +464,27 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
             za.fixup_now = it == p.maxiter;
             za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
             za.lean = lean;
-            za.compact = lean && zcompact_after() > 0 && it > zcompact_after() && it != p.maxiter;
+            za.compact = lean && kn.zcompact > 0 && it > kn.zcompact && it != p.maxiter;
             // the steady-state Z-step in apply_AH's epilogue (not at the last iteration, whose
             // pending convergence tests the one-wave kernels finish, unless m-space steps are on:
             // their realisations have no Z in memory, and the fused control runs dual_fixup)
-            za.xfuse = lean && (it != p.maxiter || msp) && fuse_enabled(m);
+            za.xfuse = lean && (it != p.maxiter || msp) && fuse_ok(kn, m);
             za.msp = msp;
             za.Af = L.A;
             za.Sold = wh.Sg[(it + 1) & 1];
             za.Snew = wh.Sg[it & 1];
             za.optS = wh.optS;
-            za.msp_fail_it = msp_fail_it();
+            za.msp_fail_it = kn.msp_fail_it;
             // and apply_AH in the same launch as gyk (g stays on chip)
-            const bool gyf = za.xfuse && za0.lazy_dual && gyf_enabled(m);
+            const bool gyf = za.xfuse && za0.lazy_dual && gyf_ok(kn, m);
             GykArgs ga{L.Gf, wh.T, Bh, wh.Y[q], wh.M, wh.Y[1 - q], wh.g, wh.KY[q], wh.KY[1 - q], wh.optY,
                        L.LK8, L.c8, wh.st, wh.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za0.lazy_dual, dc, gyf ? 1 : 0,
                        gyf && msp ? 1 : 0, it, za.Sold, wh.Sg[it & 1], wh.optS, za0.np,
-                       {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one, msp_room()};
+                       {za0.fl[0], za0.fl[1], za0.fl[2], za0.fl[3]}, za.rank_one, kn.msp_room};
             if (!(pmask & 1)) {
             } else if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
-                launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, sh);
+                launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, kn.gyf_ctl, sh);
             } else {
                 {
                     ProfScope ps(ACE_K_APPLY_G, sh);
@@ -480,9 +505,13 @@ int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmState& w,
       }
         q = 1 - q;
         if (!p.fixed_iters && (it % 8 == 0) && it < p.maxiter) {
-            for (int h = 0; h < nsplit; ++h) ACE_HIP(hipStreamSynchronize(ss[h]));
+            for (int h = 1; h < nsplit; ++h) {   // (the caller's stream waits for the sub-batches)
+                ACE_HIP(hipEventRecord(cev[h], ss[h]));
+                ACE_HIP(hipStreamWaitEvent(st, cev[h], 0));
+            }
             int h_done = 0;
-            ACE_HIP(hipMemcpy(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost));
+            ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
+            ACE_HIP(hipStreamSynchronize(st));
             if (h_done >= batch) break;
         }
     }
@@ -510,6 +539,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
              const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu_out,
              hipStream_t st) {
     const int m = L.m, n = L.n, r = p.r;
+    const Knobs kn = read_knobs();
     if (!L.shared && r != 1) return fail(ACE_ERR_UNSUPPORTED, "private sensing matrices support r = 1 only");
     const int row_mode = (r == 1) ? 1 : p.row_mode;   // the two modes coincide at r = 1
     const int nv = batch * r;                         // vectors per apply
@@ -522,6 +552,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // private phase-code codebooks: T, g = G T, Y-step, W = A^H g and the dual terms in one kernel
     const bool pc = !L.shared && L.pc_ok && r == 1 && zstep_takes_w(p.variant, r);
     const bool wmode = i8 || pc;
+    g_path[i8 ? 0 : pc ? 1 : L.shared ? 2 : 3].fetch_add(1, std::memory_order_relaxed);
+    // pc_ok means K and G hold the code-image path's tiles, not the m x m matrices the generic path reads
+    if (L.pc_ok && !pc) return fail(ACE_ERR_UNSUPPORTED, "private phase-code setup without its iteration path");
 
     auto applyA = [&](int mode, const double* Vin, double* C, const double* E) {  // C = E (-) A Vin
         if (L.shared) launch_zgemm(mode, false, m, n, nv, L.A, n, 0, Vin, n, 0, C, E, m, 0, 1, st);
@@ -566,7 +599,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.nuclear = p.variant == ACE_VARIANT_NUCLEAR;
     // the fused g / Y-step kernel skips K Y; the Z-step forms the dual terms when the convergence
     // test needs them (RealState::dpend), from the shared f64 K
-    za.lazy_dual = (gyk && lazy_dual_enabled()) ? 1 : 0;
+    za.lazy_dual = (gyk && kn.lazy_dual) ? 1 : 0;
     za.Kf = L.K;
 
     // ---- init (:296-310)
@@ -586,7 +619,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     int q = 0;
     const int poll = 8;
     const int nsplit = gyk ? split_count(batch) : 1;
-    if (nsplit > 1 || (gyk && mspace_enabled() && p.variant != ACE_VARIANT_NUCLEAR)) return admm_iterate_split(L, p, w, za, batch, B, nsplit, Xo, Yo, iters, status, mu_out, st);
+    if (nsplit > 1 || (gyk && kn.mspace && p.variant != ACE_VARIANT_NUCLEAR))
+        return admm_iterate_split(L, p, w, za, batch, B, nsplit, kn, Xo, Yo, iters, status, mu_out, st);
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
@@ -635,8 +669,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         if (!pc) {
             ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
             if (wmode) {
-                za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled() &&
-                           it != p.maxiter && fuse_enabled(m);
+                za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && kn.lean &&
+                           it != p.maxiter && fuse_ok(kn, m);
                 if (za.xfuse) {   // the fused kernel needs this iteration's Z-step arguments
                     za.it = it;
                     za.wmode = 1;
@@ -665,9 +699,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.Yold = w.Y[q];
         za.KYnew = w.KY[1 - q];
         za.KYold = w.KY[q];
-        za.lean = wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && zlean_enabled();
+        za.lean = wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && kn.lean;
         za.fixup_now = it == p.maxiter;
-        za.compact = za.lean && zcompact_after() > 0 && it > zcompact_after();
+        za.compact = za.lean && kn.zcompact > 0 && it > kn.zcompact;
         {
             ProfScope ps(ACE_K_ZSTEP, st);
             if (za.lean && !za.xfuse) launch_zlean(za, batch, st);

@@ -62,6 +62,15 @@ int ace_prof_msp_steps(long long* steps) {
     return ACE_OK;
 }
 
+int ace_path_counts(int64_t* counts, int reset) {
+    g_err.clear();
+    for (int k = 0; k < 4; ++k) {
+        const long long v = reset ? g_path[k].exchange(0) : g_path[k].load();
+        if (counts) counts[k] = v;
+    }
+    return ACE_OK;
+}
+
 int ace_prof_stop(double* total_ms, int32_t* launches) {
     g_err.clear();
     g_prof.on = false;
@@ -204,6 +213,17 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
     if (mu) ACE_HIPC(hipMemcpy(mu, dM, 8 * (size_t)batch, hipMemcpyDeviceToHost));
 #undef ACE_HIPC
     cleanup();
+    return ACE_OK;
+}
+
+int ace_nuclear_prox_batch(int batch, int n, int r, const double* E, double tau, double* Z, void* stream) {
+    g_err.clear();
+    if (!E || !Z) return fail(ACE_ERR_ARG, "NULL buffer");
+    if (batch < 1 || n < 1 || r < 1) return fail(ACE_ERR_ARG, "batch/n/r must be >= 1 (got %d/%d/%d)", batch, n, r);
+    if (r > 32 || n > 4096) return fail(ACE_ERR_UNSUPPORTED, "nuclear prox needs r <= 32 and n <= 4096 (got %d, %d)", r, n);
+    if (!(tau > 0) || !std::isfinite(tau)) return fail(ACE_ERR_ARG, "tau must be finite and > 0");
+    const int e = launch_nuclear_prox(batch, n, r, E, tau, Z, (hipStream_t)stream);
+    if (e) return fail(ACE_ERR_HIP, "nuclear prox: %s", hipGetErrorString((hipError_t)e));
     return ACE_OK;
 }
 

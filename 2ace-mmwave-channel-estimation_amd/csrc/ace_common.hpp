@@ -255,7 +255,9 @@ struct GykArgs {
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st);
 // gyk + the fused apply_AH (Z-step pass) in one launch; needs a.lazy and a.glds
 size_t gyf_lds_bytes(int m);
-void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, hipStream_t st);
+// ctl = 0: the Z-step launch, not gyf_kernel, runs the m-space control (ACE_GYF_CTL, A/B)
+void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, int ctl,
+                hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);
@@ -380,6 +382,9 @@ void launch_zgemm_ystep(int m, int nb, const double* G, const double* T, double*
                         const RealState* rs, hipStream_t st);
 
 void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t st);
+// Z_b = U soft(S, tau) V^H of the n x r matrices E_b ([b][r][n] c128, r <= 32): the r-general
+// nuclear Z-prox kernel in its init form.  Returns 0 or a hipError_t.
+int launch_nuclear_prox(int batch, int n, int r, const double* E, double tau, double* Z, hipStream_t st);
 bool zstep_takes_w(int variant, int r);
 
 // ArgMinZ rank profile of realisation b (inferLowRankV4_multi.m:437-464; use_rank_one -> :448-450).
@@ -408,7 +413,6 @@ void launch_zstep1w(bool init, const ZArgs& a, int batch, hipStream_t st);  // A
 // steady-state A2only Z-step (wmode, ping-pong, N = 0 on entry) under the perturbation
 // certificate (RealState::kf); realisations it cannot certify are left to launch_zstep1w
 void launch_zlean(const ZArgs& a, int batch, hipStream_t st);
-bool zlean_enabled();
 void launch_pre(int n, int m, int batch, const double* Z, const double* N, const double* Y, const double* M, double* V,
                 double* S, const RealState* rs, hipStream_t st);
 void launch_ystep(int m, int batch, const double* S, const double* g, double* M, const double* B, const double* Yold,

@@ -22,6 +22,9 @@
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
 
 #include "ace_host.hpp"
 
@@ -36,6 +39,11 @@ const uint64_t kSeeds[40] = {58659179, 42737934, 36326041, 89830260, 90710947, 9
                              99245881, 19650488, 5314224,  98859252, 60803022, 76056701, 14112116, 64027813,
                              73073690, 6288587,  42217659, 45632040, 7495955,  31960297, 92863244, 93081516};
 const uint64_t kNuclearSeeds[4] = {1024, 2048, 4096, 8192};   // ..._A2nuclear.m:103
+
+// multiresolution tiers (..._multiresolution.m:111-112, :137-144): rows [0, 1984) are the
+// 4-antenna-group probes, then 3968 2-antenna-group probes, then 3968 per-antenna probes
+const int kTierLen[3] = {1984, 3968, 3968};
+int multires_tier(int M) { return M <= 96 ? 0 : (M <= 256 ? 1 : 2); }
 
 // splitmix64 counter RNG (the same construction as ace_synth.hip / ace_amd.synth)
 uint64_t sm64(uint64_t seed, uint64_t stream, uint64_t ctr) {
@@ -69,6 +77,128 @@ int m_sweep(int tx, int rx, int32_t* M) {
         M[i] = (int32_t)(r * r);
     }
     return 8;
+}
+
+
+// exp(1j*angle) with the components MATLAB's phase-code angles leave a rounding residue in
+// (cos(pi/2) = 6.1e-17, sin(pi) = 1.2e-16) snapped to the exact 0 / +-1 they stand for: within
+// 4 ulp of 1 for |value| ~ 1 and 1e-15 for |value| ~ 0, i.e. a change below 1e-15 of the amplitude.
+// A phase-code codebook passed as |cb| / angle(cb) (main.py:301-302) is then the exact phase
+// code again, whose applies run as int8 digit planes; any other codebook moves
+// by less than the rounding of its own cos / sin.
+inline double snap_unit(double v) {
+    if (std::fabs(v) < 1e-15) return 0.0;
+    if (std::fabs(std::fabs(v) - 1.0) <= 4 * 2.220446049250313e-16) return std::copysign(1.0, v);
+    return v;
+}
+
+// A resident device buffer set for one sweep point, released on every exit path.
+struct DevBufs {
+    std::vector<void*> p;
+    hipStream_t st = nullptr;
+    hipError_t alloc(size_t bytes, void** q) {
+        hipError_t e = hipMalloc(q, bytes);
+        if (e == hipSuccess) p.push_back(*q);
+        return e;
+    }
+    ~DevBufs() {
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+        for (void* q : p) (void)hipFree(q);
+    }
+};
+
+// One sweep point i (M rows): rows, cb_train / rss_train, the solve, H row (:137-178).
+int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
+                const double* rss_dbm, uint64_t seed, int i, int M, int dev, double* H_amp, double* H_angle) {
+    g_err.clear();
+    ACE_HIP(hipSetDevice(dev));
+    const int n = tx * rx;
+    ace_pipeline_cfg cfg;
+    ace_pipeline_cfg_default(&cfg, driver == ACE_DRIVER_A2NUCLEAR ? ACE_VARIANT_NUCLEAR : ACE_VARIANT_A2ONLY);
+    // ---- :137 M_idx = randperm(length(rss_final), M) (multiresolution: within its tier)
+    std::vector<int32_t> idx(M);
+    int avail = P, off = 0;
+    if (driver == ACE_DRIVER_MULTIRES) {
+        const int t = multires_tier(M);
+        avail = kTierLen[t];
+        for (int k = 0; k < t; ++k) off += kTierLen[k];
+    }
+    randperm_k(seed, 0x100 + 2 * (uint64_t)i, avail, M, idx.data());
+    // ---- :120, :138-139 cb_train (row-major M x n c128), rss_train
+    std::vector<double> A(2 * (size_t)M * n), B(M);
+    for (int r = 0; r < M; ++r) {
+        const int row = idx[r] + off;
+        for (int k = 0; k < n; ++k) {
+            const double a = cb_amp[(size_t)row * n + k], ph = cb_angle[(size_t)row * n + k];
+            A[2 * ((size_t)r * n + k)] = a * snap_unit(std::cos(ph));
+            A[2 * ((size_t)r * n + k) + 1] = a * snap_unit(std::sin(ph));
+        }
+        B[r] = std::sqrt(std::pow(10.0, rss_dbm[row] / 10.0) / 1000.0) * kRssFct;   // db2pow
+    }
+    std::vector<double> X(2 * (size_t)n);
+    if (driver != ACE_DRIVER_PHASELIFT) {
+        const int r = std::min(std::min(cfg.r, M), n);
+        const int mt = (int)std::floor(M * cfg.cc_frac);
+        if (mt < r) {
+            // ill-posed sweep point (fewer train rows than spectral columns, e.g. M = 4):
+            // reported as NaN -> 0 like a failed MATLAB recovery (H_out(isnan) = 0, :176)
+            for (int k = 0; k < n; ++k) H_amp[k] = H_angle[k] = 0.0;
+            return ACE_OK;
+        }
+    }
+    DevBufs d;
+    ACE_HIP(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
+    void *dA, *dB, *dX, *dY, *dW;
+    const size_t nA = 16 * (size_t)M * n, nB = 8 * (size_t)M, nX = 16 * (size_t)n, nY = 16 * (size_t)M;
+    if (driver == ACE_DRIVER_PHASELIFT) {
+        // ---- Recover_Channel.m:32-35: MyPhaseLift((meas/2e5).^2*1e10, beams)/sqrt(1e10)*2e5
+        ace_phaselift_cfg pcfg;
+        ace_phaselift_cfg_default(&pcfg);
+        for (int r = 0; r < M; ++r) B[r] = (B[r] / 2e5) * (B[r] / 2e5) * 1e10;
+        const size_t ws = ace_phaselift_workspace_size(&pcfg, 1, M, n);
+        if (!ws) return fail(ACE_ERR_UNSUPPORTED, "phaselift: unsupported size M = %d, n = %d", M, n);
+        ACE_HIP(d.alloc(nA, &dA));
+        ACE_HIP(d.alloc(nB, &dB));
+        ACE_HIP(d.alloc(nX, &dX));
+        ACE_HIP(d.alloc(ws, &dW));
+        ACE_HIP(hipMemcpyAsync(dA, A.data(), nA, hipMemcpyHostToDevice, d.st));
+        ACE_HIP(hipMemcpyAsync(dB, B.data(), nB, hipMemcpyHostToDevice, d.st));
+        ACE_TRY(ace_phaselift_solve_batch(&pcfg, 1, M, n, (const double*)dA, (const double*)dB, (double*)dX, nullptr,
+                                          nullptr, dW, ws, d.st));
+        ACE_HIP(hipMemcpyAsync(X.data(), dX, nX, hipMemcpyDeviceToHost, d.st));
+        ACE_HIP(hipStreamSynchronize(d.st));
+        for (int k = 0; k < 2 * n; ++k) X[k] = X[k] / std::sqrt(1e10) * 2e5;
+    } else {
+        // ---- Recover_Channel -> ADMM_v2(..., 4): the pipeline with its own train partitions
+        const int mt = (int)std::floor(M * cfg.cc_frac);
+        std::vector<int32_t> tr((size_t)cfg.restarts * mt);
+        for (int s = 0; s < cfg.restarts; ++s)
+            randperm_k(seed, 0x101 + 2 * (uint64_t)i + 0x10000 * (uint64_t)s, M, mt, tr.data() + (size_t)s * mt);
+        const size_t ws = ace_pipeline_workspace_size(&cfg, 1, M, n);
+        if (!ws) return fail(ACE_ERR_UNSUPPORTED, "pipeline: unsupported size M = %d, n = %d", M, n);
+        ACE_HIP(d.alloc(nA, &dA));
+        ACE_HIP(d.alloc(nB, &dB));
+        ACE_HIP(d.alloc(nX, &dX));
+        ACE_HIP(d.alloc(nY, &dY));
+        ACE_HIP(d.alloc(ws, &dW));
+        ACE_HIP(hipMemcpyAsync(dA, A.data(), nA, hipMemcpyHostToDevice, d.st));
+        ACE_HIP(hipMemcpyAsync(dB, B.data(), nB, hipMemcpyHostToDevice, d.st));
+        ACE_TRY(ace_pipeline_solve_batch(&cfg, 1, M, n, tx, rx, (const double*)dA, (const double*)dB, tr.data(),
+                                         (double*)dX, (double*)dY, nullptr, nullptr, nullptr, dW, ws, d.st));
+        ACE_HIP(hipMemcpyAsync(X.data(), dX, nX, hipMemcpyDeviceToHost, d.st));
+        ACE_HIP(hipStreamSynchronize(d.st));
+    }
+    // ---- :170-178 H_out = X / rss_fct, NaN -> 0, amplitude and angle
+    for (int k = 0; k < n; ++k) {
+        std::complex<double> h(X[2 * k] / kRssFct, X[2 * k + 1] / kRssFct);
+        if (std::isnan(h.real()) || std::isnan(h.imag())) h = 0.0;
+        H_amp[k] = std::abs(h);
+        H_angle[k] = std::arg(h);
+    }
+    return ACE_OK;
 }
 
 }  // namespace
@@ -112,17 +242,14 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
         n_M = k;
     }
     const int n = tx * rx;
-    // multiresolution tiers (..._multiresolution.m:111-112, :137-144)
-    const int thresh[2] = {96, 256};
-    const int tier_len[3] = {1984, 3968, 3968};
     for (int i = 0; i < n_M; ++i) {
         const int M = Ms[i];
         int avail = P;
         if (driver == ACE_DRIVER_MULTIRES) {
-            const int t = M <= thresh[0] ? 0 : (M <= thresh[1] ? 1 : 2);
-            avail = tier_len[t];
+            const int t = multires_tier(M);
+            avail = kTierLen[t];
             int off = 0;
-            for (int k = 0; k < t; ++k) off += tier_len[k];
+            for (int k = 0; k < t; ++k) off += kTierLen[k];
             if (off + avail > P)
                 return fail(ACE_ERR_ARG, "multiresolution codebook needs %d rows (tier %d), got %d", off + avail, t, P);
         }
@@ -134,69 +261,31 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
                           : driver == ACE_DRIVER_PHASELIFT ? 4096
                                                            : kSeeds[seed_id - 1];
 
-    ace_pipeline_cfg cfg;
-    ace_pipeline_cfg_default(&cfg, driver == ACE_DRIVER_A2NUCLEAR ? ACE_VARIANT_NUCLEAR : ACE_VARIANT_A2ONLY);
-    for (int i = 0; i < n_M; ++i) {
-        const int M = Ms[i];
-        // ---- :137 M_idx = randperm(length(rss_final), M) (multiresolution: within its tier)
-        std::vector<int32_t> idx(M);
-        int avail = P, off = 0;
-        if (driver == ACE_DRIVER_MULTIRES) {
-            const int t = M <= thresh[0] ? 0 : (M <= thresh[1] ? 1 : 2);
-            avail = tier_len[t];
-            for (int k = 0; k < t; ++k) off += tier_len[k];
-        }
-        randperm_k(seed, 0x100 + 2 * (uint64_t)i, avail, M, idx.data());
-        // ---- :120, :138-139 cb_train (row-major M x n c128), rss_train
-        std::vector<double> A(2 * (size_t)M * n), B(M);
-        for (int r = 0; r < M; ++r) {
-            const int row = idx[r] + off;
-            for (int k = 0; k < n; ++k) {
-                const double a = cb_amp[(size_t)row * n + k], ph = cb_angle[(size_t)row * n + k];
-                A[2 * ((size_t)r * n + k)] = a * std::cos(ph);
-                A[2 * ((size_t)r * n + k) + 1] = a * std::sin(ph);
-            }
-            B[r] = std::sqrt(std::pow(10.0, rss_dbm[row] / 10.0) / 1000.0) * kRssFct;   // db2pow
-        }
-        std::vector<double> X(2 * (size_t)n), Y(2 * (size_t)M);
-        double q = 0.0;
-        int rc = ACE_OK;
-        if (driver == ACE_DRIVER_PHASELIFT) {
-            // ---- Recover_Channel.m:32-35: MyPhaseLift((meas/2e5).^2*1e10, beams)/sqrt(1e10)*2e5
-            ace_phaselift_cfg pcfg;
-            ace_phaselift_cfg_default(&pcfg);
-            std::vector<double> bq(M);
-            for (int r = 0; r < M; ++r) bq[r] = (B[r] / 2e5) * (B[r] / 2e5) * 1e10;
-            rc = ace_phaselift_solve_host(&pcfg, 1, M, n, A.data(), bq.data(), X.data(), nullptr, nullptr);
-            if (rc) return rc;
-            for (int k = 0; k < 2 * n; ++k) X[k] = X[k] / std::sqrt(1e10) * 2e5;
-        } else {
-        // ---- Recover_Channel -> ADMM_v2(..., 4): the pipeline with its own train partitions
-        {
-            const int r = std::min(std::min(cfg.r, M), n);
-            const int mt = (int)std::floor(M * cfg.cc_frac);
-            if (mt < r) {
-                // ill-posed sweep point (fewer train rows than spectral columns, e.g. M = 4):
-                // reported as NaN -> 0 like a failed MATLAB recovery (H_out(isnan) = 0, :176)
-                for (int k = 0; k < n; ++k) H_amp[(size_t)i * n + k] = H_angle[(size_t)i * n + k] = 0.0;
-                continue;
-            }
-            std::vector<int32_t> tr((size_t)cfg.restarts * mt);
-            for (int s = 0; s < cfg.restarts; ++s)
-                randperm_k(seed, 0x101 + 2 * (uint64_t)i + 0x10000 * (uint64_t)s, M, mt, tr.data() + (size_t)s * mt);
-            rc = ace_pipeline_solve_host(&cfg, 1, M, n, tx, rx, A.data(), B.data(), tr.data(), X.data(), Y.data(),
-                                         &q, nullptr, nullptr);
-        }
-        if (rc) return rc;
-        }
-        // ---- :170-178 H_out = X / rss_fct, NaN -> 0, amplitude and angle
-        for (int k = 0; k < n; ++k) {
-            std::complex<double> h(X[2 * k] / kRssFct, X[2 * k + 1] / kRssFct);
-            if (std::isnan(h.real()) || std::isnan(h.imag())) h = 0.0;
-            H_amp[(size_t)i * n + k] = std::abs(h);
-            H_angle[(size_t)i * n + k] = std::arg(h);
-        }
+    // The sweep points are independent recoveries of different sizes M: each runs on its own host
+    // thread, HIP stream and device buffers, so the 8 pipelines (whose restarts each synchronise
+    // their stream once, ace_pipeline.cpp) overlap on the GPU; the call returns when all are done.
+    int dev = 0;
+    ACE_HIP(hipGetDevice(&dev));
+    std::vector<int> rcs(n_M, ACE_OK);
+    std::vector<std::string> errs(n_M);
+    auto point = [&](int i) {
+        rcs[i] = sweep_point(driver, tx, rx, P, cb_amp, cb_angle, rss_dbm, seed, i, Ms[i], dev,
+                             H_amp + (size_t)i * n, H_angle + (size_t)i * n);
+        if (rcs[i]) errs[i] = g_err;
+    };
+    if (n_M == 1) {
+        point(0);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(n_M);
+        for (int i = 0; i < n_M; ++i) th.emplace_back(point, i);
+        for (auto& t : th) t.join();
     }
+    for (int i = 0; i < n_M; ++i)
+        if (rcs[i]) {
+            g_err = errs[i];
+            return rcs[i];
+        }
     return n_M;
 }
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -55,6 +56,9 @@ struct Prof {
     long long msp_total = 0;
 };
 inline Prof g_prof;
+// solves per apply path since the last reset (ace_path_counts): 0 shared phase code (int8 digit
+// planes), 1 private phase codes (2-bit code images), 2 f64 shared A, 3 f64 private A
+inline std::atomic<long long> g_path[4];
 
 struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
     hipStream_t st;

@@ -1412,7 +1412,8 @@ size_t gyf_lds_bytes(int m) {
     const size_t ts = gyf_ts_bytes(m), ad = gyk_lds_bytes(m) - ts, zs = i8ah_fuse_lds_bytes();
     return ts + ad + (ts >= zs ? 0 : zs);
 }
-void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, hipStream_t st) {
+void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, int ctl,
+                hipStream_t st) {
     static const bool attr = [] {
         const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gyf_kernel),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, GYK_MAXDYN) == hipSuccess;
@@ -1421,8 +1422,6 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     }();
     (void)attr;
     const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
-    const char* ce = getenv("ACE_GYF_CTL");   // 0: the Z-step launch runs the m-space control (read per call)
-    const int ctl = ce ? atoi(ce) : 1;
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad, ctl);
 }

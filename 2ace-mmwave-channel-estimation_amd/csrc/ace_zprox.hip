@@ -433,6 +433,44 @@ void launch_zstep(int variant, bool init, const ZArgs& a, int batch, hipStream_t
     }
 #undef ACE_ZL
 }
+// Shrink (inferLowRank_Nuclear.m:421-439) of the n x r matrices E_b on their own: the init form of
+// the GRAM nuclear Z-step (mu = 1, N = 0, threshold 1) on E / tau, scaled back by tau
+// (exact for a power-of-two tau).  Columns of E_b are contiguous ([b][r][n]).
+__global__ void scale_kernel(long long cnt, double f, const double* __restrict__ x, double* __restrict__ y) {
+    const long long i = blockIdx.x * 256LL + threadIdx.x;
+    if (i < cnt) y[i] = x[i] * f;
+}
+int launch_nuclear_prox(int batch, int n, int r, const double* E, double tau, double* Zo, hipStream_t st) {
+    const long long cnt = 2LL * batch * r * n;
+    double *X = nullptr, *N = nullptr;
+    RealState* rs = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&X), sizeof(double) * cnt, st);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&N), sizeof(double) * cnt, st);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&rs), sizeof(RealState) * batch, st);
+    if (e == hipSuccess) e = hipMemsetAsync(N, 0, sizeof(double) * cnt, st);
+    if (e == hipSuccess) e = hipMemsetAsync(rs, 0, sizeof(RealState) * batch, st);
+    if (e == hipSuccess) {
+        const unsigned gb = (unsigned)((cnt + 255) / 256);
+        if (tau == 1.0) e = hipMemcpyAsync(X, E, sizeof(double) * cnt, hipMemcpyDeviceToDevice, st);
+        else hipLaunchKernelGGL(scale_kernel, dim3(gb), dim3(256), 0, st, cnt, 1.0 / tau, E, X);
+        ZArgs a{};
+        a.n = n;
+        a.r = r;
+        a.tx = n;
+        a.rx = 1;
+        a.X = X;
+        a.N = N;
+        a.Z = Zo;
+        a.st = rs;
+        hipLaunchKernelGGL((zstep_kernel<ACE_VARIANT_NUCLEAR, true, true>), dim3(batch), dim3(256), 0, st, a);
+        if (tau != 1.0) hipLaunchKernelGGL(scale_kernel, dim3(gb), dim3(256), 0, st, cnt, tau, Zo, Zo);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (X) (void)hipFreeAsync(X, st);
+    if (N) (void)hipFreeAsync(N, st);
+    if (rs) (void)hipFreeAsync(rs, st);
+    return e == hipSuccess ? 0 : (int)e;
+}
 void launch_pre(int n, int m, int batch, const double* Z, const double* N, const double* Y, const double* M, double* V,
                 double* S, const RealState* rs, hipStream_t st) {
     hipLaunchKernelGGL(pre_kernel, dim3(batch), dim3(256), 0, st, n, m, Z, N, Y, M, V, S, rs);

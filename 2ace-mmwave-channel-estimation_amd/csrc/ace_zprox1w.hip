@@ -859,10 +859,15 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         printf("1w b %d it %d fast: E %llu F %llu cert %llu rest %llu\n", b, a.it, dbg_fa - dbg_t0, dbg_fb - dbg_fa,
                dbg_fc - dbg_fb, dbg_t4 - dbg_fc);
 #endif
-    // bound for the next iteration's V = Z - N/mu (after iter_control's mu update)
+    // bound for the next iteration's V = Z - N/mu (after iter_control's mu update).  A convergence
+    // test left pending (RealState::dpend) may still multiply mu by rho in the next gyk_kernel
+    // (dual_finish): the bound takes the smaller of the two mu values (the same mu for rho >= 1)
     auto write_vbound = [&]() {
         const double zm = wave_max(vz.m), nm = wave_max(vn.m), sn = wave_sum(vz.s + vn.s);
-        if (lane == 0) st->vbound = (zm + nm * (1.0 / st->mu)) * (1.0 + 0x1p-40) + sn;
+        if (lane == 0) {
+            const double mu_lo = st->dpend ? fmin(st->mu, st->mu * a.rho) : st->mu;
+            st->vbound = (zm + nm * (1.0 / mu_lo)) * (1.0 + 0x1p-40) + sn;
+        }
     };
     if (INIT) {
         write_vbound();   // N = 0 after init (init_r_kernel)
@@ -1061,11 +1066,6 @@ __global__ __launch_bounds__(64 * ZL_WAVES) __attribute__((amdgpu_waves_per_eu(2
 }
 
 }  // namespace
-
-bool zlean_enabled() {
-    const char* e = getenv("ACE_LEAN");
-    return !(e && e[0] == '0');
-}
 
 void launch_zlean(const ZArgs& a, int batch, hipStream_t st) {
     if (a.n % 64 != 0 || a.n > 1024) return;   // the full kernel handles every realisation

@@ -300,14 +300,6 @@ def msp_bytes(m):
     return 16.0 * 8 * m + 8.0 * m
 
 
-def msp_bytes(m):
-    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel for a realisation in m-space
-    form (RealState::msp: Z implicit as Z0 + A^H S, no apply_AH pass): read Y, M, AX, S (c128) and
-    B (f64); write AX, M, Y_new and S' = S + g.  (opt_S, copied when the iterate improves, is not
-    counted: a bookkeeping copy like the deferred opt_X / opt_Y.)"""
-    return 16.0 * 8 * m + 8.0 * m
-
-
 def unit_bytes(m, n, tx, rx):
     """Algorithmic HBM bytes per realisation per iteration of the steady-state unit path
     (complex128 = 16 B, each array read or written once):

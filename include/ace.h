@@ -236,6 +236,14 @@ int ace_svd_beamformer_host(int batch, int tx, int rx, const double* H, const do
                             uint8_t* wr_code, uint8_t* wt_code, int32_t* beam_idx, double* rss,
                             uint32_t* status, double* vh_r, double* vh_t);
 
+/* ---- nuclear-norm prox (A2nuclear ArgMinZ / Shrink) ---------------------------------------
+ *   Z = U * Shrink(S, tau) * V'  with [U,S,V] = svd(E)     inferLowRank_Nuclear.m:411-439
+ * for a batch of n x r matrices E_b (DEVICE, c128, [batch][r][n]: column j of E_b at
+ * E + 2*(b*r + j)*n doubles), r <= 32, tau > 0: the r-general Z-prox kernel of the A2nuclear
+ * stages (singular values through the r x r Gram matrix and the Jacobi eigensolver).  Exposed for
+ * the prox's own known-answer test; asynchronous on `stream`. */
+int ace_nuclear_prox_batch(int batch, int n, int r, const double* E, double tau, double* Z, void* stream);
+
 /* Synthetic traces (device).  Counter-based RNG (splitmix64 of seed/stream/counter),
  * identical integer streams to ace_amd.synth on the host.
  *   ace_synth_codebook: A[count][m][n] c128 with entries exp(j*pi/2*k)/sqrt(n),
@@ -276,6 +284,13 @@ int ace_prof_stop(double* total_ms, int32_t* launches);
  * settled in m-space form (RealState::msp: no apply_AH pass, no Z traffic), for the bench's
  * per-launch work accounting. */
 int ace_prof_msp_steps(long long* steps);
+
+/* InferADMM solves (unit solves and every pipeline stage) per apply path since the last reset,
+ * process-wide: counts[0] shared phase-code codebook on the exact int8 digit-plane applies,
+ * counts[1] private phase-code codebooks (2-bit code images), counts[2] f64 applies on a shared
+ * A, counts[3] f64 applies on private A.  reset != 0 zeroes the counters after reading them;
+ * counts may be NULL.  Tells a caller whether its codebook reached the phase-code path. */
+int ace_path_counts(int64_t* counts, int reset);
 
 /* Last error text for this thread ("" if none). */
 const char* ace_last_error(void);

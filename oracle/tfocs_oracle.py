@@ -225,3 +225,26 @@ def my_phaselift(measurements, Phi, *, maxIts=4000, tol=1e-10, restart=200, lam=
     w, V = np.linalg.eigh(res.x)                      # [recoveredSig, eVal] = eig(recoveredMat)
     sig = math.sqrt(w[-1]) * V[:, -1] if w[-1] >= 0 else np.sqrt(complex(w[-1])) * V[:, -1]
     return sig, res
+
+
+def my_phaselift_reduced(measurements, Phi, *, maxIts=4000, tol=1e-10, restart=200, lam=5e-2):
+    """my_phaselift in the coordinates of range(Phi^H) (m <= n, Phi of full row rank): with the zero
+    start every TFOCS iterate is Q Xr Q^H, Phi^H = Q R (R = chol(Phi Phi^H)), A(Q Xr Q^H) =
+    diag(R^H Xr R), A*(g) = Q (R diag(g) R^H) Q^H, and norms / inner products are preserved, so the
+    same tfocs_at_tracels run on m x m matrices is the dense iteration up to rounding
+    (tests/test_oracle.py::test_phaselift_reduction_is_exact).  Returns (sig, result) like
+    my_phaselift, sig mapped back to n coordinates (Q u = Phi^H R^-1 u)."""
+    Phi = np.asarray(Phi, dtype=np.complex128)
+    m, n = Phi.shape
+    if m > n:
+        return my_phaselift(measurements, Phi, maxIts=maxIts, tol=tol, restart=restart, lam=lam)
+    R = np.linalg.cholesky(Phi @ Phi.conj().T).conj().T          # upper, Phi Phi^H = R^H R
+    Rc = R.conj()
+    res = tfocs_at_tracels(lambda X: np.sum(Rc * (X @ R), axis=0), lambda g: (R * g[None, :]) @ R.conj().T,
+                           np.asarray(measurements, dtype=np.float64).reshape(m), lam,
+                           np.zeros((m, m), np.complex128), maxIts=maxIts, tol=tol, restart=restart)
+    w, V = np.linalg.eigh(res.x)
+    u = np.linalg.solve(R, V[:, -1])
+    sig = Phi.conj().T @ u
+    sig = (math.sqrt(w[-1]) if w[-1] >= 0 else np.sqrt(complex(w[-1]))) * sig
+    return sig, res

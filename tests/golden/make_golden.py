@@ -124,6 +124,46 @@ def tfocs_tracels_kat():
     print("TFOCS traceLS_problem1 KAT", d["X_reference"].shape)
 
 
+def nuclear_norm_kat():
+    """TFOCS's own known answer for nuclear-norm minimisation (examples/smallscale/
+    test_nuclearNorm.m, reference_solutions/nuclearNorm_problem1_noiseless.mat): the observed
+    entries omega (1-based, column-major), b and the CVX minimiser X_reference (data only)."""
+    mat = pathlib.Path("/root/reference/main/3rd_software_component/sparsepr/third/TFOCS/examples/smallscale/"
+                       "reference_solutions/nuclearNorm_problem1_noiseless.mat")
+    if not mat.exists():
+        print("TFOCS reference solutions not present; keeping existing fixture")
+        return
+    import scipy.io as sio
+    d = sio.loadmat(str(mat))           # plain MATLAB v5 numeric arrays
+    np.savez_compressed(HERE / "tfocs_nuclearNorm_problem1.npz", omega=d["omega"].ravel().astype(np.int64),
+                        b=d["b"].ravel(), X_reference=d["X_reference"],
+                        obj_reference=float(d["obj_reference"].ravel()[0]))
+    print("TFOCS nuclearNorm_problem1 KAT", d["X_reference"].shape)
+
+
+def reference_codebooks_packed():
+    """The reference's probing codebooks as 2-bit phase codes, four per byte (code k of entry
+    j^k in bits 2*(c % 4) of byte c // 4 of its row): codebook/codebook_mat/
+    random_probe_cb_16x16.mat (3968 x 256) and random_probe_cb_16x16_multires.mat (9920 x 256,
+    tiers of 1984 / 3968 / 3968 rows, processsing_codebook_multires.m)."""
+    import scipy.io as sio
+    out = {}
+    for key, name in (("random", "random_probe_cb_16x16.mat"), ("multires", "random_probe_cb_16x16_multires.mat")):
+        mat = pathlib.Path("/root/reference/codebook/codebook_mat") / name
+        if not mat.exists():
+            print("reference codebooks not present; keeping existing fixture")
+            return
+        cb = sio.loadmat(str(mat))["cb"]   # plain MATLAB v5 numeric array, no pickle
+        k = np.rint(np.angle(cb) / (np.pi / 2)).astype(np.int64) % 4
+        assert np.array_equal(1j ** k, cb) or np.allclose(1j ** k, cb, atol=1e-12), name
+        k = k.astype(np.uint8).reshape(cb.shape[0], -1, 4)
+        out[key] = (k[..., 0] | (k[..., 1] << 2) | (k[..., 2] << 4) | (k[..., 3] << 6)).astype(np.uint8)
+        out[key + "_sha256"] = np.array(hashlib.sha256(np.ascontiguousarray(
+            np.rint(np.angle(cb) / (np.pi / 2)).astype(np.int64) % 4).astype(np.uint8).tobytes()).hexdigest())
+    np.savez_compressed(HERE / "ref_codebooks_16x16_packed.npz", **out)
+    print("reference codebooks packed", {k: v.shape for k, v in out.items() if v.ndim == 2})
+
+
 def main():
     # config 1 (SURVEY §8): 16-ant, 64 RSS meas -- single-restart inferLowRankV4 and the
     # 3-restart inferLowRankV4_multi / 1-restart inferLowRank_Nuclear
@@ -140,6 +180,8 @@ def main():
                         normals=synth.normal_pairs(58659179, 3, 4), vecH=synth.channel(58659179, 0, 4, 4))
     reference_codebook_slice()
     tfocs_tracels_kat()
+    nuclear_norm_kat()
+    reference_codebooks_packed()
 
 
 if __name__ == "__main__":

@@ -442,3 +442,48 @@ def test_gyf_ragged_batches_and_sizes(gpu, batch, m, tx):
                              fixed_iters=True)
     torch.cuda.synchronize()
     assert _errs(small.X.cpu().numpy(), X[batch - 16:]).max() <= 1e-12
+
+
+def test_nuclear_config3_split_path_vs_oracle(gpu):
+    """Config 3's benchmarked path: A2nuclear at 32 antennas, m = 256, a 4096-realisation batch, so
+    the solve runs as concurrent sub-batches (admm_iterate_split: gyk_kernel, apply_AH, one-wave
+    Z-step with the soft threshold of inferLowRank_Nuclear.m:411-419).  A sample against the C oracle
+    on the horizon where the oracle is stable against itself (60 iterations; see
+    test_oracle.py::test_nuclear_refinement_is_rounding_chaotic)."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(71, 0, 4096, 256, 32, 32)
+    r = infer_admm_batch(A, B, X0, 32, 32, variant="A2nuclear", maxiter=60, fixed_iters=True)
+    torch.cuda.synchronize()
+    idx = [0, 1500, 2048, 4095]
+    X = r.X.cpu().numpy()[idx]
+    Ah, Bh, X0h = A.cpu().numpy(), B.cpu().numpy()[idx], X0.cpu().numpy()[idx]
+    Xo, _, ito, _, _ = _oracle(Ah, Bh, X0h, 32, variant=1, maxiter=60, fixed_iters=True)
+    assert (r.iters.cpu().numpy() == 60).all() and (ito == 60).all()
+    assert _errs(X, Xo).max() <= 1e-8
+
+
+def test_nuclear_config3_split_path_batch_invariance_200(gpu):
+    """The same benchmarked path over the full 200-iteration horizon: every sampled realisation
+    is bit-identical to its result in a small batch (no sub-batch split, the single-stream loop of
+    admm_run), so the benchmarked output is the verified small-batch output."""
+    import torch
+    from ace_amd import infer_admm_batch, synth_problem
+    A, B, X0, _ = synth_problem(73, 0, 4096, 256, 32, 32)
+    big = infer_admm_batch(A, B, X0, 32, 32, variant="A2nuclear", maxiter=200, fixed_iters=True)
+    torch.cuda.synchronize()
+    Xb, Yb, itb = big.X.cpu().numpy(), big.Y.cpu().numpy(), big.iters.cpu().numpy()
+    assert np.isfinite(Xb).all() and (itb == 200).all()
+    for lo in (0, 2040, 4032):
+        sub = infer_admm_batch(A, B[lo:lo + 64].contiguous(), X0[lo:lo + 64].contiguous(), 32, 32,
+                               variant="A2nuclear", maxiter=200, fixed_iters=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(sub.X.cpu().numpy(), Xb[lo:lo + 64]), lo
+        assert np.array_equal(sub.Y.cpu().numpy(), Yb[lo:lo + 64]), lo
+    # and the small batch against the oracle on its stable horizon
+    one = infer_admm_batch(A, B[:4].contiguous(), X0[:4].contiguous(), 32, 32, variant="A2nuclear", maxiter=60,
+                           fixed_iters=True)
+    torch.cuda.synchronize()
+    Xo, _, _, _, _ = _oracle(A.cpu().numpy(), B[:4].cpu().numpy(), X0[:4].cpu().numpy(), 32, variant=1,
+                             maxiter=60, fixed_iters=True)
+    assert _errs(one.X.cpu().numpy(), Xo).max() <= 1e-8

@@ -124,3 +124,33 @@ def test_private_unnormalised_codes(gpu):
     res = infer_admm_host(A, B, X0, 16, 16, **kw)
     Xo, _, ito, _, _ = _oracle(A, B, X0, 16, variant=0, maxiter=200, fixed_iters=True)
     assert _errs(res.X, Xo).max() <= TOL
+
+
+_FOUR_WAVE_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = sys.argv[1:]
+import ace_amd, ace_oracle as O, ace_oracle_c as OC
+from ace_amd import synth
+A, B, X0, _ = synth.problem(37, 0, 3, 64, 16, 16, a_shared=False)
+res = ace_amd.infer_admm_host(A, B, X0, 16, 16, variant="A2only", maxiter=150, fixed_iters=True)
+U = np.stack([OC.make_U(a) for a in A])
+Xo, _, ito, _, _ = OC.infer_admm_r1_batch(A, U, B, X0, 16, 16, variant=0, maxiter=150, fixed_iters=True)
+e = max(O.unit_phase_aligned_rel_err(res.X[b], Xo[b]) for b in range(3))
+assert e <= 1e-5 and np.array_equal(res.iters, ito), (e, res.iters, ito)
+print("ok", e)
+"""
+
+
+def test_private_codes_with_four_wave_zstep(gpu):
+    """ACE_ZSTEP_4WAVE=1 (the four-wave A/B Z-step, read once per process, hence a child process)
+    cannot run the code-image iteration, so the private phase-code setup must not be taken either:
+    the solve runs the generic f64 private path on properly formed K and G and matches the oracle."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT, PKG_DIR
+    env = dict(os.environ, ACE_ZSTEP_4WAVE="1")
+    out = subprocess.run([sys.executable, "-c", _FOUR_WAVE_SCRIPT, str(PKG_DIR), str(ROOT / "oracle")], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("ok")

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Generic GPU-box step runner: bash tools/gpu/run.sh <tag> <step>...
+# steps: smoke | tests[:<pytest -k expr or file>] | bench[:<bench args, comma-separated>]
+set -o pipefail
+TAG=$1; shift
+O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+i=0
+for s in "$@"; do
+  i=$((i+1))
+  echo "== $i $s $(date +%T)"
+  case $s in
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/$i.smoke.log 2>&1 || { tail -30 $O/$i.smoke.log; exit 1; } ; tail -3 $O/$i.smoke.log ;;
+    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/$i.tests.log 2>&1 || { tail -40 $O/$i.tests.log; exit 1; } ; tail -3 $O/$i.tests.log ;;
+    tests:*) t=${s#tests:}; timeout -k 10 1000 python -u -m pytest $t -m gpu -x -v --timeout 300 --timeout-method thread > $O/$i.tests.log 2>&1 || { tail -40 $O/$i.tests.log; exit 1; } ; tail -3 $O/$i.tests.log ;;
+    bench:*) a=${s#bench:}; a=${a//,/ }; timeout -k 10 600 python -u bench.py $a > $O/$i.bench.json 2> $O/$i.bench.err || { tail -30 $O/$i.bench.err; exit 1; } ; cat $O/$i.bench.json ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

@@ -61,7 +61,8 @@ class PipelineCfg(C.Structure):
         ("r", C.c_int),
         ("maxiter", C.c_int),
         ("eig_warm", C.c_int),
-        ("reserved", C.c_int * 3),
+        ("stop_before_refine", C.c_int),
+        ("reserved", C.c_int * 2),
         ("mu0", C.c_double),
         ("rho", C.c_double),
         ("cc_frac", C.c_double),
@@ -113,6 +114,8 @@ def _load():
     lib.ace_prof_stop.restype = C.c_int
     lib.ace_prof_msp_steps.argtypes = [C.POINTER(C.c_longlong)]
     lib.ace_prof_msp_steps.restype = C.c_int
+    lib.ace_prof_work.argtypes = [dp]
+    lib.ace_prof_work.restype = C.c_int
     lib.ace_nuclear_prox_batch.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]
     lib.ace_nuclear_prox_batch.restype = C.c_int
     lib.ace_path_counts.argtypes = [C.POINTER(C.c_int64), C.c_int]

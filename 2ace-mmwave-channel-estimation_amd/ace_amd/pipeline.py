@@ -151,9 +151,12 @@ def inferLowRank_Nuclear(A, B, tx, rx, lambda_=0.0, r=20, mu0=1e-3, rho=1.03, cc
 
 def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", restarts=None, r=20, mu0=1e-3,
                                   rho=1.03, cc_frac=0.95, tol_rel=1e-4, tol_abs=1e-8, maxiter=500,
-                                  eig_warm=True, workspace=None, stream=None) -> PipelineResult:
+                                  eig_warm=True, stop_before_refine=False, workspace=None,
+                                  stream=None) -> PipelineResult:
     """Batched pipeline on device tensors: A [m][n] complex128 (shared codebook),
-    B [batch][m] float64, train_idx [restarts][m_t] (host, shared by the batch)."""
+    B [batch][m] float64, train_idx [restarts][m_t] (host, shared by the batch).
+    ``stop_before_refine`` returns X_max, the refinement's input (inferLowRankV4_multi.m:90-92),
+    instead of running the refinement stage."""
     import torch
     from .solver import _DEFAULT_WS
     if not (A.is_cuda and B.is_cuda):
@@ -168,6 +171,7 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
     tr = np.ascontiguousarray(np.asarray(train_idx, dtype=np.int32))
     nres = tr.shape[0] if restarts is None else int(restarts)
     cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
+    cfg.stop_before_refine = int(bool(stop_before_refine))
     ld = 4 * cfg.restarts + 1
     dev = A.device
     out = PipelineResult(torch.empty((batch, n), dtype=torch.complex128, device=dev),

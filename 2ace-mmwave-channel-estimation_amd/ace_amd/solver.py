@@ -184,16 +184,23 @@ def nuclear_prox_batch(E, tau, *, out=None, stream=None):
 
 
 def synth_problem(seed, first, count, m, tx, rx, *, a_shared=True, L=3, snr_db=30.0, x0_noise=0.5,
-                  device="cuda", stream=None):
-    """Generate a synthetic batch directly in HBM (ace_synth_codebook/ace_synth_channels)."""
+                  device="cuda", stream=None, A=None):
+    """Generate a synthetic batch directly in HBM (ace_synth_codebook/ace_synth_channels).
+    ``A`` (a device complex128 [1][m][n] tensor) replaces the random phase-code codebook, e.g. by
+    rows of a multiresolution codebook (ace_amd.synth.multires_codebook)."""
     import torch
     n = tx * rx
     dev = torch.device(device)
     if stream is None:
         stream = torch.cuda.current_stream(dev)
     na = 1 if a_shared else count
-    A = torch.empty((na, m, n), dtype=torch.complex128, device=dev)
-    check(LIB.ace_synth_codebook(seed, -1 if a_shared else first, na, m, n, A.data_ptr(), stream.cuda_stream))
+    if A is not None:
+        if not a_shared or tuple(A.shape) != (1, m, n) or A.dtype != torch.complex128 or not A.is_cuda:
+            raise ValueError("A must be a shared device complex128 [1][m][n] codebook")
+        A = A.contiguous()
+    else:
+        A = torch.empty((na, m, n), dtype=torch.complex128, device=dev)
+        check(LIB.ace_synth_codebook(seed, -1 if a_shared else first, na, m, n, A.data_ptr(), stream.cuda_stream))
     H = torch.empty((count, n), dtype=torch.complex128, device=dev)
     B = torch.empty((count, m), dtype=torch.float64, device=dev)
     X0 = torch.empty((count, n), dtype=torch.complex128, device=dev)

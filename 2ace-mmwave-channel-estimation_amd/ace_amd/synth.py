@@ -108,3 +108,88 @@ def problem(seed, first, count, m, tx, rx, *, a_shared=True, L=3, snr_db=30.0, x
     # InferADMM always sees B / ||B|| (inferLowRankV4_multi.m:32-38); A already has ||A||_F = sqrt(m)
     nb = np.sqrt(np.sum(B * B, axis=1))
     return A, B / nb[:, None], X0 / nb[:, None], H / nb[:, None]
+
+
+# ---- multiresolution probing codebooks ---------------------------------------------------------
+# codebook/generate_tx_codebook_multires_16ant.py:47-120 and generate_rx_codebook_multires_16ant.py
+# draw 2-bit phases per antenna GROUP, in three resolution tiers (groups of 4, 2 and 1 antennas;
+# grouping :48, separation [32, 96, 160] rounds :59); processsing_codebook_multires.m builds each
+# round's 62 probe rows as kron(tx row, the round's rx row) over the active antennas (two 8-element
+# blocks of the 32-element array, id = [1..8, 17..24]).  The tiers hold 1984 / 3968 / 3968 rows
+# (..._multiresolution.m:111-112) and the driver picks the tier by M (thresh [96, 256], :137-144).
+# The 32-antenna analogue (config 5, builder-defined: the reference defines tiers for 16 antennas
+# only) uses all four 8-element blocks with the same in-block grouping, 4x the rounds per tier
+# (the array has 4x the unknowns) and 4x the thresholds.
+ST_MR_TX, ST_MR_RX = 6, 7
+MR_SECTORS = 62                          # probe rows per round (sector_per_cb, :62)
+MR_ROUNDS = {16: (32, 64, 64), 32: (128, 256, 256)}
+MR_THRESH = {16: (96, 256), 32: (384, 1024)}
+
+
+def multires_tiers(tx):
+    """(rows per tier, thresholds) of the multiresolution codebook for tx antennas per side."""
+    if tx not in MR_ROUNDS:
+        raise ValueError(f"multiresolution codebooks are defined for 16 and 32 antennas (got {tx})")
+    return tuple(MR_SECTORS * r for r in MR_ROUNDS[tx]), MR_THRESH[tx]
+
+
+def multires_tier_of(M, tx):
+    """The tier ..._multiresolution.m:137-144 draws M rows from: 0 (M <= thresh[0]), 1, 2."""
+    th = MR_THRESH[tx]
+    return 0 if M <= th[0] else (1 if M <= th[1] else 2)
+
+
+def multires_groups(tx, tier):
+    """Group index of each antenna in a tier: within every 8-element block, groups
+    [0,1,2,3] [4,5,6,7] (tier 0), [0,1] [2,3] [4,6] [5,7] (tier 1, the reference's [5,7],[6,8]
+    pairs), single antennas (tier 2)."""
+    a = np.arange(tx)
+    blk, e = a // 8, a % 8
+    if tier == 0:
+        return 2 * blk + e // 4
+    if tier == 1:
+        return 4 * blk + np.array([0, 0, 1, 1, 2, 3, 2, 3])[e]
+    return a
+
+
+def multires_codes(seed, tx, rows):
+    """Phase codes k (entry j^k) of the given global rows of the tx x tx multiresolution
+    codebook, shape (len(rows), tx*tx), column t*tx + r = kron(tx row, rx row) (the vec(H)
+    order of ``channel``).  Row p belongs to round p // 62; the tx phases are drawn per (row,
+    group), the round's rx phases per (round, group)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    lens, _ = multires_tiers(tx)
+    bounds = np.cumsum(lens)
+    if rows.size and (rows.min() < 0 or rows.max() >= bounds[-1]):
+        raise ValueError("row index outside the codebook")
+    tiers = np.searchsorted(bounds, rows, side="right")
+    out = np.empty((rows.size, tx * tx), np.uint8)
+    for t in range(3):
+        sel = np.nonzero(tiers == t)[0]
+        if sel.size == 0:
+            continue
+        g = multires_groups(tx, t)
+        ng = int(g.max()) + 1
+        p = rows[sel].astype(np.uint64)
+        rnd = (rows[sel] // MR_SECTORS).astype(np.uint64)
+        gg = np.arange(ng, dtype=np.uint64)
+        ktx = (sm64(seed, ST_MR_TX, p[:, None] * np.uint64(ng) + gg[None, :]) >> np.uint64(62)).astype(np.uint8)
+        krx = (sm64(seed, ST_MR_RX, rnd[:, None] * np.uint64(ng) + gg[None, :]) >> np.uint64(62)).astype(np.uint8)
+        out[sel] = ((ktx[:, g][:, :, None] + krx[:, g][:, None, :]) % 4).reshape(sel.size, tx * tx)
+    return out
+
+
+def multires_codebook(seed, tx, rows):
+    """A = j^k / sqrt(n) of the given rows (Random_Phase_State normalisation)."""
+    k = multires_codes(seed, tx, rows)
+    return (1j ** k.astype(np.int64)).astype(np.complex128) / np.sqrt(tx * tx)
+
+
+def multires_rows(seed, tx, M):
+    """The M codebook rows ..._multiresolution.m:137-144 draws for a sweep point: randperm within
+    the tier M selects (M_idx = randperm(tier rows, M) + tier offset), from the build's RNG
+    (ace_driver_randperm, stream 0x100 of the first sweep point).  Returns (rows, tier)."""
+    from .engine import randperm
+    lens, _ = multires_tiers(tx)
+    tier = multires_tier_of(M, tx)
+    return sum(lens[:tier]) + randperm(seed, 0x100, lens[tier], M).astype(np.int64), tier

@@ -145,11 +145,16 @@ static int i8_setup(LinOps& L, hipStream_t st) {
 
 // G = (I + K)^{-1} of the shared K by Newton-Schulz on the matrix cores:
 //   X0 = 2/(1 + b) I  with b >= lambda_max(I + K) (Gershgorin) and lambda_min(I + K) >= 1,
-//   R_k = I - (I + K) X_k,   X_{k+1} = X_k + X_k R_k      (||R_{k+1}|| = ||R_k||^2).
-// Every X_k is a polynomial in I + K, hence Hermitian and commuting with it, which lets both
-// products run as the GEMM's  C = E -/+ V L^H  form.  The iteration stops one step after
-// max|R_k| < 1e-10 (the next step's error is ~1e-20, i.e. converged to rounding).  A single
-// Gauss-Jordan work-group on one CU took 5.2 ms for m = 256; this takes a few dozen small GEMMs.
+//   S_k = I - X_k (I + K),   X_{k+1} = X_k + X_k S_k^H = 2 X_k - X_k (I + K) X_k,
+//   then X_{k+1} <- (X_{k+1} + X_{k+1}^H) / 2.
+// With X_k exactly Hermitian, S_k^H = I - (I + K) X_k, so this is the self-correcting Schulz step
+// (error E -> -E (I + K) E, ||S_{k+1}|| = ||S_k||^2) written in the GEMM's  C = E -/+ V L^H  form.
+// (The round-1 form 2X - X X (I + K) is only first-order stable in the part of the rounding error
+// that does not commute with I + K: E -> E - (I + K)^-1 E (I + K), which grows like the condition
+// number per step -- measured divergence on the reference's 972-row kron-structured train rows.)
+// The iteration stops one step after max|S_k| < 1e-10 (the next step's error is ~1e-20, i.e.
+// converged to rounding).  A single Gauss-Jordan work-group on one CU took 5.2 ms for m = 256;
+// this takes a few dozen small GEMMs.
 int ns_inverse(LinOps& L, hipStream_t st) {
     const int m = L.m;
     const long long mm = (long long)m * m;
@@ -177,8 +182,9 @@ int ns_inverse(LinOps& L, hipStream_t st) {
     int it = 0;
     bool done = false;
     auto step = [&]() -> int {
-        launch_zgemm(1, true, m, m, m, X, m, 0, Ap, m, 0, R, Id, m, 0, 1, st);   // R = I - (I+K) X
-        launch_zgemm(2, true, m, m, m, R, m, 0, X, m, 0, Xn, X, m, 0, 1, st);    // X' = X + X R
+        launch_zgemm(1, true, m, m, m, Ap, m, 0, X, m, 0, R, Id, m, 0, 1, st);   // S = I - X (I+K)
+        launch_zgemm(2, true, m, m, m, R, m, 0, X, m, 0, Xn, X, m, 0, 1, st);    // X' = X + X S^H
+        launch_hermitize(m, Xn, st);
         std::swap(X, Xn);
         ++it;
         return ACE_OK;
@@ -192,17 +198,21 @@ int ns_inverse(LinOps& L, hipStream_t st) {
         done = h < 1e-10;
     }
     for (; it < 60 && !done;) {   // (rounding kept the residual above the bound: poll as before)
-        launch_zgemm(1, true, m, m, m, X, m, 0, Ap, m, 0, R, Id, m, 0, 1, st);
+        launch_zgemm(1, true, m, m, m, Ap, m, 0, X, m, 0, R, Id, m, 0, 1, st);
         double h = 0.0;
         launch_max_abs(2 * mm, R, flag, st);
         ACE_HIP(hipMemcpyAsync(&h, flag, sizeof(double), hipMemcpyDeviceToHost, st));
         ACE_HIP(hipStreamSynchronize(st));
         done = h < 1e-10;
         launch_zgemm(2, true, m, m, m, R, m, 0, X, m, 0, Xn, X, m, 0, 1, st);
+        launch_hermitize(m, Xn, st);
         std::swap(X, Xn);
         ++it;
     }
     ACE_HIP(hipFreeAsync(flag, st));
+#ifdef ACE_DEBUG_SPEC
+    fprintf(stderr, "ns_inverse m %d b %g kpred %d it %d done %d\n", m, b, kpred, it, (int)done);
+#endif
     if (!done) return fail(ACE_ERR_UNSUPPORTED, "setup: Newton-Schulz inverse of I + K did not converge");
     if (X != L.G) ACE_HIP(hipMemcpyAsync(L.G, X, sizeof(double) * 2 * mm, hipMemcpyDeviceToDevice, st));
     return ACE_OK;
@@ -621,6 +631,9 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const int nsplit = gyk ? split_count(batch) : 1;
     if (nsplit > 1 || (gyk && kn.mspace && p.variant != ACE_VARIANT_NUCLEAR))
         return admm_iterate_split(L, p, w, za, batch, B, nsplit, kn, Xo, Yo, iters, status, mu_out, st);
+    // algorithmic flops of the f64 GEMM-shaped applies as launched (all batch * r vectors; the
+    // unit path's fused int8 kernels are accounted by the bench): ace_prof_work
+    const double fl_mn = 8.0 * m * n * nv, fl_mm = 8.0 * m * m * nv;
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     for (int it = 1; it <= p.maxiter; ++it) {
@@ -635,11 +648,11 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
-            ProfScope ps(ACE_K_APPLY_A, st);
+            ProfScope ps(ACE_K_APPLY_A, st, fl_mn);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
         } else {
             { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
-            { ProfScope ps(ACE_K_APPLY_A, st); applyA(1, w.V, w.T, w.S); }      // T = S - A V
+            { ProfScope ps(ACE_K_APPLY_A, st, fl_mn); applyA(1, w.V, w.T, w.S); }   // T = S - A V
         }
         if (pc) {
             // g, the Y-step, W = A^H g and the dual terms came from pgk_kernel
@@ -650,11 +663,11 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                              DualCtl{za.tol_abs, za.tol_rel, za.rho, za.fixed_iters, n, 1, w.done}};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
-            ProfScope ps(ACE_K_APPLY_G, st);
+            ProfScope ps(ACE_K_APPLY_G, st, fl_mm);
             const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
             launch_zgemm_ystep(m, batch, L.G, w.T, w.g, ys, w.st, st);
         } else {
-            { ProfScope ps(ACE_K_APPLY_G, st); applyMM(L.G, w.T, w.g); }        // g = G T
+            { ProfScope ps(ACE_K_APPLY_G, st, fl_mm); applyMM(L.G, w.T, w.g); }   // g = G T
             {
                 ProfScope ps(ACE_K_YSTEP, st);
                 if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
@@ -662,12 +675,12 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             }
         }
         if (!gyk && !pc) {   // K Y
-            ProfScope ps(ACE_K_APPLY_K, st);
+            ProfScope ps(ACE_K_APPLY_K, st, i8 ? 0.0 : fl_mm);
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
         }
         if (!pc) {
-            ProfScope ps(ACE_K_APPLY_AH, st);                                    // X = V + A^H g
+            ProfScope ps(ACE_K_APPLY_AH, st, wmode ? 0.0 : fl_mn);               // X = V + A^H g
             if (wmode) {
                 za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && kn.lean &&
                            it != p.maxiter && fuse_ok(kn, m);

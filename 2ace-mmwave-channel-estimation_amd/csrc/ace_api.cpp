@@ -44,6 +44,7 @@ int ace_prof_start(int max_launches) {
     g_prof.ev.assign(2 * (size_t)max_launches, nullptr);
     for (auto& e : g_prof.ev) ACE_HIP(hipEventCreate(&e));
     g_prof.cls.assign(max_launches, 0);
+    g_prof.work.assign(max_launches, 0.0);
     g_prof.used = 0;
     for (int& c : g_prof.seen) c = 0;
     if (!g_prof.msp_slots) {
@@ -62,6 +63,13 @@ int ace_prof_msp_steps(long long* steps) {
     return ACE_OK;
 }
 
+int ace_prof_work(double* flops) {
+    g_err.clear();
+    if (!flops) return fail(ACE_ERR_ARG, "flops is NULL");
+    for (int c = 0; c < ACE_NKCLASS; ++c) flops[c] = g_prof.work_tot[c];
+    return ACE_OK;
+}
+
 int ace_path_counts(int64_t* counts, int reset) {
     g_err.clear();
     for (int k = 0; k < 4; ++k) {
@@ -77,18 +85,21 @@ int ace_prof_stop(double* total_ms, int32_t* launches) {
     for (int c = 0; c < ACE_NKCLASS; ++c) {
         if (total_ms) total_ms[c] = 0.0;
         if (launches) launches[c] = 0;
+        g_prof.work_tot[c] = 0.0;
     }
     for (size_t i = 0; i < g_prof.used; ++i) {
         ACE_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
         float ms = 0.f;
         ACE_HIP(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
         const int c = g_prof.cls[i];
+        g_prof.work_tot[c] += g_prof.work[i];
         if (total_ms) total_ms[c] += ms;
         if (launches) launches[c] += 1;
     }
     for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
     g_prof.ev.clear();
     g_prof.cls.clear();
+    g_prof.work.clear();
     g_prof.used = 0;
     ACE_HIP(hipDeviceSynchronize());   // (the m-space counters are copied after the last events)
     g_prof.msp_total = 0;
@@ -133,6 +144,7 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     const size_t need = ace_admm_workspace_size(cfg, batch, m, n);
     if (need > workspace_bytes)
         return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
+    poison_workspace(workspace, workspace_bytes, st);
     Carver cv{(char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255)};
     LinOps L;
     AdmmState w;

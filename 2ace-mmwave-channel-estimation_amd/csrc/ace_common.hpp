@@ -267,6 +267,8 @@ void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double*
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st, double* bnd);
 // out[0] = max |x_i| over n doubles
 void launch_max_abs(long long n, const double* x, double* out, hipStream_t st);
+// X <- (X + X^H) / 2 for an m x m complex matrix (exactly Hermitian, real diagonal)
+void launch_hermitize(int m, double* X, hipStream_t st);
 
 // Private phase-code codebooks (ace_private.hip): 2-bit code images of each A_b, G_b = (I + A_b A_b^H)^{-1}
 // as lower 16 x 16 tiles, and the per-realisation iteration kernel (T, g = G T, Y-step, W = A^H g and the

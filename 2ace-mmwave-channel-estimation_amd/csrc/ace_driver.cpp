@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -40,10 +41,19 @@ const uint64_t kSeeds[40] = {58659179, 42737934, 36326041, 89830260, 90710947, 9
                              73073690, 6288587,  42217659, 45632040, 7495955,  31960297, 92863244, 93081516};
 const uint64_t kNuclearSeeds[4] = {1024, 2048, 4096, 8192};   // ..._A2nuclear.m:103
 
-// multiresolution tiers (..._multiresolution.m:111-112, :137-144): rows [0, 1984) are the
-// 4-antenna-group probes, then 3968 2-antenna-group probes, then 3968 per-antenna probes
-const int kTierLen[3] = {1984, 3968, 3968};
-int multires_tier(int M) { return M <= 96 ? 0 : (M <= 256 ? 1 : 2); }
+// multiresolution tiers (..._multiresolution.m:111-112, :137-144): for 16 antennas rows
+// [0, 1984) are the 4-antenna-group probes, then 3968 2-antenna-group probes, then 3968
+// per-antenna probes, picked by M <= 96 / <= 256 / else.  The reference defines tiers for 16
+// antennas only; the 32-antenna layout is the build's analogue (ace_amd.synth.multires_tiers:
+// 4x the rows and 4x the thresholds).
+const int kTierLen16[3] = {1984, 3968, 3968}, kThresh16[2] = {96, 256};
+const int kTierLen32[3] = {7936, 15872, 15872}, kThresh32[2] = {384, 1024};
+bool multires_defined(int tx, int rx) { return tx == rx && (tx == 16 || tx == 32); }
+int multires_tier(int M, int tx) {
+    const int* th = tx == 32 ? kThresh32 : kThresh16;
+    return M <= th[0] ? 0 : (M <= th[1] ? 1 : 2);
+}
+int tier_len(int tx, int t) { return (tx == 32 ? kTierLen32 : kTierLen16)[t]; }
 
 // splitmix64 counter RNG (the same construction as ace_synth.hip / ace_amd.synth)
 uint64_t sm64(uint64_t seed, uint64_t stream, uint64_t ctr) {
@@ -122,9 +132,9 @@ int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const d
     std::vector<int32_t> idx(M);
     int avail = P, off = 0;
     if (driver == ACE_DRIVER_MULTIRES) {
-        const int t = multires_tier(M);
-        avail = kTierLen[t];
-        for (int k = 0; k < t; ++k) off += kTierLen[k];
+        const int t = multires_tier(M, tx);
+        avail = tier_len(tx, t);
+        for (int k = 0; k < t; ++k) off += tier_len(tx, k);
     }
     randperm_k(seed, 0x100 + 2 * (uint64_t)i, avail, M, idx.data());
     // ---- :120, :138-139 cb_train (row-major M x n c128), rss_train
@@ -242,14 +252,17 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
         n_M = k;
     }
     const int n = tx * rx;
+    if (driver == ACE_DRIVER_MULTIRES && !multires_defined(tx, rx))
+        return fail(ACE_ERR_UNSUPPORTED, "multiresolution tiers are defined for 16 x 16 (reference) and 32 x 32 "
+                    "antennas (got %d x %d)", tx, rx);
     for (int i = 0; i < n_M; ++i) {
         const int M = Ms[i];
         int avail = P;
         if (driver == ACE_DRIVER_MULTIRES) {
-            const int t = multires_tier(M);
-            avail = kTierLen[t];
+            const int t = multires_tier(M, tx);
+            avail = tier_len(tx, t);
             int off = 0;
-            for (int k = 0; k < t; ++k) off += kTierLen[k];
+            for (int k = 0; k < t; ++k) off += tier_len(tx, k);
             if (off + avail > P)
                 return fail(ACE_ERR_ARG, "multiresolution codebook needs %d rows (tier %d), got %d", off + avail, t, P);
         }
@@ -273,8 +286,10 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
                              H_amp + (size_t)i * n, H_angle + (size_t)i * n);
         if (rcs[i]) errs[i] = g_err;
     };
-    if (n_M == 1) {
-        point(0);
+    // ACE_DRIVER_SERIAL=1 runs the sweep points one after another on the calling thread (A/B)
+    const char* ser = getenv("ACE_DRIVER_SERIAL");
+    if (n_M == 1 || (ser && ser[0] == '1')) {
+        for (int i = 0; i < n_M; ++i) point(i);
     } else {
         std::vector<std::thread> th;
         th.reserve(n_M);

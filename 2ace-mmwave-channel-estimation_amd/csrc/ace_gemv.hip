@@ -145,11 +145,15 @@ __global__ __launch_bounds__(1024) void inv_ipk_kernel(int m, double* __restrict
 }
 // max |x_i| over the grid: per-block maxima combined with a 64-bit atomic max on the bit patterns
 // (for non-negative doubles the unsigned order of the patterns is the numeric order); *out must be
-// zeroed first (launch_max_abs does it).  NaNs are dropped (fmax), as before.
+// zeroed first (launch_max_abs does it).  A NaN entry yields +inf.
 __global__ __launch_bounds__(256) void max_abs_kernel(long long n, const double* __restrict__ x, double* out) {
     __shared__ double part[256];
     double v = 0.0;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += 256LL * gridDim.x) v = fmax(v, fabs(x[i]));
+    // (a NaN counts as +inf: fmax would drop it, and callers use the maximum as a convergence test)
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += 256LL * gridDim.x) {
+        const double a = fabs(x[i]);
+        v = fmax(v, a == a ? a : INFINITY);
+    }
     part[threadIdx.x] = v;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -199,6 +203,24 @@ void launch_max_abs(long long n, const double* x, double* out, hipStream_t st) {
     (void)hipMemsetAsync(out, 0, sizeof(double), st);
     const long long blocks = std::min<long long>(1024, (n + 2047) / 2048);
     hipLaunchKernelGGL(max_abs_kernel, dim3((unsigned)std::max<long long>(1, blocks)), dim3(256), 0, st, n, x, out);
+}
+
+__global__ __launch_bounds__(256) void hermitize_kernel(int m, d2* __restrict__ X) {
+    const int j = blockIdx.x * 16 + (threadIdx.x & 15), i = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (i >= m || j >= m || j < i) return;
+    const d2 u = X[(long long)i * m + j];
+    if (i == j) {
+        X[(long long)i * m + j] = make_double2(u.x, 0.0);
+        return;
+    }
+    const d2 l = X[(long long)j * m + i];
+    const d2 h = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+    X[(long long)i * m + j] = h;
+    X[(long long)j * m + i] = make_double2(h.x, -h.y);
+}
+void launch_hermitize(int m, double* X, hipStream_t st) {
+    const dim3 grid((m + 15) / 16, (m + 15) / 16);
+    hipLaunchKernelGGL(hermitize_kernel, grid, dim3(256), 0, st, m, reinterpret_cast<d2*>(X));
 }
 
 void launch_zgemv_rows(int mode, int M, int K, int nb, const double* L, long long strideL, const double* V,

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <string>
 #include <vector>
@@ -45,6 +46,8 @@ struct Prof {
     bool on = false;
     std::vector<hipEvent_t> ev;   // 2 per record
     std::vector<int> cls;
+    std::vector<double> work;     // algorithmic flops of each recorded launch (ProfScope)
+    double work_tot[ACE_NKCLASS] = {};   // per class, over the recorded launches (ace_prof_work)
     size_t used = 0;
     int stride = 1;               // record every stride-th launch of each class (ace_prof_sample) ...
     unsigned full = 0;            // ... except the classes in this mask, recorded on every launch
@@ -60,15 +63,27 @@ inline Prof g_prof;
 // planes), 1 private phase codes (2-bit code images), 2 f64 shared A, 3 f64 private A
 inline std::atomic<long long> g_path[4];
 
+// ACE_POISON=1 (debugging): fill a solve's workspace with 0xFF bytes (NaN doubles, -1 ints) before
+// it is carved, so that a read of memory the solve did not write shows up in its results
+inline void poison_workspace(void* ws, size_t bytes, hipStream_t st) {
+    static const bool on = [] {
+        const char* e = getenv("ACE_POISON");
+        return e && e[0] == '1';
+    }();
+    if (on) (void)hipMemsetAsync(ws, 0xFF, bytes, st);
+}
+
 struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
     hipStream_t st;
     int idx = -1;
-    ProfScope(int c, hipStream_t s) : st(s) {
+    // work: the launch's algorithmic flops (8 per complex MAC), 0 where the caller accounts itself
+    ProfScope(int c, hipStream_t s, double work = 0.0) : st(s) {
         const bool pick = ((g_prof.full >> c) & 1u) || (g_prof.seen[c] % g_prof.stride) == 0;
         if (g_prof.on) ++g_prof.seen[c];
         if (g_prof.on && pick && g_prof.used < g_prof.cls.size()) {
             idx = (int)g_prof.used++;
             g_prof.cls[idx] = c;
+            g_prof.work[idx] = work;
             (void)hipEventRecord(g_prof.ev[2 * idx], st);
         }
     }

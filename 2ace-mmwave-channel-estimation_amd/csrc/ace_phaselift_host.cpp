@@ -103,6 +103,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
         if (sz.off + 256 > workspace_bytes)
             return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", sz.off + 256, workspace_bytes);
     }
+    poison_workspace(workspace, workspace_bytes, st);
     Carver cv{(char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255)};
     PlWs w;
     pl_carve(cv, D, &w);
@@ -169,23 +170,27 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
                 launch_pl_set_Ay(a, st);
                 launch_pl_grad(a, st);
             }
+            // algorithmic flops per realisation still in the inner loop (h[0]): A*(g) = R diag(g) R^H
+            // (8 d^2 m), the prox's dense Hermitian eigendecomposition (17.3 d^3, SURVEY.md §8d's
+            // count for eig with vectors), its assembly V diag(s) V^H (8 d^3), A(z) (8 m d^2)
+            const double act = h[0], dd3 = (double)d * d * d, dd2m = (double)d * d * m;
             if (h[4]) {  // g_y = A*(g_Ay) = R diag(g) R^H
-                ProfScope ps(ACE_K_APPLY_AH, st);
+                ProfScope ps(ACE_K_APPLY_AH, st, 8.0 * dd2m * act);
                 launch_zgemm(0, true, d, m, batch * d, a.R, m, 0, a.Pg, m, 0, a.G, nullptr, d, 0, 1, st);
             }
             {
-                ProfScope ps(ACE_K_ZSTEP, st);   // prox_trace: eig of z_old - step g_y, shrink
+                ProfScope ps(ACE_K_ZSTEP, st, 17.3 * dd3 * act);   // prox_trace: eig of z_old - step g_y, shrink
                 launch_pl_prox_in(a, st);
                 ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st));
                 launch_pl_assemble(a, st);
             }
             {
-                ProfScope ps(ACE_K_APPLY_G, st);   // z = V diag(s) V^H
+                ProfScope ps(ACE_K_APPLY_G, st, 8.0 * dd3 * act);   // z = V diag(s) V^H
                 launch_zgemm(0, true, d, d, d, a.VT, d, (long long)d * d, a.P, d, (long long)d * d, a.Znew, nullptr, d,
                              (long long)d * d, batch, st);
                 launch_pl_take_z(a, st);
             }
-            { ProfScope ps(ACE_K_APPLY_A, st); applyA(a.z, a.Az); }
+            { ProfScope ps(ACE_K_APPLY_A, st, 8.0 * dd2m * act); applyA(a.z, a.Az); }
             {
                 ProfScope ps(ACE_K_YSTEP, st);
                 launch_pl_make_x(a, st);

@@ -199,6 +199,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     pipe_carve(sz, d, &w);
     if (sz.off + 256 > workspace_bytes)
         return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", sz.off + 256, workspace_bytes);
+    poison_workspace(workspace, workspace_bytes, st);
     Carver cv{(char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255)};
     pipe_carve(cv, d, &w);
     const int ld = 4 * d.restarts + 1;
@@ -287,6 +288,19 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         ACE_HIP(hipGetLastError());
     }
 
+    if (cfg->stop_before_refine) {   // X_max and Y_max (on the train rows), rescaled; no rollback test
+        launch_fill(batch, -1.0, w.q_s, st);
+        ACE_HIP(hipMemsetAsync(w.Yr, 0, 16 * (size_t)batch * m, st));
+        ACE_HIP(hipMemcpy2DAsync(w.Yr, 16 * (size_t)m, w.Ymax, 16 * (size_t)d.mt, 16 * (size_t)d.mt, batch,
+                                 hipMemcpyDeviceToDevice, st));
+        launch_finish(n, m, d.mt, batch, w.q_s, w.Xmax, w.Yr, w.Xmax, w.Ymax, w.anorm, w.bnorm, Xo, Yo, nullptr, st);
+        if (quality) ACE_HIP(hipMemcpyAsync(quality, w.qlast, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+        if (stage_iters)
+            ACE_HIP(hipMemcpyAsync(stage_iters, w.stage_dev, 4 * (size_t)batch * ld, hipMemcpyDeviceToDevice, st));
+        if (status) ACE_HIP(hipMemcpyAsync(status, w.status_dev, 4 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+        ACE_HIP(hipGetLastError());
+        return ACE_OK;
+    }
     // ---- :89-101 refinement on the full A, r = 1, the last restart's use_rank_one
     w.Lf.A = w.An;
     ACE_TRY(linops_setup(w.Lf, batch, st));

@@ -193,6 +193,18 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
         dd[mt - 1] = C[(long long)(mt - 1) * mt + mt - 1].x;
         ee[mt - 1] = 0.0;
     }
+#ifdef ACE_DEBUG_SPEC
+    __syncthreads();
+    if (t == 0 && b < 2) {
+        int nd = 0, ne = 0, nt0 = 0, f = -1;
+        for (int i = 0; i < mt; ++i) {
+            if (!isfinite(dd[i])) { ++nd; if (f < 0) f = i; }
+            if (!isfinite(ee[i])) ++ne;
+            if (i + 1 < mt && taus[i].x == 0.0 && taus[i].y == 0.0) ++nt0;
+        }
+        printf("hetrd b %d mt %d nan dd %d ee %d first %d tau0 %d dd0 %g ee0 %g\n", b, mt, nd, ne, f, nt0, dd[0], ee[0]);
+    }
+#endif
 }
 
 // Sturm count: number of eigenvalues of the tridiagonal (d, e) below x.
@@ -370,6 +382,17 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         }
     }
     if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+#ifdef ACE_DEBUG_SPEC
+    __syncthreads();
+    if (t == 0 && b < 2) {
+        int nl = 0, nz = 0;
+        for (int q = 0; q < k; ++q) {
+            if (!isfinite(lam[q])) ++nl;
+            for (int i = 0; i < mt; ++i) nz += !isfinite(Z[(long long)q * mt + i]);
+        }
+        printf("trieig b %d k %d ncl %d nan lam %d z %d lam0 %g lam_k-1 %g tn %g\n", b, k, ncl, nl, nz, lam[0], lam[k - 1], tn);
+    }
+#endif
 }
 
 // u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),

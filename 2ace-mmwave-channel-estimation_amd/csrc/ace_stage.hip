@@ -55,6 +55,9 @@ __global__ __launch_bounds__(256) void init_r_kernel(int n, int m, int r, const 
         scale[t] = nB / sqrt(s2);
     }
     __syncthreads();
+#ifdef ACE_DEBUG_SPEC
+    if (t == 0 && b == 0) printf("init_r r %d m %d n %d nB %g scale0 %g scale1 %g P0sq0 %g\n", r, m, n, nB, scale[0], r > 1 ? scale[1] : 0.0, v[1]);
+#endif
     d2* X = reinterpret_cast<d2*>(Xp) + b * rn;
     d2* N = reinterpret_cast<d2*>(Np) + b * rn;
     for (long long k = t; k < rn; k += nt) {

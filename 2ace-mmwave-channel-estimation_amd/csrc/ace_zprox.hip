@@ -299,6 +299,11 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
     }
     block_sum<6>(v6, red);
+#ifdef ACE_DEBUG_SPEC
+    if (t == 0 && b == 0 && a.it <= 4)
+        printf("zstep v%d r %d it %d mu %g obj2 %g nAX2 %g nY2 %g | nX2 %g nZ2 %g jn2 %g dZ2 %g dAtY %g nAtY %g\n", VARIANT, r,
+               a.it, mu, st->obj2, st->nAX2, st->nY2, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]);
+#endif
     if (t == 0) flag_improved = iter_control(a, st, mu, v6[0], v6[1], v6[2], v6[3], v6[4], v6[5]) & 1;   // (no lazy_dual here)
     write_vbound();
     __syncthreads();

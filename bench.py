@@ -13,17 +13,24 @@ already resident in HBM when the timed region starts.  With N GPUs each rank
 solves its own 4096 realisations (weak scaling) and the recovered channels are
 gathered to rank 0 over RCCL inside the timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--mode MODE]
 
-``--mode pipeline`` measures a different, separately named metric: full
-inferLowRankV4_multi recoveries/s (3 restarts of spectral init + two r = 20 ADMM stages
-+ rank-one retries, then the r = 1 refinement; convergence mode, up to 500 iterations
-per stage), one partition set per batch.  It is never reported as the unit metric.
+Modes (each its own line; only ``unit`` is the headline metric):
+  unit       configs[1] (default; ``--variant A2nuclear`` = configs[2]); also measures regime P
+             (private codebooks) and the unit on the reference's own refinement input
+             (X0 = the pipeline's X_max, inferLowRankV4_multi.m:90-92)
+  config5    configs[4]: 32-ant multiresolution codebook, A2nuclear, 65 536 realisations in
+             total sharded over the ranks (strong scaling), one RCCL gather
+  pipeline   full inferLowRankV4_multi recoveries/s (a separately named metric)
+  phaselift  configs[3]: MyPhaseLift/TFOCS, 200 iterations, batch 512
+  beamformer downstream svd_beamformer codebooks/s
+  driver     latency of one drop-in driver call (main.py:427) on the reference probe codebook
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import pathlib
 import sys
@@ -38,9 +45,11 @@ METRIC = "channel recoveries/sec (32-ant, 256 RSS meas, 200 ADMM iters) @1/2/4/8
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= FP64 vector) dense peak, spec
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec
 PEAK_I8_TOPS = 5000.0     # MI355X int8 matrix dense peak, spec (2x the BF16 rate per clock)
-PROF_STRIDE = 7           # unit mode: kernel events on every 7th launch of each class (about 86 samples per
+PROF_STRIDE = 7           # unit mode: kernel events on every 7th launch of each kernel class (about 86 samples per
                           # class and stream over 3 steps; 200 mod 7 != 0, so the sampled iteration indices
                           # drift over the steps; the event pairs cost < 1 % of the throughput)
+CONFIG5_GLOBAL = 65536    # configs[4]: realisations over all GPUs
+ITER_CLASSES = ("pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep")
 
 
 def parse():
@@ -48,20 +57,549 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4096, help="recoveries per GPU per step")
+    ap.add_argument("--batch", type=int, default=0, help="recoveries per GPU per step (0 = the mode's default)")
+    ap.add_argument("--global-batch", type=int, default=CONFIG5_GLOBAL, help="config5: realisations over all GPUs")
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--variant", default="A2only", choices=["A2only", "A2nuclear"])
     ap.add_argument("--private", action="store_true", help="private codebook per realisation (regime P)")
-    ap.add_argument("--tx", type=int, default=32)
+    ap.add_argument("--tx", type=int, default=0, help="antennas per side (0 = the mode's default)")
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--seed", type=int, default=58659179)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-regime-p", action="store_true", help="unit mode: skip the regime-P measurement")
+    ap.add_argument("--no-refine-input", action="store_true",
+                    help="unit mode: skip the measurement on the pipeline's refinement input")
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
-    ap.add_argument("--mode", default="unit", choices=["unit", "pipeline", "phaselift", "beamformer"])
-    return ap.parse_args()
+    ap.add_argument("--mode", default="unit",
+                    choices=["unit", "config5", "pipeline", "phaselift", "beamformer", "driver"])
+    a = ap.parse_args()
+    if not a.tx:
+        a.tx = 16 if a.mode in ("beamformer", "driver") else 32
+    if not a.batch:
+        a.batch = {"phaselift": 512, "beamformer": 65536}.get(a.mode, 4096)
+    return a
 
+
+# ------------------------------------------------------------------ roofline accounting
+# Algorithmic work per realisation per iteration of each kernel class: f64 flops
+# (8 per complex MAC), int8 matrix-core ops, HBM bytes (complex128 = 16 B, each array once).
+
+def unit_flops(m, n, tx, rx):
+    """Algorithmic flops per kernel launch class per realisation per iteration (complex MAC = 8)."""
+    return {
+        "apply_A": 8.0 * m * n,
+        "apply_G": 8.0 * m * m,
+        "apply_K": 8.0 * m * m,
+        "apply_AH": 8.0 * n * m,
+    }
+
+
+def unit_i8_ops(m, n):
+    """int8 matrix-core ops executed per realisation per launch by the digit-plane applies
+    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC.
+    gyk_kernel runs no K Y in the steady state (lazy dual residual, from r02): its int8 work is the
+    rare pending-test resolution, not counted."""
+    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m), "apply_G": 0.0}
+
+
+def gyf_bytes(m, n):
+    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel (gyk + the fused apply_AH in
+    one launch, g on chip): read Y, M, AX (c128), B (f64) and Z; write AX, M, Y_new and Z' = X."""
+    return 16.0 * 6 * m + 8.0 * m + 16.0 * 2 * n
+
+
+def msp_bytes(m):
+    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel for a realisation in m-space
+    form (RealState::msp: Z implicit as Z0 + A^H S, no apply_AH pass): read Y, M, AX, S (c128) and
+    B (f64); write AX, M, Y_new and S' = S + g.  (opt_S, copied when the iterate improves, is not
+    counted: a bookkeeping copy like the deferred opt_X / opt_Y.)"""
+    return 16.0 * 8 * m + 8.0 * m
+
+
+def unit_bytes(m, n, tx, rx):
+    """Algorithmic HBM bytes per realisation per iteration of the steady-state A2only unit path
+    (complex128 = 16 B, each array read or written once):
+      apply_G (gyk):  read Y, M, AX (T = Y - M/mu - AX, the Y-step re-reads M and Y) and B (f64);
+                      write g, AX, M, Y_new.  No K Y and no dual-term reads (lazy dual residual);
+                      opt_Y is deferred to the Y ping-pong buffer (RealState::optysrc)
+      apply_AH (fused i8ah_kernel<false, true>): read g and Z; write Z' = X = Z + A^H g (W stays
+                      on chip); N is the exact zero vector and is neither read nor written
+      zstep:          certificate and iteration control from RealState (no vector traffic in the
+                      steady state; the full Z-step only for realisations the bound cannot certify)
+      apply_A (i8):   read Z, Y, M; write T -- cold iterations only (A V = AX in the steady state)"""
+    return {
+        "zstep": 0.0,
+        "apply_G": 16.0 * 7 * m + 8.0 * m,
+        "apply_A": 16.0 * (n + 3 * m),
+        "apply_AH": 16.0 * (m + 2 * n),
+    }
+
+
+def nuclear_bytes(m, n):
+    """The A2nuclear unit path (configs[2], configs[4]): its soft threshold never leaves Z' = E, so N
+    is nonzero and A V is formed every iteration:
+      apply_G (gyk_kernel): read Y, M, AX, B and Z, N (the digit planes of V = Z - N/mu);
+                            write g, AX, M, Y_new
+      apply_AH (i8ah_kernel<false, false>): read g, write W = A^H g
+      zstep (one-wave, soft threshold): read W, Z, N; write Z', N'"""
+    return {"apply_G": 16.0 * 7 * m + 8.0 * m + 32.0 * n, "apply_AH": 16.0 * (m + n), "zstep": 80.0 * n}
+
+
+def private_bytes(m, n):
+    """Algorithmic HBM bytes per realisation per iteration of pgk_kernel (private phase-code
+    codebooks, ace_private.hip) in the steady state (A V = AX):
+      G_b = (I + A_b A_b^H)^{-1}: its Hermitian lower triangle, m (m + 1) / 2 complex128
+      A_b^H: 2-bit codes, m n / 4 bytes
+      read Y, M, AX (c128) and B (f64); write AX, M, Y_new; write W = A^H g (n c128)"""
+    return 16.0 * m * (m + 1) / 2 + m * n / 4.0 + 16.0 * 6 * m + 8.0 * m + 16.0 * n
+
+
+def private_ops(m, n):
+    """pgk_kernel's matrix-core and vector work per realisation per iteration: int8 ops of the three
+    digit-plane right-hand sides (g, Y, Y - Y0; 8 digits each) times the 2x2 real expansion of A^H,
+    and f64 flops of g = G T (8 per complex MAC over the full Hermitian G)."""
+    return {"int8": 2.0 * 3 * 8 * (2 * n) * (2 * m), "f64": 8.0 * m * m}
+
+
+def unit_resources(k, m, n, *, variant, pc, gyf, gyk, i8, msp_frac):
+    """Per-realisation work of one launch of kernel class k on the unit path: {resource: amount}
+    with resources f64 (flops), int8 (ops), hbm (bytes).  {} = latency-bound, no roofline."""
+    uf, io, ub = unit_flops(m, n, 0, 0), unit_i8_ops(m, n), unit_bytes(m, n, 0, 0)
+    if pc:
+        po = private_ops(m, n)
+        return {"hbm": private_bytes(m, n), "int8": po["int8"], "f64": po["f64"]} if k == "apply_G" else {}
+    if variant == "A2nuclear" and i8:
+        nb = nuclear_bytes(m, n)
+        if k == "apply_G" and gyk:
+            return {"f64": uf["apply_G"], "int8": io["apply_A"], "hbm": nb["apply_G"]}
+        if k == "apply_AH":
+            return {"int8": io["apply_AH"], "hbm": nb["apply_AH"]}
+        if k == "zstep":
+            return {"hbm": nb["zstep"]}
+    if k == "apply_G" and gyf:   # gyk + the fused apply_AH; m-space realisations skip the int8 pass
+        return {"f64": uf[k], "int8": io["apply_AH"] * (1.0 - msp_frac),
+                "hbm": msp_frac * msp_bytes(m) + (1.0 - msp_frac) * gyf_bytes(m, n)}
+    if k == "apply_G" and gyk:
+        return {"f64": uf[k], "hbm": ub[k]}
+    if k in io and i8 and k != "apply_G":
+        return {"int8": io[k], "hbm": ub[k]}
+    if k in uf:
+        return {"f64": uf[k]}
+    return {}
+
+
+_RES = {  # resource -> (peak per second, unit label, unit scale, roofline bound name, amount key)
+    "f64": (PEAK_FP64_TFLOPS * 1e12, "TFLOP/s", 1e12, "mfma", "flops_per_launch"),
+    "int8": (PEAK_I8_TOPS * 1e12, "TOP/s", 1e12, "mfma", "ops_per_launch"),
+    "hbm": (PEAK_HBM_GBS * 1e9, "GB/s", 1e9, "hbm", "bytes_per_launch"),
+}
+
+
+def roofline_from(kernel, avg_s, res, bounds=None, note=None):
+    """Roofline entry of one launch of `kernel` (avg_s seconds) doing `res` = {resource: amount}:
+    the resource with the largest time at peak is the bound; the others go to other_resources;
+    serial_frac = (sum of the times at peak) / launch time (phases that run one after another)."""
+    bounds = bounds or {}
+    t = {r: a / _RES[r][0] for r, a in res.items() if a > 0}
+    main = max(t, key=t.get)
+
+    def ent(r):
+        peak, unit, scale, bound, key = _RES[r]
+        a = res[r]
+        return {"bound": bounds.get(r, bound), "achieved": round(a / avg_s / scale, 3), "peak": peak / scale,
+                "unit": unit, "frac": round(a / avg_s / peak, 4), key: a}
+
+    out = ent(main)
+    out.update({"traffic": None, "kernel": kernel, "resource": main,
+                "other_resources": {r: ent(r) for r in t if r != main},
+                "serial_frac": round(sum(t.values()) / avg_s, 4)})
+    if note:
+        out["flop_note"] = note
+    return out
+
+
+def _pmc_traffic(kernel_prefix, tag):
+    """HBM bytes per launch (PMC FETCH_SIZE, gfx950-corrected, + WRITE_SIZE) of the kernel whose name
+    starts with `kernel_prefix`, from the newest committed profiles/r<R>_v<V>[_<tag>]_pmc_hbm.json
+    measured on the same workload (tag: unit | private | nuclear | config5; files without a tag are
+    unit-mode passes, *_private_* regime-P passes), or None.  Written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc passes."""
+    def parse_name(f):   # r<round>_v<version>[_<tag>]_pmc_hbm.json
+        parts = f.name[: -len("_pmc_hbm.json")].split("_")
+        try:
+            return (int(parts[0][1:]), int(parts[1][1:])), "_".join(parts[2:]) or "unit"
+        except (IndexError, ValueError):
+            return None, None
+    files = []
+    for f in (ROOT / "profiles").glob("r*_pmc_hbm.json"):
+        ver, ftag = parse_name(f)
+        if ver is not None and ftag == tag:
+            files.append((ver, f))
+    for _, f in sorted(files, reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.split(" grid=")[0].strip().startswith(kernel_prefix):
+                return round(v["hbm_bytes"]), f"profiles/{f.name}"
+    return None
+
+
+PMC_KERNEL = {  # kernel-class -> kernel name prefix in the PMC profiles, per workload tag
+    "unit": {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false, true>",
+             "apply_G": "gyf_kernel"},
+    "private": {"zstep": "zstep1w_kernel<false>", "apply_G": "pgk_kernel"},
+    "nuclear": {"zstep": "zstep1w_kernel<false>", "apply_AH": "i8ah_kernel<false, false>", "apply_G": "gyk_kernel"},
+}
+PMC_KERNEL["config5"] = PMC_KERNEL["nuclear"]
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def _cores():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _blas_threads():
+    for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
+        if os.environ.get(k, "").isdigit():
+            return int(os.environ[k])
+    return len(os.sched_getaffinity(0))
+
+
+def _max_over_ranks(elapsed, dev, world):
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _prof_read(nclass=10):
+    """(total ms, launches, algorithmic flops) per kernel class since ace_prof_start."""
+    import ctypes as C
+    from ace_amd._lib import LIB, check
+    kt, kn, kw = (C.c_double * nclass)(), (C.c_int32 * nclass)(), (C.c_double * nclass)()
+    check(LIB.ace_prof_stop(kt, kn))
+    check(LIB.ace_prof_work(kw))
+    return list(kt), list(kn), list(kw)
+
+
+def work_roofline(kt, kn, kw, note):
+    """Roofline of the dominant kernel class among those whose launches carry an algorithmic flop
+    count (ace_prof_work: the f64 GEMM-shaped applies and prox steps), plus every class's share
+    of the device time."""
+    from ace_amd._lib import KERNEL_CLASSES
+    tot = sum(kt)
+    shares = {KERNEL_CLASSES[i]: round(kt[i] / tot, 4) for i in range(len(kt)) if kn[i]}
+    cand = [i for i in range(len(kt)) if kn[i] and kw[i] > 0]
+    if not cand:
+        return None, shares
+    i = max(cand, key=lambda c: kt[c])
+    avg_s = kt[i] / kn[i] * 1e-3
+    r = roofline_from(KERNEL_CLASSES[i], avg_s, {"f64": kw[i] / kn[i]}, note=note)
+    r["launches"] = kn[i]
+    r["device_time_share"] = shares[KERNEL_CLASSES[i]]
+    return r, shares
+
+
+# ------------------------------------------------------------------ CPU baselines
+
+def cpu_baseline(args, n_samples, private, variant=None, A_host=None):
+    """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
+    timed on the host cores on a bounded sample of the same workload.  Shared codebook: one
+    U = inv(A'A + I) amortised over a GPU-sized batch, as on the GPU.  Private codebooks: one U
+    per realisation, inside the timed sample (as on the GPU, whose setup is in the timed step)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ace_oracle_c as OC
+    from ace_amd import synth
+    tx = args.tx
+    n = tx * tx
+    cores = _cores()
+    variant = variant or args.variant
+    if A_host is not None:   # a given shared codebook (config5): the same synthetic channels on it
+        A = A_host[None]
+        H = np.stack([synth.channel(args.seed, c, tx, tx) for c in range(n_samples)])
+        B = np.stack([synth.measurements(args.seed, c, A[0], H[c]) for c in range(n_samples)])
+        X0 = np.stack([synth.initial_iterate(args.seed, c, H[c]) for c in range(n_samples)])
+        nb = np.sqrt(np.sum(B * B, axis=1))
+        B, X0 = B / nb[:, None], X0 / nb[:, None]
+    else:
+        A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not private)
+    var = 0 if variant == "A2only" else 1
+    t0 = time.perf_counter()
+    if private:
+        U = np.stack([OC.make_U(a, nthreads=cores) for a in A])
+    else:
+        U = OC.make_U(A[0], nthreads=cores)[None]
+    t_setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    OC.infer_admm_r1_batch(A if private else A[:1], U, B, X0, tx, tx, variant=var, fixed_iters=True,
+                           maxiter=args.iters, nthreads=cores)
+    t_solve = time.perf_counter() - t0
+    if private:
+        t_total = t_solve + t_setup
+        setup_note = f"U=inv(A'A+I) per realisation {t_setup:.2f}s"
+    else:
+        t_total = t_solve + t_setup * n_samples / args.batch
+        setup_note = f"U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}"
+    return {"value": n_samples / t_total, "unit": "recoveries/s", "cores": cores, "kind": "port",
+            "sample": (f"{n_samples} recoveries of the same workload ({variant}, {args.iters} fixed iters, "
+                       f"m={args.m}, n={n}, {'private' if private else 'shared'} codebook) on {cores} threads of "
+                       f"{_cpu_model()}; {setup_note}; solve {t_solve:.2f}s")}
+
+
+# ------------------------------------------------------------------ unit / config5
+
+def unit_bench(args, private, dev, rank, world, workload=None):
+    """One unit-metric measurement (regime S or P, or a given workload); the JSON line dict on rank 0.
+    workload: {"tag", "name", "variant", "A" (device codebook), "A_host", "bsz", "first", "counts",
+    "scaling", "codebook", "X0" (device X0), "x0_note"} -- all optional."""
+    import torch
+    import ace_amd
+    from ace_amd import infer_admm_batch, synth_problem
+    from ace_amd._lib import LIB, KERNEL_CLASSES, check
+    from ace_amd.dist import gather_to_root
+    import ctypes as C
+
+    wl = workload or {}
+    tx = args.tx
+    variant = wl.get("variant", args.variant)
+    n, m = tx * tx, args.m
+    bsz = wl.get("bsz", args.batch)
+    first = wl.get("first", rank * bsz)
+    counts = wl.get("counts", [bsz] * world)
+    A, B, X0, H = synth_problem(args.seed, first, bsz, m, tx, tx, a_shared=not private, device=dev, A=wl.get("A"))
+    if wl.get("X0") is not None:
+        X0 = wl["X0"]
+    ws = ace_amd.solver.Workspace()
+    out = None
+
+    def step():
+        nonlocal out
+        out = infer_admm_batch(A, B, X0, tx, tx, variant=variant, maxiter=args.iters, fixed_iters=True,
+                               out=out, workspace=ws)
+        if world > 1:   # the single result gather of recovered channels over RCCL/xGMI (north_star)
+            gather_to_root(out.X, counts)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    prof = not args.no_prof
+    if prof:   # HIP event pairs on every PROF_STRIDE-th launch of each kernel class
+        check(LIB.ace_prof_sample(PROF_STRIDE, 0))
+        check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
+    torch.cuda.synchronize()
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    elapsed = time.perf_counter() - t0
+    msp_steps = C.c_longlong(0)
+    if prof:
+        kt, kn, _ = _prof_read()
+        check(LIB.ace_prof_msp_steps(C.byref(msp_steps)))
+    elapsed = _max_over_ranks(elapsed, dev, world)
+    it_ok = bool((out.iters == args.iters).all().item())
+    finite = bool(torch.isfinite(torch.view_as_real(out.X)).all().item())
+    if rank != 0:
+        return None
+
+    total = sum(counts) * args.steps
+    kernels, roof, roof_gemm = {}, None, None
+    tag = wl.get("tag", "private" if private else ("nuclear" if variant == "A2nuclear" else "unit"))
+    msp_frac = 0.0
+    if prof:
+        for i, name in enumerate(KERNEL_CLASSES):
+            if kn[i]:
+                kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
+        # the int8 digit-plane applies run for a phase-code codebook in the r = 1 iteration
+        i8 = (not private) and os.environ.get("ACE_NO_I8") != "1"
+        # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
+        # every launch of an iteration kernel covers bsz / nsplit realisations
+        nsplit = 1
+        if i8 and m <= 256:
+            nsplit = max(1, min(4, int(os.environ.get("ACE_SPLIT", "2"))))
+            while nsplit > 1 and bsz // nsplit < 256:
+                nsplit -= 1
+        per_launch = -(-bsz // nsplit)
+        env_on = lambda k: os.environ.get(k) != "0"   # noqa: E731
+        gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
+        # m-space steps (ACE_MSPACE) for A2only: every iteration is gyf_kernel + Z-step
+        msp_on = env_on("ACE_MSPACE") and variant == "A2only"
+        gyf = gyk and variant == "A2only" and (nsplit > 1 or msp_on) and all(
+            env_on(k) for k in ("ACE_GYF", "ACE_FUSE", "ACE_LAZY_DUAL", "ACE_LEAN"))
+        # share of the realisation-iterations gyf_kernel settled in m-space form (no apply_AH pass,
+        # no Z traffic: ace_prof_msp_steps); the per-launch work below is averaged with it
+        msp_frac = msp_steps.value / float(args.steps * bsz * args.iters) if msp_on else 0.0
+        # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
+        pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
+        ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac)
+        timed = [k for k in kernels if k in ITER_CLASSES and unit_resources(k, m, n, **ctx)]
+        # every timed class launches once per iteration: dominant = largest average launch
+        dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
+
+        def roof_of(k):
+            res = {r: a * per_launch for r, a in unit_resources(k, m, n, **ctx).items()}
+            name = "apply_G (gyf_kernel)" if (k == "apply_G" and gyf) else k
+            note = None
+            if k == "apply_G" and gyf:
+                note = ("gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per complex MAC), the "
+                        "Y-step, then W = A^H g (int8 digit planes) with the certified Z-step pass (Z in, Z' out) "
+                        "in its epilogue, one phase after another in each work-group; a realisation in m-space "
+                        "form (msp_frac of the realisation-iterations) skips the int8 pass and the Z traffic and "
+                        "moves S in / S' out instead (bench.msp_bytes); bound = the resource with the largest "
+                        "time at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time")
+            elif variant == "A2nuclear" and i8:
+                note = ("A2nuclear unit path (bench.nuclear_bytes): A V in gyk_kernel every iteration, plain "
+                        "apply_AH, the soft-threshold Z-step streams W, Z, N")
+            r = roofline_from(name, kernels[k]["avg_ms"] * 1e-3, res, bounds={"f64": "valu"} if pc else None,
+                              note=note)
+            if gyf:
+                r["msp_frac"] = round(msp_frac, 4)
+            r["realisations_per_launch"] = per_launch
+            # the nsplit sub-batch launches of a class run at the same time on disjoint CUs (rocprofv3
+            # kernel trace, tools/timeline.py): the chip-level rate is nsplit x the per-launch rate
+            r["concurrent_launches"] = nsplit
+            r["chip_frac"] = round(r["frac"] * nsplit, 4)
+            pmc = PMC_KERNEL.get(tag, {}).get(k)
+            tr = _pmc_traffic(pmc, tag) if pmc else None
+            if tr:
+                r["traffic"], r["traffic_source"] = tr
+                if res.get("hbm"):
+                    r["traffic_per_algorithmic"] = round(tr[0] / res["hbm"], 3)
+            return r
+
+        roof = roof_of(dom)
+        roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
+                        f"region, on every {PROF_STRIDE}th launch of each kernel class); peaks: MI355X spec (FP64 "
+                        "78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); traffic: PMC FETCH_SIZE+WRITE_SIZE per launch "
+                        "from the profile named in traffic_source (same workload tag)")
+        if not pc:
+            fk = [k for k in timed if "f64" in unit_resources(k, m, n, **ctx)]
+            if fk:
+                roof_gemm = roof_of(max(fk, key=lambda k: kernels[k]["avg_ms"]))
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        ns = args.cpu_recoveries or (32 if private else 256)
+        cpu = cpu_baseline(args, ns, private, variant, wl.get("A_host"))
+    if variant == "A2only" and tx == 32 and m == 256:
+        default_name = ("config 2: 32-ant URA (n=1024), 256 random-codebook RSS meas, A2only ADMM refinement "
+                        "solve (r=1), 200 fixed iterations")
+    elif tx == 32 and m == 256:
+        default_name = "config 3: 32-ant, 256 meas, A2nuclear ADMM refinement solve (r=1), 200 fixed iterations"
+    else:
+        default_name = f"{variant}, tx=rx={tx}, m={m}, {args.iters} fixed iterations"
+    return {
+        "metric": METRIC,
+        "value": round(total / elapsed, 2),
+        "unit": "recoveries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": wl.get("scaling", "weak"),
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Generate_Channel/Random_Phase_State/Generate_Measurement semantics, 30 dB SNR)",
+        "config": {
+            "workload": wl.get("name", default_name),
+            "variant": variant,
+            "codebook": wl.get("codebook", "private per realisation (regime P)" if private else "shared (regime S)"),
+            "batch_per_gpu": bsz,
+            "global_batch": sum(counts),
+            "m": m, "n": n, "iters": args.iters,
+            "x0": wl.get("x0_note", "H + 0.5 CN noise (synthetic warm start; refine_input measures the "
+                                    "reference's own refinement input)"),
+            "parallelism": f"dp{world} (realisation sharding, RCCL gather of X to rank 0)",
+        },
+        "roofline": roof,
+        "roofline_gemm": roof_gemm,
+        "cpu_baseline": cpu,
+        "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+        "msp_frac": round(msp_frac, 4),
+        "checks": {"all_iters_ran": it_ok, "finite": finite},
+    }
+
+
+def refine_input_bench(args, dev, rank, world):
+    """The unit on the reference's own refinement input: X0 = X_max of the 3-restart pipeline
+    (inferLowRankV4_multi.m:90-92: spectral init, the r = 20 stages, rank-one retries, best of
+    restarts) on the same synthetic batch, instead of the bench's H + 0.5 noise warm start.  The
+    synthetic A has ||A||_F = sqrt(m) and B is unit-norm, so X_max is already in the unit's
+    coordinates (A_norm = B_norm = 1, :27-38)."""
+    import torch
+    from ace_amd import synth_problem, infer_low_rank_pipeline_batch, draw_partitions
+    tx, m, bsz = args.tx, args.m, args.batch
+    A, B, _, _ = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
+    tr = draw_partitions(np.random.default_rng(args.seed), m, 3)
+    t0 = time.perf_counter()
+    pr = infer_low_rank_pipeline_batch(A, B, tx, tx, tr, stop_before_refine=True)
+    torch.cuda.synchronize()
+    t_pipe = time.perf_counter() - t0
+    X0 = pr.X.contiguous()
+    saved = args.no_cpu_baseline
+    args.no_cpu_baseline = True
+    line = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max"})
+    args.no_cpu_baseline = saved
+    if rank != 0:
+        return None
+    q = pr.quality.cpu().numpy()
+    return {"value": line["value"], "unit": "recoveries/s", "ms_per_step": line["ms_per_step"],
+            "msp_frac": line["msp_frac"],
+            "x0": "X_max of inferLowRankV4_multi's 3 restarts (:90-92) on the same batch (ace_pipeline_solve_batch "
+                  "with stop_before_refine)",
+            "pipeline_s": round(t_pipe, 2), "quality_median": float(np.median(q)),
+            "roofline_frac": line["roofline"]["frac"] if line["roofline"] else None,
+            "kernels_ms": line["kernels_ms"], "checks": line["checks"]}
+
+
+def config5_workload(args, rank, world, dev):
+    """configs[4]: the 32-antenna multiresolution codebook (ace_amd.synth.multires_codes, the
+    builder-defined analogue of generate_tx_codebook_multires_16ant.py / processsing_codebook_
+    multires.m), M = m rows drawn by randperm within the tier ..._multiresolution.m:137-144 selects
+    (the same rows on every rank), A2nuclear, the global batch sharded contiguously over the ranks."""
+    import torch
+    from ace_amd import synth
+    from ace_amd.dist import shard_range
+    tx, m = args.tx, args.m
+    lens, th = synth.multires_tiers(tx)
+    rows, tier = synth.multires_rows(args.seed, tx, m)
+    A_host = synth.multires_codebook(args.seed, tx, rows)
+    A = torch.from_numpy(A_host[None]).to(dev)
+    counts = [shard_range(args.global_batch, world, r)[1] for r in range(world)]
+    first, bsz = shard_range(args.global_batch, world, rank)
+    name = (f"config 5: 32-ant multiresolution codebook (tier {tier}: {['4', '2', '1'][tier]}-antenna groups, "
+            f"{m} of {lens[tier]} rows), A2nuclear ADMM refinement solve (r=1), {args.iters} fixed iterations, "
+            f"{args.global_batch} realisations over {world} GPU(s)")
+    return {"tag": "config5", "name": name, "variant": "A2nuclear", "A": A, "A_host": A_host, "bsz": bsz,
+            "first": first, "counts": counts, "scaling": "strong",
+            "codebook": f"shared multiresolution rows (tier {tier}, thresholds {list(th)})"}
+
+
+# ------------------------------------------------------------------ other modes
 
 PIPE_METRIC = "pipeline recoveries/sec (inferLowRankV4_multi, 32-ant, 256 RSS meas, convergence mode)"
 
@@ -72,7 +610,6 @@ def bench_pipeline(args, dev, rank, world):
     import ace_amd
     from ace_amd import infer_low_rank_pipeline_batch, synth_problem, draw_partitions
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
-    import ctypes as C
     tx, m, bsz = args.tx, args.m, args.batch
     restarts = 3 if args.variant == "A2only" else 1
     A, B, _, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
@@ -87,22 +624,22 @@ def bench_pipeline(args, dev, rank, world):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    _barrier(world)
     if not args.no_prof:
-        check(LIB.ace_prof_start(200000))
+        check(LIB.ace_prof_sample(1, 0))
+        check(LIB.ace_prof_start(400000))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    _barrier(world)
     elapsed = time.perf_counter() - t0
-    kt = (C.c_double * 10)()
-    kn = (C.c_int32 * 10)()
+    roof, shares, kt = None, None, None
     if not args.no_prof:
-        check(LIB.ace_prof_stop(kt, kn))
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        kt, kn, kw = _prof_read()
+        roof, shares = work_roofline(kt, kn, kw, "f64 flops of the GEMM-shaped applies as launched (all batch*r "
+                                     "vectors of the stage, 8 per complex MAC; ace_prof_work)")
+    elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return
     its = res.stage_iters.cpu().numpy()
@@ -124,9 +661,29 @@ def bench_pipeline(args, dev, rank, world):
         "rel_err_note": ("phase-aligned error vs the synthetic channel; m < n magnitude measurements are "
                          "underdetermined and the reference algorithm (oracle) does not recover H there "
                          "either: see DESIGN.md §3 (recovery regime)") if m < tx * tx else None,
-        "kernels_total_ms": {KERNEL_CLASSES[i]: round(kt[i], 2) for i in range(10) if kn[i]},
+        "roofline": roof,
+        "device_time_shares": shares,
+        "kernels_total_ms": {KERNEL_CLASSES[i]: round(kt[i], 2) for i in range(10) if kt[i]} if kt else None,
     }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline_pipeline(args, A[0].cpu().numpy(), B.cpu().numpy(), tr)
     print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_pipeline(args, A, B, tr):
+    """The numpy oracle pipeline (oracle/ace_oracle.py::infer_low_rank_pipeline, the reference's
+    algorithm line by line; BLAS threads as the host provides) on a bounded sample of the batch."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ace_oracle as O
+    k, t0 = 0, time.perf_counter()
+    while k < min(len(B), args.cpu_recoveries or 8) and (k == 0 or time.perf_counter() - t0 < 20.0):
+        O.infer_low_rank_pipeline(A, B[k], args.tx, args.tx, list(tr),
+                                  variant=O.VARIANT_A2ONLY if args.variant == "A2only" else O.VARIANT_NUCLEAR)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(k / dt, 4), "unit": "recoveries/s", "cores": _blas_threads(), "kind": "port",
+            "sample": f"{k} recoveries of the same batch through oracle/ace_oracle.py (numpy, BLAS threads as "
+                      f"available) on {_cpu_model()}"}
 
 
 PL_METRIC = "PhaseLift recoveries/sec (MyPhaseLift/TFOCS, 32-ant, 256 meas, 200 TFOCS iters)"
@@ -138,7 +695,6 @@ def bench_phaselift(args, dev, rank, world):
     import ace_amd
     from ace_amd import phaselift_batch, synth_problem
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
-    import ctypes as C
     tx, m, bsz = args.tx, args.m, args.batch
     A, B, _, _ = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
     Phi = A[0] * float(np.sqrt(tx * tx))                       # unit-modulus codebook rows
@@ -153,28 +709,32 @@ def bench_phaselift(args, dev, rank, world):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    _barrier(world)
     if not args.no_prof:
+        check(LIB.ace_prof_sample(1, 0))
         check(LIB.ace_prof_start(400000))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    _barrier(world)
     elapsed = time.perf_counter() - t0
-    kt = (C.c_double * 10)()
-    kn = (C.c_int32 * 10)()
+    roof, shares, kt = None, None, None
     if not args.no_prof:
-        check(LIB.ace_prof_stop(kt, kn))
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        kt, kn, kw = _prof_read()
+        roof, shares = work_roofline(
+            kt, kn, kw, "algorithmic f64 flops per realisation in the backtracking step (8 per complex MAC) in "
+            "the d = min(m, n) reduced coordinates: prox eig 17.3 d^3 (SURVEY.md §8d's count for a dense Hermitian "
+            "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2")
+    elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return
     its = res.iters.cpu().numpy()
     names = {"setup": "setup (reduction)", "pre": "y, A_y, gradient", "apply_AH": "A*(g) GEMM",
              "zstep": "prox eig (tridiag+bisect+invit+backxf)", "apply_G": "prox assembly GEMM",
              "apply_A": "A(z) GEMM", "ystep": "x update, backtracking", "final": "final eig + map"}
+    if roof:
+        roof["kernel"] = names.get(roof["kernel"], roof["kernel"])
     line = {
         "metric": PL_METRIC, "value": round(world * bsz * args.steps / elapsed, 3), "unit": "recoveries/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -183,10 +743,30 @@ def bench_phaselift(args, dev, rank, world):
         "config": {"workload": f"config 4: MyPhaseLift, tx=rx={tx} (n={tx * tx}), m={m}, {args.iters} TFOCS iters",
                    "batch_per_gpu": bsz, "reduced_dim": min(m, tx * tx)},
         "iters_all": bool((its == args.iters).all()),
+        "roofline": roof,
+        "device_time_shares": {names.get(k, k): v for k, v in shares.items()} if shares else None,
         "kernels_total_ms": {names.get(KERNEL_CLASSES[i], KERNEL_CLASSES[i]): round(kt[i], 2)
-                             for i in range(10) if kn[i]},
+                             for i in range(10) if kt[i]} if kt else None,
     }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline_phaselift(args, Phi.cpu().numpy(), b[:4].cpu().numpy())
     print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_phaselift(args, Phi, b):
+    """The TFOCS oracle (oracle/tfocs_oracle.py::my_phaselift_reduced: MyPhaseLift + solver_TraceLS in
+    the coordinates of range(Phi^H), the dense iteration up to rounding; numpy BLAS / LAPACK threads as
+    available), the same 200 iterations, on a bounded sample of the batch."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import tfocs_oracle as T
+    k, t0 = 0, time.perf_counter()
+    while k < len(b) and (k == 0 or time.perf_counter() - t0 < 20.0):
+        T.my_phaselift_reduced(b[k], Phi, maxIts=args.iters)
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(k / dt, 4), "unit": "recoveries/s", "cores": _blas_threads(), "kind": "port",
+            "sample": f"{k} recoveries of the same batch, {args.iters} TFOCS iterations, through "
+                      f"oracle/tfocs_oracle.my_phaselift_reduced (numpy) on {_cpu_model()}"}
 
 
 BF_METRIC = "beamformer codebooks/sec (svd_beamformer: 2 zgesdd + 2-bit quantise + all-pairs search, 16x16)"
@@ -199,8 +779,7 @@ def bench_beamformer(args, dev, rank, world):
     in HBM; --tx selects the array size (default 16 in this mode)."""
     import torch
     from ace_amd import svd_beamformer_batch, synth_problem
-    tx = args.tx if args.tx != 32 else 16
-    bsz = args.batch if args.batch != 4096 else 65536
+    tx, bsz = args.tx, args.batch
     _, _, X0, _ = synth_problem(args.seed, rank * bsz, bsz, 8, tx, tx, x0_noise=0.3, device=dev)
     H = X0.reshape(bsz, tx, tx).contiguous()
     res = None
@@ -212,9 +791,7 @@ def bench_beamformer(args, dev, rank, world):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    _barrier(world)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
@@ -222,13 +799,10 @@ def bench_beamformer(args, dev, rank, world):
         step()
     ev1.record()
     torch.cuda.synchronize()
+    _barrier(world)
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return
     st = res.status.cpu().numpy()
@@ -268,151 +842,100 @@ def cpu_baseline_beamformer(tx, Hs):
                       f"on {_cpu_model()}"}
 
 
-def unit_flops(m, n, tx, rx):
-    """Algorithmic flops per kernel launch class per realisation per iteration (complex MAC = 8)."""
-    return {
-        "apply_A": 8.0 * m * n,
-        "apply_G": 8.0 * m * m,
-        "apply_K": 8.0 * m * m,
-        "apply_AH": 8.0 * n * m,
-    }
+DRIVER_METRIC = ("drop-in driver call latency (channel_recovery_ADMM_v2_simulation_A2only, 16x16, "
+                 "reference probe codebook, 8-point M sweep)")
+DRIVER_SEED_ID = 3
 
 
-def unit_i8_ops(m, n):
-    """int8 matrix-core ops executed per realisation per launch by the digit-plane applies
-    (ace_i8gemm.hip): 8 digit planes x the 2x2 real expansion (2m x 2n) x 2 ops per MAC.
-    gyk_kernel runs no K Y in the steady state (lazy dual residual, from r02): its int8 work is the
-    rare pending-test resolution, not counted."""
-    return {"apply_A": 2.0 * 8 * (2 * m) * (2 * n), "apply_AH": 2.0 * 8 * (2 * n) * (2 * m), "apply_G": 0.0}
-
-
-def gyf_bytes(m, n):
-    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel (gyk + the fused apply_AH in
-    one launch, g on chip): read Y, M, AX (c128), B (f64) and Z; write AX, M, Y_new and Z' = X."""
-    return 16.0 * 6 * m + 8.0 * m + 16.0 * 2 * n
-
-
-def msp_bytes(m):
-    """Algorithmic HBM bytes per realisation per iteration of gyf_kernel for a realisation in m-space
-    form (RealState::msp: Z implicit as Z0 + A^H S, no apply_AH pass): read Y, M, AX, S (c128) and
-    B (f64); write AX, M, Y_new and S' = S + g.  (opt_S, copied when the iterate improves, is not
-    counted: a bookkeeping copy like the deferred opt_X / opt_Y.)"""
-    return 16.0 * 8 * m + 8.0 * m
-
-
-def unit_bytes(m, n, tx, rx):
-    """Algorithmic HBM bytes per realisation per iteration of the steady-state unit path
-    (complex128 = 16 B, each array read or written once):
-      apply_G (gyk):  read Y, M, AX (T = Y - M/mu - AX, the Y-step re-reads M and Y) and B (f64);
-                      write g, AX, M, Y_new.  No K Y and no dual-term reads (lazy dual residual);
-                      opt_Y is deferred to the Y ping-pong buffer (RealState::optysrc)
-      apply_AH (fused i8ah_kernel<false, true>): read g and Z; write Z' = X = Z + A^H g (W stays
-                      on chip); N is the exact zero vector and is neither read nor written
-      zstep:          certificate and iteration control from RealState (no vector traffic in the
-                      steady state; the full Z-step only for realisations the bound cannot certify)
-      apply_A (i8):   read Z, Y, M; write T -- cold iterations only (A V = AX in the steady state)"""
-    return {
-        "zstep": 0.0,
-        "apply_G": 16.0 * 7 * m + 8.0 * m,
-        "apply_A": 16.0 * (n + 3 * m),
-        "apply_AH": 16.0 * (m + 2 * n),
-    }
-
-
-def private_bytes(m, n):
-    """Algorithmic HBM bytes per realisation per iteration of pgk_kernel (private phase-code
-    codebooks, ace_private.hip) in the steady state (A V = AX):
-      G_b = (I + A_b A_b^H)^{-1}: its Hermitian lower triangle, m (m + 1) / 2 complex128
-      A_b^H: 2-bit codes, m n / 4 bytes
-      read Y, M, AX (c128) and B (f64); write AX, M, Y_new; write W = A^H g (n c128)"""
-    return 16.0 * m * (m + 1) / 2 + m * n / 4.0 + 16.0 * 6 * m + 8.0 * m + 16.0 * n
-
-
-def private_ops(m, n):
-    """pgk_kernel's matrix-core and vector work per realisation per iteration: int8 ops of the three
-    digit-plane right-hand sides (g, Y, Y - Y0; 8 digits each) times the 2x2 real expansion of A^H,
-    and f64 flops of g = G T (8 per complex MAC over the full Hermitian G)."""
-    return {"int8": 2.0 * 3 * 8 * (2 * n) * (2 * m), "f64": 8.0 * m * m}
-
-
-def cpu_baseline(args, n_samples, private):
-    """C restatement oracle (oracle/ace_oracle.c, the reference's U-form algorithm)
-    timed on the host cores on a bounded sample of the same workload.  Shared codebook: one
-    U = inv(A'A + I) amortised over a GPU-sized batch, as on the GPU.  Private codebooks: one U
-    per realisation, inside the timed sample (as on the GPU, whose setup is in the timed step)."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import ace_oracle_c as OC
+def driver_trace(tx, seed):
+    """main.py's inputs to the driver: the reference's probing codebook (tests/golden/
+    ref_codebooks_16x16_packed.npz = codebook/codebook_mat/random_probe_cb_16x16.mat as 2-bit codes)
+    as |cb| and angle(cb) (main.py:301-302), RSS in dBm (main.py:113) of a synthetic channel."""
     from ace_amd import synth
-    tx = args.tx
-    n = tx * tx
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    A, B, X0, _ = synth.problem(args.seed, 0, n_samples, args.m, tx, tx, a_shared=not private)
-    var = 0 if args.variant == "A2only" else 1
+    p = np.load(ROOT / "tests" / "golden" / "ref_codebooks_16x16_packed.npz")["random"]
+    k = np.stack([(p >> (2 * i)) & 3 for i in range(4)], axis=-1).reshape(p.shape[0], -1).astype(np.int64)
+    cb = np.exp(1j * np.pi / 2 * k)
+    h = synth.channel(seed, 0, tx, tx)
+    rss = 10 * np.log10(1000 * (np.abs(cb @ h) * 1e-4) ** 2)
+    return np.abs(cb), np.angle(cb), rss
+
+
+def bench_driver(args, dev, rank, world):
+    """Wall-clock latency of one drop-in driver call, as main.py:427 makes it (host arrays in, host
+    arrays out: the 8 sweep points' row draws, uploads, pipelines and downloads).  The reference
+    states "2ACE solve time ... normally within a second" for 16 x 16 CSI (README.md:87, MATLAB on a
+    laptop): the only published timing of the path, a qualitative upper bound."""
+    from ace_amd import engine
+    if rank != 0:
+        return
+    tx = 16
+    amp, ang, rss = driver_trace(tx, 17)
+    eng = engine.start_matlab()
+
+    def call():
+        return eng.channel_recovery_ADMM_v2_simulation_A2only(tx, tx, engine.double(amp), engine.double(ang),
+                                                             engine.double(rss[:, None]),
+                                                             eng.double(DRIVER_SEED_ID), nargout=2)
+
+    for _ in range(max(1, args.warmup)):
+        call()
+    lat = {}
+    for mode in ("0", "1"):   # concurrent sweep points (default) and ACE_DRIVER_SERIAL=1
+        os.environ["ACE_DRIVER_SERIAL"] = mode
+        ts = []
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            Ha, _ = call()
+            ts.append(time.perf_counter() - t0)
+        lat[mode] = ts
+    os.environ.pop("ACE_DRIVER_SERIAL", None)
+    med = float(np.median(lat["0"]))
+    line = {
+        "metric": DRIVER_METRIC, "value": round(med, 4), "unit": "s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * med, 2), "higher_is_better": False, "scaling": "none",
+        "vs_baseline": round(med / 1.0, 4), "dtype": "f64",
+        "data": "reference probe codebook random_probe_cb_16x16.mat (3968 x 256), synthetic channel RSS",
+        "config": {"workload": "one ace_recover_driver call: M in round(linspace(2, 32, 8)).^2, 3-restart pipeline "
+                               "per point (M = 4 ill-posed, returned as 0)",
+                   "sweep_points": "concurrent host threads / HIP streams"},
+        "baseline": {"value": 1.0, "unit": "s", "source": "README.md:87 'normally within a second' (MATLAB, "
+                                                          "testbed laptop): a qualitative upper bound"},
+        "latency_s": {"concurrent_median": round(med, 4), "concurrent_all": [round(t, 4) for t in lat["0"]],
+                      "serial_median": round(float(np.median(lat["1"])), 4)},
+        "finite": bool(np.all(np.isfinite(Ha))),
+        "nonzero_points": int(sum(bool(Ha[i].max() > 0) for i in range(Ha.shape[0]))),
+        "roofline": None,
+        "roofline_note": "latency-bound (one realisation per sweep point); see the unit and pipeline lines",
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_driver(tx, amp, ang, rss)
+    print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_driver(tx, amp, ang, rss):
+    """The same driver call composed on the CPU: the driver's rows (engine.randperm, the build's RNG),
+    then the numpy oracle pipeline per sweep point (oracle/ace_oracle.py)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import ace_oracle as O
+    from ace_amd import engine
+    seed, fct = 36326041, 1e5 / 3      # seeds(3) of ..._A2only.m:103, rss_fct :132
+    cb = amp * np.exp(1j * ang)
     t0 = time.perf_counter()
-    if private:
-        U = np.stack([OC.make_U(a, nthreads=cores) for a in A])
-    else:
-        U = OC.make_U(A[0], nthreads=cores)[None]
-    t_setup = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    OC.infer_admm_r1_batch(A if private else A[:1], U, B, X0, tx, tx, variant=var, fixed_iters=True,
-                           maxiter=args.iters, nthreads=cores)
-    t_solve = time.perf_counter() - t0
-    if private:
-        t_total = t_solve + t_setup
-        setup_note = f"U=inv(A'A+I) per realisation {t_setup:.2f}s"
-    else:
-        t_total = t_solve + t_setup * n_samples / args.batch
-        setup_note = f"U=inv(A'A+I) setup {t_setup:.2f}s amortised over {args.batch}"
-    return {"value": n_samples / t_total, "unit": "recoveries/s", "cores": cores, "kind": "port",
-            "sample": (f"{n_samples} recoveries of the same workload ({args.iters} fixed iters, m={args.m}, "
-                       f"n={n}, {'private' if private else 'shared'} codebook) on {cores} threads of "
-                       f"{_cpu_model()}; {setup_note}; solve {t_solve:.2f}s")}
-
-
-PMC_KERNEL = {"zstep": "zstep1w_kernel<false>", "apply_A": "i8a_kernel", "apply_AH": "i8ah_kernel<false, true>",
-              "apply_G": "gyf_kernel"}
-
-
-PMC_KERNEL_PRIVATE = {"zstep": "zstep1w_kernel<false>", "apply_G": "pgk_kernel"}
-
-
-def _pmc_traffic(cls, private=False):
-    """HBM bytes per launch (PMC FETCH_SIZE, gfx950-corrected, + WRITE_SIZE) of a kernel class from
-    the newest committed profiles/*_pmc_hbm.json that has it (written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc passes of this benchmark; private-codebook profiles are named
-    *_private_pmc_hbm.json), or None."""
-    name = (PMC_KERNEL_PRIVATE if private else PMC_KERNEL).get(cls)
-    def version(f):   # r<round>_v<version>_pmc_hbm.json
-        parts = f.name.split("_")
-        try:
-            return int(parts[0][1:]), int(parts[1][1:])
-        except (IndexError, ValueError):
-            return -1, -1
-    files = sorted((f for f in (ROOT / "profiles").glob("r*_pmc_hbm.json") if ("_private_" in f.name) == private),
-                   key=version)
-    if not name:
-        return None
-    for f in reversed(files):
-        try:
-            d = json.loads(f.read_text())
-        except (OSError, ValueError):
+    for i, M in enumerate(engine.m_sweep(tx, tx)):
+        mt = math.floor(0.95 * M)
+        if mt < min(20, M):
             continue
-        for k, v in d.items():
-            if k.split(" grid=")[0].strip().startswith(name):
-                return round(v["hbm_bytes"]), f"profiles/{f.name}"
-    return None
+        idx = engine.randperm(seed, 0x100 + 2 * i, len(rss), int(M))
+        B = np.sqrt(10.0 ** (rss[idx] / 10.0) / 1000.0) * fct
+        tr = [engine.randperm(seed, 0x101 + 2 * i + 0x10000 * s, int(M), mt) for s in range(3)]
+        O.infer_low_rank_pipeline(cb[idx], B, tx, tx, tr)
+    dt = time.perf_counter() - t0
+    return {"value": round(dt, 3), "unit": "s", "cores": _blas_threads(), "kind": "port",
+            "sample": f"one full driver call (7 well-posed sweep points) through oracle/ace_oracle.py (numpy) on "
+                      f"{_cpu_model()}"}
 
 
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown CPU"
-
+# ------------------------------------------------------------------ main
 
 def main():
     args = parse()
@@ -429,285 +952,33 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    if args.mode in ("pipeline", "phaselift", "beamformer"):
-        {"pipeline": bench_pipeline, "phaselift": bench_phaselift,
-         "beamformer": bench_beamformer}[args.mode](args, dev, rank, world)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    line = unit_bench(args, args.private, dev, rank, world)
-    if not args.private and not args.no_regime_p and args.variant == "A2only":
-        # both codebook regimes, each against its own bound; the headline value is
-        # regime S (one codebook for the batch, as in Vs_M.m:192-194 and main.py's one cb_train per call)
-        lp = unit_bench(args, True, dev, rank, world)
+    if args.mode in ("pipeline", "phaselift", "beamformer", "driver"):
+        {"pipeline": bench_pipeline, "phaselift": bench_phaselift, "beamformer": bench_beamformer,
+         "driver": bench_driver}[args.mode](args, dev, rank, world)
+    elif args.mode == "config5":
+        line = unit_bench(args, False, dev, rank, world, config5_workload(args, rank, world, dev))
         if rank == 0:
-            line["regime_P"] = {k: lp[k] for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline",
-                                                   "kernels_ms", "checks")}
-            line["regime_P"]["codebook"] = lp["config"]["codebook"]
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+            print(json.dumps(line), flush=True)
+    else:
+        line = unit_bench(args, args.private, dev, rank, world)
+        if not args.private and args.variant == "A2only":
+            if not args.no_regime_p:
+                # both codebook regimes, each against its own bound; the headline value is
+                # regime S (one codebook for the batch, as in Vs_M.m:192-194 and main.py's one cb_train per call)
+                lp = unit_bench(args, True, dev, rank, world)
+                if rank == 0:
+                    line["regime_P"] = {k: lp[k] for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline",
+                                                           "kernels_ms", "checks")}
+                    line["regime_P"]["codebook"] = lp["config"]["codebook"]
+            if not args.no_refine_input and world == 1 and args.tx == 32:
+                ri = refine_input_bench(args, dev, rank, world)
+                if rank == 0:
+                    line["refine_input"] = ri
+        if rank == 0:
+            print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def unit_bench(args, private, dev, rank, world):
-    """One unit-metric measurement (regime S or P); returns the JSON line dict on rank 0."""
-    import torch
-    import torch.distributed as dist
-    import ace_amd
-    from ace_amd import infer_admm_batch, synth_problem
-    from ace_amd._lib import LIB, KERNEL_CLASSES, check
-    import ctypes as C
-
-    tx = args.tx
-    n, m, bsz = tx * tx, args.m, args.batch
-    A, B, X0, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, a_shared=not private, device=dev)
-    ws = ace_amd.solver.Workspace()
-    out = None
-    from ace_amd.dist import gather_to_root
-    counts = [bsz] * world
-
-    def step():
-        nonlocal out
-        out = infer_admm_batch(A, B, X0, tx, tx, variant=args.variant, maxiter=args.iters, fixed_iters=True,
-                               out=out, workspace=ws)
-        if world > 1:   # the single result gather of recovered channels over RCCL/xGMI (north_star)
-            gather_to_root(out.X, counts)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    prof = not args.no_prof
-    if prof:   # HIP event pairs on every PROF_STRIDE-th launch of each kernel class
-        check(LIB.ace_prof_sample(PROF_STRIDE, 0))
-        check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kt = (C.c_double * 10)()
-    kn = (C.c_int32 * 10)()
-    msp_steps = C.c_longlong(0)
-    if prof:
-        check(LIB.ace_prof_stop(kt, kn))
-        check(LIB.ace_prof_msp_steps(C.byref(msp_steps)))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    it_ok = bool((out.iters == args.iters).all().item())
-    finite = bool(torch.isfinite(torch.view_as_real(out.X)).all().item())
-
-    if rank == 0:
-        total = world * bsz * args.steps
-        value = total / elapsed
-        kernels = {}
-        roof = roof_gemm = None
-        if prof:
-            uf, ub = unit_flops(m, n, tx, tx), unit_bytes(m, n, tx, tx)
-            for i, name in enumerate(KERNEL_CLASSES):
-                if kn[i]:
-                    kernels[name] = {"launches": int(kn[i]), "avg_ms": kt[i] / kn[i], "total_ms": kt[i]}
-
-            # the int8 digit-plane applies run for a phase-code codebook in the A2only r = 1 iteration
-            i8 = (not private) and os.environ.get("ACE_NO_I8") != "1"
-            io = unit_i8_ops(m, n)
-            # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
-            # every launch of an iteration kernel covers bsz / nsplit realisations
-            nsplit = 1
-            if i8 and m <= 256:
-                nsplit = max(1, min(4, int(os.environ.get("ACE_SPLIT", "2"))))
-                while nsplit > 1 and bsz // nsplit < 256:
-                    nsplit -= 1
-            per_launch = -(-bsz // nsplit)
-
-            gyk = i8 and m <= 256   # apply_G is the fused gyk_kernel (ace_i8gemm.hip)
-            # with concurrent sub-batches apply_G is gyf_kernel: gyk and the fused apply_AH in one launch
-            env_on = lambda k: os.environ.get(k) != "0"
-            # (and with m-space steps, ACE_MSPACE, on one batch too, A2only)
-            msp_on = env_on("ACE_MSPACE") and args.variant == "A2only"
-            gyf = gyk and (nsplit > 1 or msp_on) and all(env_on(k) for k in ("ACE_GYF", "ACE_FUSE", "ACE_LAZY_DUAL",
-                                                                             "ACE_LEAN"))
-            # share of the realisation-iterations gyf_kernel settled in m-space form (no apply_AH
-            # pass, no Z traffic: ace_prof_msp_steps); the per-launch work below is averaged with it
-            msp_frac = msp_steps.value / float(args.steps * bsz * args.iters) if msp_on else 0.0
-            # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
-            pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
-
-            def roofline(k):
-                avg_s = kernels[k]["avg_ms"] * 1e-3
-                if k == "apply_G" and pc:
-                    b, po = private_bytes(m, n) * per_launch, private_ops(m, n)
-                    o, f = po["int8"] * per_launch, po["f64"] * per_launch
-                    return {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                            "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
-                            "kernel": k, "bytes_per_launch": b,
-                            "other_resources": {
-                                "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
-                                         "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
-                                         "ops_per_launch": o},
-                                "f64": {"bound": "valu", "achieved": round(f / avg_s / 1e12, 3),
-                                        "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                                        "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4), "flops_per_launch": f}},
-                            "bytes_note": "per realisation: G_b lower triangle (c128) + A_b^H as 2-bit codes + "
-                                          "Y, M, AX, B in and AX, M, Y out + W = A^H g out (bench.private_bytes)"}
-                if k == "apply_G" and gyf:   # f64 G T, int8 A^H g, HBM (T, Y-step, Z pass), phase after phase
-                    f = uf[k] * per_launch
-                    o = io["apply_AH"] * per_launch * (1.0 - msp_frac)
-                    b = (msp_frac * msp_bytes(m) + (1.0 - msp_frac) * gyf_bytes(m, n)) * per_launch
-                    tf, to, tb = f / (PEAK_FP64_TFLOPS * 1e12), o / (PEAK_I8_TOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
-                    res = {
-                        "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
-                                "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
-                                "flops_per_launch": f},
-                        "int8": {"bound": "mfma", "achieved": round(o / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
-                                 "unit": "TOP/s", "frac": round(o / avg_s / 1e12 / PEAK_I8_TOPS, 4),
-                                 "ops_per_launch": o},
-                        "hbm": {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
-                    }
-                    main = max((("f64", tf), ("int8", to), ("hbm", tb)), key=lambda x: x[1])[0]
-                    out = dict(res[main])
-                    out.update({"traffic": None, "kernel": "apply_G (gyf_kernel)", "resource": main,
-                                "other_resources": {r: v for r, v in res.items() if r != main},
-                                "serial_frac": round((tf + to + tb) / avg_s, 4),
-                                "msp_frac": round(msp_frac, 4),
-                                "flop_note": "gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per "
-                                             "complex MAC), the Y-step, then W = A^H g (int8 digit planes) with the "
-                                             "certified Z-step pass (Z in, Z' out) in its epilogue, one phase after "
-                                             "another in each work-group; a realisation in m-space form (msp_frac of "
-                                             "the realisation-iterations) skips the int8 pass and the Z traffic and "
-                                             "moves S in / S' out instead (bench.msp_bytes); int8 ops and bytes are "
-                                             "averaged with msp_frac; bound = the resource with the largest time "
-                                             "at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time"})
-                    return out
-                if k == "apply_G" and gyk:   # f64 G T + the Y-step's HBM traffic, phase after phase
-                    f, b = uf[k] * per_launch, ub[k] * per_launch
-                    tf, tb = f / (PEAK_FP64_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)
-                    res = {
-                        "f64": {"bound": "mfma", "achieved": round(f / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
-                                "unit": "TFLOP/s", "frac": round(f / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
-                                "flops_per_launch": f},
-                        "hbm": {"bound": "hbm", "achieved": round(b / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": round(b / avg_s / 1e9 / PEAK_HBM_GBS, 4), "bytes_per_launch": b},
-                    }
-                    main = "f64" if tf >= tb else "hbm"   # the resource that needs the most time at its peak
-                    out = dict(res[main])
-                    out.update({"traffic": None, "kernel": k, "resource": main,
-                                "other_resources": {r: v for r, v in res.items() if r != main},
-                                "serial_frac": round((tf + tb) / avg_s, 4),
-                                "flop_note": "gyk_kernel runs g = G T (f64 3M; achieved counts 8 flops per complex "
-                                             "MAC) and the Y-step (HBM) one after the other in each work-group; "
-                                             "bound = the resource with the largest time at peak; "
-                                             "serial_frac = (t_f64 + t_hbm at peak) / launch time"})
-                    return out
-                if k in io and i8:   # exact int8 digit planes on the matrix cores (+ apply_AH: the fused Z-step pass)
-                    per, pb = io[k] * per_launch, ub[k] * per_launch
-                    to, tb = per / (PEAK_I8_TOPS * 1e12), pb / (PEAK_HBM_GBS * 1e9)
-                    res = {
-                        "int8": {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 1), "peak": PEAK_I8_TOPS,
-                                 "unit": "TOP/s", "frac": round(per / avg_s / 1e12 / PEAK_I8_TOPS, 4),
-                                 "ops_per_launch": per},
-                        "hbm": {"bound": "hbm", "achieved": round(pb / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": round(pb / avg_s / 1e9 / PEAK_HBM_GBS, 4),
-                                "bytes_per_launch": pb},
-                    }
-                    main = "int8" if to >= tb else "hbm"
-                    out = dict(res[main])
-                    out.update({"traffic": None, "kernel": k, "resource": main,
-                                "other_resources": {r: v for r, v in res.items() if r != main},
-                                "serial_frac": round((to + tb) / avg_s, 4),
-                                "f64_equiv_tflops": round(uf[k] * per_launch / avg_s / 1e12, 1),
-                                "op_note": "int8 x int8 -> int32 ops of the 8 digit planes x the 2x2 real expansion "
-                                           "(exact: the codebook is a phase code); f64_equiv_tflops counts the same "
-                                           "product as 8 flops per complex MAC; apply_AH also streams Z in and Z' out "
-                                           "(the steady-state Z-step pass fused into its epilogue)"})
-                    return out
-                if k in uf:   # MFMA-bound complex f64 GEMM
-                    per = uf[k] * per_launch
-                    # algorithmic = conventional 8 flops per complex MAC; the 3M kernel executes 6
-                    return {"bound": "mfma", "achieved": round(per / avg_s / 1e12, 3), "peak": PEAK_FP64_TFLOPS,
-                            "unit": "TFLOP/s", "frac": round(per / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
-                            "traffic": None, "kernel": k, "flops_per_launch": per,
-                            "executed_frac": round(0.75 * per / avg_s / 1e12 / PEAK_FP64_TFLOPS, 4),
-                            "flop_note": "achieved counts 8 real flops per complex MAC; the 3M (Gauss) kernel "
-                                         "executes 6, so the matrix cores run at executed_frac of peak"}
-                per = ub[k] * per_launch
-                return {"bound": "hbm", "achieved": round(per / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                        "unit": "GB/s", "frac": round(per / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
-                        "kernel": k, "bytes_per_launch": per}
-
-            timed = [k for k in kernels if k in uf or k in ub]
-            if pc:   # pgk_kernel and the Z-step are the only iteration launches
-                timed = [k for k in kernels if k in ("apply_G", "zstep")]
-            # every timed class launches once per iteration: dominant = largest average launch
-            dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
-            roof = roofline(dom)
-            roof["realisations_per_launch"] = per_launch
-            # the nsplit sub-batch launches of a class run at the same time on disjoint CUs (rocprofv3
-            # kernel trace, tools/timeline.py): the chip-level rate is nsplit x the per-launch rate
-            roof["concurrent_launches"] = nsplit
-            roof["chip_frac"] = round(roof["frac"] * nsplit, 4)
-            roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
-                            f"region, on every {PROF_STRIDE}th launch of each kernel class); peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); "
-                            "traffic: PMC FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source")
-            tr = _pmc_traffic(dom, private=pc)
-            if tr:
-                roof["traffic"], roof["traffic_source"] = tr
-            if not pc:
-                gemm = max((k for k in kernels if k in uf), key=lambda k: kernels[k]["avg_ms"])
-                roof_gemm = roofline(gemm)
-                roof_gemm["concurrent_launches"] = nsplit
-                roof_gemm["chip_frac"] = round(roof_gemm["frac"] * nsplit, 4)
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            ns = args.cpu_recoveries or (32 if private else 256)
-            cpu = cpu_baseline(args, ns, private)
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "recoveries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (Generate_Channel/Random_Phase_State/Generate_Measurement semantics, 30 dB SNR)",
-            "config": {
-                "workload": ("config 2: 32-ant URA (n=1024), 256 random-codebook RSS meas, A2only ADMM "
-                             "refinement solve (r=1), 200 fixed iterations" if args.variant == "A2only" and tx == 32
-                             else f"{args.variant}, tx=rx={tx}, m={m}, {args.iters} fixed iterations"),
-                "variant": args.variant,
-                "codebook": "private per realisation (regime P)" if private else "shared (regime S)",
-                "batch_per_gpu": bsz,
-                "global_batch": world * bsz,
-                "m": m, "n": n, "iters": args.iters,
-                "parallelism": f"dp{world} (realisation sharding, RCCL gather of X to rank 0)",
-            },
-            "roofline": roof,
-            "roofline_gemm": roof_gemm if prof else None,
-            "cpu_baseline": cpu,
-            "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
-            "checks": {"all_iters_ran": it_ok, "finite": finite},
-        }
-        return line
-    return None
-
 
 
 if __name__ == "__main__":

@@ -135,7 +135,10 @@ typedef struct ace_pipeline_cfg {
     int r;             /* 20 (:7); clipped to min(r, m, n) (:19), must be <= 32 */
     int maxiter;       /* 500 (:13), every stage */
     int eig_warm;      /* warm-start the Z-prox eigensolver inside each stage */
-    int reserved[3];
+    int stop_before_refine; /* 0 (reference); 1: return X_max, the refinement's input (:90-92), rescaled
+                          (:106-107), with Y_max on the train rows and no refinement stage (its
+                          stage_iters column is 0) -- for measuring the unit on the reference's input */
+    int reserved[2];
     double mu0;        /* 1e-3 */
     double rho;        /* 1.03 */
     double cc_frac;    /* 0.95 (:10) */
@@ -284,6 +287,11 @@ int ace_prof_stop(double* total_ms, int32_t* launches);
  * settled in m-space form (RealState::msp: no apply_AH pass, no Z traffic), for the bench's
  * per-launch work accounting. */
 int ace_prof_msp_steps(long long* steps);
+/* Algorithmic flops (8 per complex multiply-add) of the launches the last ace_prof_start /
+ * ace_prof_stop pair recorded, per kernel class: the GEMM-shaped applies and prox steps of the
+ * f64 path (pipeline stages, PhaseLift) carry their count; classes the caller accounts for
+ * itself (the unit path's fused kernels) report 0.  flops: [ACE_NKCLASS]. */
+int ace_prof_work(double* flops);
 
 /* InferADMM solves (unit solves and every pipeline stage) per apply path since the last reset,
  * process-wide: counts[0] shared phase-code codebook on the exact int8 digit-plane applies,

@@ -63,3 +63,37 @@ def test_metric_is_baselines():
     b = _bench()
     base = json.loads((ROOT / "BASELINE.json").read_text())
     assert b.METRIC == base["metric"]
+
+
+def test_nuclear_bytes():
+    b = _bench()
+    m, n = 256, 1024
+    nb = b.nuclear_bytes(m, n)
+    # gyk: Y, M, AX, B in, g, AX, M, Y out, plus Z and N for the digit planes of V = Z - N/mu
+    assert nb["apply_G"] == 16 * 7 * m + 8 * m + 32 * n
+    assert nb["apply_AH"] == 16 * (m + n)          # g in, W out
+    assert nb["zstep"] == 16 * 5 * n               # W, Z, N in; Z', N' out
+    r = b.unit_resources("apply_G", m, n, variant="A2nuclear", pc=False, gyf=False, gyk=True, i8=True, msp_frac=0.0)
+    assert r == {"f64": 8 * m * m, "int8": 2 * 8 * 2 * m * 2 * n, "hbm": nb["apply_G"]}
+
+
+def test_roofline_picks_bound_and_serial_frac():
+    b = _bench()
+    r = b.roofline_from("k", 1e-4, {"f64": 78.6e12 * 2e-5, "hbm": 8e12 * 5e-5})
+    assert r["resource"] == "hbm" and abs(r["frac"] - 0.5) < 1e-9
+    assert abs(r["serial_frac"] - 0.7) < 1e-9 and r["other_resources"]["f64"]["frac"] == 0.2
+
+
+def test_pmc_traffic_is_keyed_by_workload(tmp_path, monkeypatch):
+    import json
+    b = _bench()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r02_v9_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 1.0}}))
+    (prof / "r03_v1_nuclear_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 2.0}}))
+    (prof / "r03_v2_config5_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 3.0}}))
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    assert b._pmc_traffic("gyk_kernel", "unit") == (1, "profiles/r02_v9_pmc_hbm.json")
+    assert b._pmc_traffic("gyk_kernel", "nuclear") == (2, "profiles/r03_v1_nuclear_pmc_hbm.json")
+    assert b._pmc_traffic("gyk_kernel", "config5") == (3, "profiles/r03_v2_config5_pmc_hbm.json")
+    assert b._pmc_traffic("gyk_kernel", "private") is None

@@ -65,3 +65,48 @@ def test_gather_two_ranks_gloo(total):
     from ace_amd import synth
     _, _, _, H = synth.problem(4242, 0, total, 16, 4, 4)
     np.testing.assert_array_equal(got, H)   # same realisations, same order, bit-identical
+
+
+def _config5_worker(rank, world, port, total, out_q):
+    """configs[4]'s sharding: every rank draws the same multiresolution rows (same seed), builds its
+    contiguous shard of realisations on that shared codebook, and rank 0 gathers the per-realisation
+    results (here the measurement vectors, standing in for the recovered X)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ace_amd import synth
+        rows, tier = synth.multires_rows(58659179, 32, 256)
+        A = synth.multires_codebook(58659179, 32, rows)
+        digest = torch.tensor([float(np.sum(np.abs(A) * np.arange(A.size).reshape(A.shape)))], dtype=torch.float64)
+        digests = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(digests, digest)
+        assert all(d.item() == digest.item() for d in digests)
+        counts = [shard_range(total, world, r)[1] for r in range(world)]
+        first, count = shard_range(total, world, rank)
+        B = np.stack([synth.measurements(7, first + c, A, synth.channel(7, first + c, 32, 32)) for c in range(count)])
+        full = gather_to_root(torch.from_numpy(B), counts)
+        if rank == 0:
+            out_q.put((tier, full.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_sharding_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    total = 5
+    procs = [ctx.Process(target=_config5_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    tier, got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from ace_amd import synth
+    rows, t = synth.multires_rows(58659179, 32, 256)
+    assert tier == t == 0                       # M = 256 <= 384: the 4-antenna-group tier
+    A = synth.multires_codebook(58659179, 32, rows)
+    ref = np.stack([synth.measurements(7, c, A, synth.channel(7, c, 32, 32)) for c in range(total)])
+    np.testing.assert_array_equal(got, ref)

@@ -47,7 +47,7 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->pcflag = pc ? cv.take<int>(sizeof(int)) : nullptr;
     L->pc_ok = false;
     L->batch = batch;
-    L->ns = shared ? cv.take(cz * 4 * m * m) : nullptr;
+    L->ns = shared ? cv.take(cz * 4 * m * m + 2 * sizeof(double)) : nullptr;
     L->LA8 = shared ? cv.take<int8_t>(i8_frag_bytes(m, n)) : nullptr;
     L->LAH8 = shared ? cv.take<int8_t>(i8_frag_bytes(n, m)) : nullptr;
     L->LK8 = shared ? cv.take<int8_t>(i8k_frag_bytes(m)) : nullptr;
@@ -126,17 +126,15 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     launch_i8_expand(m, n, L.A, L.c8, L.LA8, L.LAH8, L.i8flag, st);
     int flag = 1;
     double c[2] = {0.0, 0.0};
-    ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipMemcpyAsync(c, L.c8, sizeof(double), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipStreamSynchronize(st));
+    ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
+    ACE_HIP(read_back(c, L.c8, sizeof(double), st));
     L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= 160 * 1024 - 8192;
     if (!L.i8ok) return ACE_OK;
     c[1] = c[0] * c[0];
-    ACE_HIP(hipMemcpyAsync(L.c8 + 1, c + 1, sizeof(double), hipMemcpyHostToDevice, st));
+    ACE_HIP(upload(L.c8 + 1, c + 1, sizeof(double), st));
     ACE_HIP(hipMemsetAsync(L.LK8, 0, i8k_frag_bytes(m), st));
     launch_i8k_expand(m, L.K, L.c8, L.LK8, L.i8flag, st);
-    ACE_HIP(hipMemcpyAsync(&flag, L.i8flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipStreamSynchronize(st));
+    ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     L.i8ok = flag == 0;
     L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= (size_t)GYK_MAXDYN;
     if (L.gyk_ok) launch_gyk_gfrag(m, L.G, L.Gf, st);
@@ -163,16 +161,14 @@ int ns_inverse(LinOps& L, hipStream_t st) {
     double* R = L.ns + 4 * mm;
     double* Xn = L.ns + 6 * mm;
     double* X = L.G;
-    double* flag = nullptr;
-    ACE_HIP(hipMallocAsync((void**)&flag, 2 * sizeof(double), st));
+    double* flag = L.ns + 8 * mm;   // [0] max|R|, [1] Gershgorin bound (workspace, not a stream-ordered allocation)
     launch_ns_prep(m, L.K, Ap, Id, X, st, flag + 1);
     // The spectrum of I + K lies in [1, b], so ||R_0|| <= rho = (b - 1) / (b + 1) and
     // ||R_k|| <= rho^(2^k): the iteration count that brings max|R_k| below 1e-10 is known from b
     // (one host read instead of a read after every iteration); one more step, as below, and a
     // final check (the polling loop takes over if rounding kept it above the bound).
     double b = 0.0;
-    ACE_HIP(hipMemcpyAsync(&b, flag + 1, sizeof(double), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipStreamSynchronize(st));
+    ACE_HIP(read_back(&b, flag + 1, sizeof(double), st));
     int kpred = 60;
     if (std::isfinite(b) && b >= 1.0) {
         const double rho = (b - 1.0) / (b + 1.0);
@@ -193,23 +189,20 @@ int ns_inverse(LinOps& L, hipStream_t st) {
     {   // check R of the last step (it is the residual of the iterate before it: converged one step earlier)
         double h = 0.0;
         launch_max_abs(2 * mm, R, flag, st);
-        ACE_HIP(hipMemcpyAsync(&h, flag, sizeof(double), hipMemcpyDeviceToHost, st));
-        ACE_HIP(hipStreamSynchronize(st));
+        ACE_HIP(read_back(&h, flag, sizeof(double), st));
         done = h < 1e-10;
     }
     for (; it < 60 && !done;) {   // (rounding kept the residual above the bound: poll as before)
         launch_zgemm(1, true, m, m, m, Ap, m, 0, X, m, 0, R, Id, m, 0, 1, st);
         double h = 0.0;
         launch_max_abs(2 * mm, R, flag, st);
-        ACE_HIP(hipMemcpyAsync(&h, flag, sizeof(double), hipMemcpyDeviceToHost, st));
-        ACE_HIP(hipStreamSynchronize(st));
+        ACE_HIP(read_back(&h, flag, sizeof(double), st));
         done = h < 1e-10;
         launch_zgemm(2, true, m, m, m, R, m, 0, X, m, 0, Xn, X, m, 0, 1, st);
         launch_hermitize(m, Xn, st);
         std::swap(X, Xn);
         ++it;
     }
-    ACE_HIP(hipFreeAsync(flag, st));
 #ifdef ACE_DEBUG_SPEC
     fprintf(stderr, "ns_inverse m %d b %g kpred %d it %d done %d\n", m, b, kpred, it, (int)done);
 #endif
@@ -231,8 +224,7 @@ static int pc_setup(LinOps& L, int batch, hipStream_t st) {
     ACE_HIP(hipMemsetAsync(L.pcflag, 0, sizeof(int), st));
     launch_pc_pack(batch, m, n, L.A, L.pcb, L.pcodes, L.pcflag, st);
     int flag = 1;
-    ACE_HIP(hipMemcpyAsync(&flag, L.pcflag, sizeof(int), hipMemcpyDeviceToHost, st));
-    ACE_HIP(hipStreamSynchronize(st));
+    ACE_HIP(read_back(&flag, L.pcflag, sizeof(int), st));
     if (flag != 0) return ACE_OK;
     launch_pc_ginv(batch, m, n, L.pcodes, L.pcb, L.K, L.G, st);
     ACE_HIP(hipGetLastError());
@@ -520,8 +512,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 ACE_HIP(hipStreamWaitEvent(st, cev[h], 0));
             }
             int h_done = 0;
-            ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
-            ACE_HIP(hipStreamSynchronize(st));
+            ACE_HIP(read_back(&h_done, w.done, sizeof(int), st));
             if (h_done >= batch) break;
         }
     }
@@ -727,8 +718,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         }
         if (!p.fixed_iters && (it % poll == 0) && it < p.maxiter) {
             int h_done = 0;
-            ACE_HIP(hipMemcpyAsync(&h_done, w.done, sizeof(int), hipMemcpyDeviceToHost, st));
-            ACE_HIP(hipStreamSynchronize(st));
+            ACE_HIP(read_back(&h_done, w.done, sizeof(int), st));
             if (h_done >= batch) break;
         }
     }

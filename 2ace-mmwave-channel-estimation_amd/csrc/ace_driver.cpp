@@ -174,12 +174,11 @@ int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const d
         ACE_HIP(d.alloc(nB, &dB));
         ACE_HIP(d.alloc(nX, &dX));
         ACE_HIP(d.alloc(ws, &dW));
-        ACE_HIP(hipMemcpyAsync(dA, A.data(), nA, hipMemcpyHostToDevice, d.st));
-        ACE_HIP(hipMemcpyAsync(dB, B.data(), nB, hipMemcpyHostToDevice, d.st));
+        ACE_HIP(upload(dA, A.data(), nA, d.st));
+        ACE_HIP(upload(dB, B.data(), nB, d.st));
         ACE_TRY(ace_phaselift_solve_batch(&pcfg, 1, M, n, (const double*)dA, (const double*)dB, (double*)dX, nullptr,
                                           nullptr, dW, ws, d.st));
-        ACE_HIP(hipMemcpyAsync(X.data(), dX, nX, hipMemcpyDeviceToHost, d.st));
-        ACE_HIP(hipStreamSynchronize(d.st));
+        ACE_HIP(read_back(X.data(), dX, nX, d.st));
         for (int k = 0; k < 2 * n; ++k) X[k] = X[k] / std::sqrt(1e10) * 2e5;
     } else {
         // ---- Recover_Channel -> ADMM_v2(..., 4): the pipeline with its own train partitions
@@ -194,12 +193,11 @@ int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const d
         ACE_HIP(d.alloc(nX, &dX));
         ACE_HIP(d.alloc(nY, &dY));
         ACE_HIP(d.alloc(ws, &dW));
-        ACE_HIP(hipMemcpyAsync(dA, A.data(), nA, hipMemcpyHostToDevice, d.st));
-        ACE_HIP(hipMemcpyAsync(dB, B.data(), nB, hipMemcpyHostToDevice, d.st));
+        ACE_HIP(upload(dA, A.data(), nA, d.st));
+        ACE_HIP(upload(dB, B.data(), nB, d.st));
         ACE_TRY(ace_pipeline_solve_batch(&cfg, 1, M, n, tx, rx, (const double*)dA, (const double*)dB, tr.data(),
                                          (double*)dX, (double*)dY, nullptr, nullptr, nullptr, dW, ws, d.st));
-        ACE_HIP(hipMemcpyAsync(X.data(), dX, nX, hipMemcpyDeviceToHost, d.st));
-        ACE_HIP(hipStreamSynchronize(d.st));
+        ACE_HIP(read_back(X.data(), dX, nX, d.st));
     }
     // ---- :170-178 H_out = X / rss_fct, NaN -> 0, amplitude and angle
     for (int k = 0; k < n; ++k) {

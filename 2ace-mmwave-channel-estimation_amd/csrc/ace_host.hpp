@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <atomic>
 #include <string>
 #include <vector>
@@ -62,6 +63,44 @@ inline Prof g_prof;
 // solves per apply path since the last reset (ace_path_counts): 0 shared phase code (int8 digit
 // planes), 1 private phase codes (2-bit code images), 2 f64 shared A, 3 f64 private A
 inline std::atomic<long long> g_path[4];
+
+// Host <-> device copies of host (pageable) buffers ordered on `st` for any stream kind: through a
+// per-thread pinned staging buffer, the device -> host direction followed by a stream
+// synchronisation.  (Pageable-memory hipMemcpyAsync on a non-blocking stream was measured returning
+// values the stream's earlier kernels had not written yet: the driver's concurrent sweep points.)
+struct Pinned {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = bytes < 4096 ? 4096 : bytes;
+        const hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+inline thread_local Pinned g_stage;
+inline hipError_t read_back(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    hipError_t e = g_stage.reserve(bytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(g_stage.p, src, bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) memcpy(dst, g_stage.p, bytes);
+    return e;
+}
+inline hipError_t upload(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    hipError_t e = g_stage.reserve(bytes);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);   // (the staging buffer may still be in use)
+    if (e == hipSuccess) memcpy(g_stage.p, src, bytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, g_stage.p, bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+}
 
 // ACE_POISON=1 (debugging): fill a solve's workspace with 0xFF bytes (NaN doubles, -1 ints) before
 // it is carved, so that a read of memory the solve did not write shows up in its results
@@ -136,7 +175,8 @@ struct LinOps {
     double* AH;
     double* K;
     double* G;
-    double* ns;  // shared regime: Newton-Schulz scratch (4 m x m: I + K, I, R, X'), else null
+    double* ns;  // shared regime: Newton-Schulz scratch (4 m x m: I + K, I, R, X', then 2 doubles:
+                 // max|R| and the Gershgorin bound), else null
     // shared regime, phase-code A (every real component in {0, +-c}): the int8 fragment images of
     // A and A^H for the exact digit-plane applies (ace_i8gemm.hip); i8ok is set by linops_setup
     int8_t* LA8;

@@ -131,8 +131,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             launch_zgemm(0, true, m, n, m, Phi, n, 0, Phi, n, 0, w.K, nullptr, m, 0, 1, st);   // K = Phi Phi^H
             launch_chol(m, w.K, w.R, w.ok, st);
             int ok = 0;
-            ACE_HIP(hipMemcpyAsync(&ok, w.ok, sizeof(int), hipMemcpyDeviceToHost, st));
-            ACE_HIP(hipStreamSynchronize(st));
+            ACE_HIP(read_back(&ok, w.ok, sizeof(int), st));
             if (!ok) return fail(ACE_ERR_UNSUPPORTED, "measurement matrix rows are linearly dependent (Phi Phi^H "
                                  "not positive definite); the reduced PhaseLift needs rank(Phi) = m <= n");
             a.R = w.R;
@@ -160,8 +159,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
         for (;;) {  // tfocs_AT.m inner (backtracking) loop, for the realisations still in it
             ACE_HIP(hipMemsetAsync(a.cnt, 0, 8 * sizeof(int), st));
             launch_pl_theta(a, st);
-            ACE_HIP(hipMemcpyAsync(h, a.cnt, sizeof h, hipMemcpyDeviceToHost, st));
-            ACE_HIP(hipStreamSynchronize(st));
+            ACE_HIP(read_back(h, a.cnt, sizeof h, st));
             if (h[0] == 0) break;
             {
                 ProfScope ps(ACE_K_PRE, st);
@@ -194,8 +192,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             {
                 ProfScope ps(ACE_K_YSTEP, st);
                 launch_pl_make_x(a, st);
-                ACE_HIP(hipMemcpyAsync(&h[2], a.cnt + 2, sizeof(int), hipMemcpyDeviceToHost, st));
-                ACE_HIP(hipStreamSynchronize(st));
+                ACE_HIP(read_back(&h[2], a.cnt + 2, sizeof(int), st));
                 if (h[2]) {
                     applyA(a.x, a.Aex);
                     launch_pl_set_Ax(a, st);
@@ -206,8 +203,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
         }
         launch_pl_iterate(a, st);   // tfocs_iterate.m: stopping tests, restart
         int ndone = 0;
-        ACE_HIP(hipMemcpyAsync(&ndone, a.cnt + 8, sizeof(int), hipMemcpyDeviceToHost, st));
-        ACE_HIP(hipStreamSynchronize(st));
+        ACE_HIP(read_back(&ndone, a.cnt + 8, sizeof(int), st));
         if (ndone >= batch) break;
     }
     // ---- MyPhaseLift.m:106-107: leading eigenvector of X, scaled by sqrt of its eigenvalue

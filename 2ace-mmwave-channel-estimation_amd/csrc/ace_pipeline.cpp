@@ -220,7 +220,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     std::vector<int> iota(m);
     for (int i = 0; i < m; ++i) iota[i] = i;
     launch_anorm(m, n, A, cfg->tol_abs, w.anorm, st);
-    ACE_HIP(hipMemcpyAsync(w.idx_rows, iota.data(), 4 * (size_t)m, hipMemcpyHostToDevice, st));
+    ACE_HIP(upload(w.idx_rows, iota.data(), 4 * (size_t)m, st));
     launch_gather_rows(m, n, A, w.idx_rows, w.anorm, w.An, st);
     launch_bnorm(m, batch, B, cfg->tol_abs, w.bnorm, w.Bn, st);
     launch_fill(batch, -1.0, w.qmax, st);                                 // max_quality = -1 (:40)
@@ -234,7 +234,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         // ---- :47-53 partition
         std::vector<int> rows(tr[i]);
         rows.insert(rows.end(), te[i].begin(), te[i].end());
-        ACE_HIP(hipMemcpyAsync(w.idx_rows, rows.data(), 4 * (size_t)m, hipMemcpyHostToDevice, st));
+        ACE_HIP(upload(w.idx_rows, rows.data(), 4 * (size_t)m, st));
         launch_gather_rows(d.mt, n, A, w.idx_rows, w.anorm, w.At, st);
         launch_gather_rows(d.mte, n, A, w.idx_rows + d.mt, w.anorm, w.Ate, st);
         launch_gather_b(m, d.mt, batch, w.Bn, w.idx_rows, w.Bt, st);
@@ -256,17 +256,16 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         ACE_TRY(run_impl(d, w, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
         launch_quality(n, d.mte, batch, w.Ate, w.X2, w.Bte, w.q, st);
         // ---- :73-77 rank-one retry on the realisations with quality < 0.6
-        ACE_HIP(hipMemcpyAsync(hq.data(), w.q, 8 * (size_t)batch, hipMemcpyDeviceToHost, st));
-        ACE_HIP(hipStreamSynchronize(st));
+        ACE_HIP(read_back(hq.data(), w.q, 8 * (size_t)batch, st));
         fails.clear();
         for (int b = 0; b < batch; ++b) {
             ro[b] = hq[b] < 0.6;
             if (ro[b]) fails.push_back(b);
         }
-        ACE_HIP(hipMemcpyAsync(w.rank_one, ro.data(), batch, hipMemcpyHostToDevice, st));
+        ACE_HIP(upload(w.rank_one, ro.data(), batch, st));
         const int nf = (int)fails.size();
         if (nf > 0) {
-            ACE_HIP(hipMemcpyAsync(w.idx_sub, fails.data(), 4 * (size_t)nf, hipMemcpyHostToDevice, st));
+            ACE_HIP(upload(w.idx_sub, fails.data(), 4 * (size_t)nf, st));
             launch_move_rows(nf, 2LL * d.r * n, w.Xs, w.Xs_s, w.idx_sub, false, st);
             launch_move_rows(nf, d.mt, w.Bt, w.Bt_s, w.idx_sub, false, st);
             launch_move_rows(nf, std::max(d.mte, 1), w.Bte, w.Bte_s, w.idx_sub, false, st);

@@ -6,9 +6,12 @@ sub-batch path bench.py --mode config5 runs.
 
 The rows are phase codes, so the solve runs the exact int8 applies (ace_amd.path_counts).  Parity:
 a sample against the C oracle (U = inv(A'A + I), inferLowRank_Nuclear.m:411-419 soft threshold) on
-the horizon where the oracle is stable against itself (60 iterations, see test_gpu_parity.py), and
-every sampled realisation of the 200-iteration benchmark horizon bit-identical to its result in a
-small batch."""
+the horizon where the oracle is stable against itself, and every sampled realisation of the
+200-iteration benchmark horizon bit-identical to its result in a small batch.  The tier-0 rows span
+only 64 dimensions (8 tx x 8 rx antenna groups), and the nuclear refinement on them is
+rounding-chaotic sooner than on the random codebook: the C oracle against ITSELF with B scaled by
+1 + 1e-15 moves 4.6e-11 at 20 iterations, 3.2e-10 at 30, 1.4e-6 at 40 and 5.3e-5 at 60 (random
+codebook: 4.7e-10 at 60), so parity is asserted at 30 iterations."""
 import numpy as np
 import pytest
 
@@ -38,15 +41,15 @@ def test_config5_unit_vs_oracle(gpu):
     A, B, X0, tier = _workload(2048)
     assert tier == 0
     path_counts(reset=True)
-    r = infer_admm_batch(A, B, X0, 32, 32, variant="A2nuclear", maxiter=60, fixed_iters=True)
+    r = infer_admm_batch(A, B, X0, 32, 32, variant="A2nuclear", maxiter=30, fixed_iters=True)
     torch.cuda.synchronize()
     assert path_counts(reset=True)["int8_shared"] == 1
     idx = [0, 777, 1024, 2047]
     Ah = A.cpu().numpy()
     U = OC.make_U(Ah[0])[None]
     Xo, _, ito, _, _ = OC.infer_admm_r1_batch(Ah, U, B.cpu().numpy()[idx], X0.cpu().numpy()[idx], 32, 32, variant=1,
-                                              maxiter=60, fixed_iters=True)
-    assert (ito == 60).all()
+                                              maxiter=30, fixed_iters=True)
+    assert (ito == 30).all()
     assert _errs(r.X.cpu().numpy()[idx], Xo).max() <= 1e-8
 
 

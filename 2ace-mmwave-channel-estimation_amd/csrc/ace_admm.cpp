@@ -54,6 +54,8 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
     L->c8 = shared ? cv.take(2 * sizeof(double)) : nullptr;
     L->i8flag = shared ? cv.take<int>(sizeof(int)) : nullptr;
     L->Gf = shared && m <= GYK_MAXM ? cv.take(gyk_gfrag_bytes(m)) : nullptr;
+    L->Kfr = shared && m <= GYK_MAXM ? cv.take(gyk_gfrag_bytes(m)) : nullptr;
+    L->frag_ok = false;
     L->i8ok = false;
     L->gyk_ok = false;
     L->allow_i8 = true;
@@ -75,9 +77,11 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //                       so the Z-step materialises Z, Z' and opt_X from the implicit form
 //   ACE_LAZY_DUAL=0     K Y in gyk_kernel every iteration
 //   ACE_LEAN=0          the full one-wave Z-step every iteration (no zlean / certified pass)
+//   ACE_NUC_MSP=0       A2nuclear r = 1 in n-space (gyk / apply_AH / Z-step) instead of the m-space
+//                       iteration of ace_nucmsp.hip
 struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1;
-    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true;
+    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true;
     double msp_room = 32.0;
 };
 static Knobs read_knobs() {
@@ -100,6 +104,7 @@ static Knobs read_knobs() {
     k.mspace = on("ACE_MSPACE");
     k.lazy_dual = on("ACE_LAZY_DUAL");
     k.lean = on("ACE_LEAN");
+    k.nuc_msp = on("ACE_NUC_MSP");
     return k;
 }
 static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192; }
@@ -137,7 +142,6 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     L.i8ok = flag == 0;
     L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= (size_t)GYK_MAXDYN;
-    if (L.gyk_ok) launch_gyk_gfrag(m, L.G, L.Gf, st);
     return ACE_OK;
 }
 
@@ -251,6 +255,11 @@ int linops_setup(LinOps& L, int batch, hipStream_t st) {
     }
     if (L.shared) {
         launch_conj_transpose(m, n, L.A, L.AH, st);
+        L.frag_ok = L.Gf && L.Kfr;
+        if (L.frag_ok) {   // G and K in f64 MFMA fragment order (gyk_kernel, the nuclear m-space iteration)
+            launch_gyk_gfrag(m, L.G, L.Gf, st);
+            launch_gyk_gfrag(m, L.K, L.Kfr, st);
+        }
         ACE_TRY(i8_setup(L, st));
     }
     ACE_HIP(hipGetLastError());
@@ -536,6 +545,70 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
     return rc;
 }
 
+// A2nuclear at r = 1 on a shared A, iterated in m-space (ace_nucmsp.hip): Z and N live as
+// (coefficient of X_init, m-vector) pairs; one launch per iteration; X = opt_a X_init + A^H opt_w
+// after the loop.  Workspace: zeta, nu in Sg[0], Sg[1], K zeta, K nu in KY[0], KY[1], P0 = A X_init
+// in T, opt_w in optS, the last iterate's m-part in g; X_init in X.
+static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmState& w, const ZArgs& za0, int batch,
+                            const double* B, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
+                            double* mu_out, hipStream_t st) {
+    const int m = L.m, n = L.n;
+    NmsArgs a{};
+    a.Gf = L.Gf;
+    a.Kf = L.Kfr;
+    a.B = B;
+    a.M = w.M;
+    a.Zs = w.Sg[0];
+    a.Ns = w.Sg[1];
+    a.KZ = w.KY[0];
+    a.KN = w.KY[1];
+    a.P0 = w.T;
+    a.optW = w.optS;
+    a.optY = w.optY;
+    a.curW = w.g;
+    a.rs = w.st;
+    a.dc = DualCtl{za0.tol_abs, za0.tol_rel, za0.rho, za0.fixed_iters, n, 1, w.done};
+    ZArgs za = za0;
+    za.lazy_dual = 1;
+    {
+        ProfScope ps(ACE_K_INIT, st);
+        launch_zgemm(0, false, m, n, batch, L.A, n, 0, w.X, n, 0, w.T, nullptr, m, 0, 1, st);   // P0 = A X_init
+        launch_nms_init(batch, n, m, w.X, a, st);
+    }
+    int q = 0, it = 1;
+    for (; it <= p.maxiter; ++it) {
+        a.Yo = w.Y[q];
+        a.Yn = w.Y[1 - q];
+        za.it = it;
+        {
+            ProfScope ps(ACE_K_APPLY_G, st);
+            launch_nms(batch, m, a, za, false, st);
+        }
+        q = 1 - q;
+        if (!p.fixed_iters && (it % 8 == 0) && it < p.maxiter) {
+            int h_done = 0;
+            ACE_HIP(read_back(&h_done, w.done, sizeof(int), st));
+            if (h_done >= batch) break;
+        }
+    }
+    ACE_HIP(hipGetLastError());
+    {
+        ProfScope ps(ACE_K_FINAL, st);
+        // convergence tests the last iteration left pending (lazy dual residual)
+        a.Yo = w.Y[q];
+        a.Yn = w.Y[1 - q];
+        za.it = std::min(it, p.maxiter);
+        launch_nms(batch, m, a, za, true, st);
+        launch_nms_out(batch, n, m, w.X, a, w.V, w.g, st);
+        // X = a X_init + A^H w  (w.V holds a X_init, w.g the selected m-part)
+        launch_zgemm(2, false, n, m, batch, L.AH, m, 0, w.g, m, 0, w.optX, w.V, n, 0, 1, st);
+        launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.optX, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st,
+                          nullptr, nullptr, nullptr, nullptr);
+    }
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
 int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch, const double* B,
              const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu_out,
              hipStream_t st) {
@@ -603,6 +676,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.lazy_dual = (gyk && kn.lazy_dual) ? 1 : 0;
     za.Kf = L.K;
 
+    // A2nuclear r = 1 on a shared A: the m-space iteration (ace_nucmsp.hip)
+    const bool nms = L.shared && L.frag_ok && r == 1 && p.variant == ACE_VARIANT_NUCLEAR && kn.nuc_msp;
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
     ACE_HIP(hipMemsetAsync(w.zeros, 0, 16 * (size_t)n, st));
@@ -611,11 +686,14 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         if (pc) launch_pc_apply_a(batch, m, n, L.pcodes + pc_codesA_off(batch, m, n), L.pcb, X0, w.T, st);
         else applyA(0, X0, w.T, nullptr);                        // AX = A*X0
         launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st);
-        za.it = 0;
-        launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)
-        if (!pc && !za.lazy_dual) applyMM(L.K, w.Y[0], w.KY[0]); // K*Y (for A'*Y terms; lazy: on demand)
+        if (!nms) {
+            za.it = 0;
+            launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)
+            if (!pc && !za.lazy_dual) applyMM(L.K, w.Y[0], w.KY[0]); // K*Y (for A'*Y terms; lazy: on demand)
+        }
     }
     ACE_HIP(hipGetLastError());
+    if (nms) return admm_nuclear_msp(L, p, w, za, batch, B, Xo, Yo, iters, status, mu_out, st);
 
     int q = 0;
     const int poll = 8;

@@ -75,6 +75,9 @@ struct RealState {
     // optsrc = 3: opt_X = Z0 + A^H opt_S; 4 / 5: the same with opt_S still in the S ping-pong
     // buffer Sg[0] / Sg[1] (deferred like opt_Y: copied only before that buffer is overwritten).
     int32_t msp, mzit, z0id, msp_pad;   // msp_pad: the entry iteration it0
+    // A2nuclear m-space iteration (ace_nucmsp.hip): Z = na X_init + A^H zeta, N = nbeta X_init +
+    // A^H nu; nx0 = ||X_init||^2; the X_init coefficients of the best / last iterate
+    double na, nbeta, nx0, nopt_a, ncur_a, npad_;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -307,6 +310,32 @@ void launch_pgk(int batch, const PgkArgs& a, hipStream_t st);
 // P0 = A X0 (init, InferADMM :296-300) from the code images (codesA = codes + pc_codesA_off)
 void launch_pc_apply_a(int batch, int m, int n, const uint32_t* codesA, const double* cb, const double* X0, double* P0,
                        hipStream_t st);
+
+// A2nuclear r = 1 in m-space on a shared A (ace_nucmsp.hip): per-realisation m-vectors, c128
+// [batch][m]; Gf, Kf: G = (I + K)^-1 and K = A A^H in f64 MFMA fragment order (launch_gyk_gfrag).
+struct NmsArgs {
+    const double* Gf;
+    const double* Kf;
+    const double* B;
+    const double* Yo;   // Y of the previous iterate (read)
+    double* Yn;         // Y_new (written)
+    double* M;
+    double* Zs;         // zeta: Z = na X_init + A^H zeta
+    double* Ns;         // nu:   N = nbeta X_init + A^H nu
+    double* KZ;         // K zeta
+    double* KN;         // K nu
+    const double* P0;   // A X_init
+    double* optW;       // best iterate X = nopt_a X_init + A^H optW
+    double* optY;
+    double* curW;       // the last iterate's m-part while no objective was finite
+    RealState* rs;
+    DualCtl dc;
+};
+size_t nms_lds_bytes(int m);
+// fin: only finish the convergence tests the previous (last) iteration left pending
+void launch_nms(int nb, int m, const NmsArgs& a, const ZArgs& za, bool fin, hipStream_t st);
+void launch_nms_init(int nb, int n, int m, const double* Xi, const NmsArgs& a, hipStream_t st);
+void launch_nms_out(int nb, int n, int m, const double* Xi, const NmsArgs& a, double* V, double* Wsel, hipStream_t st);
 
 // Arguments of the Z-step kernel (ace_zprox.hip).
 struct ZArgs {

@@ -185,7 +185,9 @@ struct LinOps {
     double* c8;   // device: c, c^2
     int* i8flag;  // device: set when some component is not in {0, +-c}
     bool i8ok;
-    double* Gf;     // G in f64 MFMA fragment order for gyk_kernel (m <= GYK_MAXM), set when gyk_ok
+    double* Gf;     // G in f64 MFMA fragment order (m <= GYK_MAXM; built by linops_setup)
+    double* Kfr;    // K in the same fragment order (the A2nuclear m-space iteration, ace_nucmsp.hip)
+    bool frag_ok;   // Gf, Kfr hold G, K
     bool gyk_ok;
     bool allow_i8;  // caller's choice (ace_admm_cfg::f64_applies == 0), set before linops_setup
     // private regime, phase-code A_b (ace_private.hip): 2-bit code images, c_b, and G_b as lower

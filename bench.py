@@ -146,6 +146,14 @@ def nuclear_bytes(m, n):
     return {"apply_G": 16.0 * 7 * m + 8.0 * m + 32.0 * n, "apply_AH": 16.0 * (m + n), "zstep": 80.0 * n}
 
 
+def nms_bytes(m):
+    """A2nuclear at r = 1 in m-space (ace_nucmsp.hip::nms_kernel, one launch per iteration): Z and N
+    as (X_init coefficient, m-vector) pairs, so no n-vector moves.  Per realisation and iteration:
+    read Y, M, P0 = A X_init, zeta, nu, K zeta, K nu (c128) and B (f64); write Y_new, M, zeta', nu',
+    K zeta', K nu' (opt_w / opt_Y on an improved objective are bookkeeping copies, not counted)."""
+    return 16.0 * 13 * m + 8.0 * m
+
+
 def private_bytes(m, n):
     """Algorithmic HBM bytes per realisation per iteration of pgk_kernel (private phase-code
     codebooks, ace_private.hip) in the steady state (A V = AX):
@@ -162,10 +170,12 @@ def private_ops(m, n):
     return {"int8": 2.0 * 3 * 8 * (2 * n) * (2 * m), "f64": 8.0 * m * m}
 
 
-def unit_resources(k, m, n, *, variant, pc, gyf, gyk, i8, msp_frac):
+def unit_resources(k, m, n, *, variant, pc, gyf, gyk, i8, msp_frac, nms=False):
     """Per-realisation work of one launch of kernel class k on the unit path: {resource: amount}
     with resources f64 (flops), int8 (ops), hbm (bytes).  {} = latency-bound, no roofline."""
     uf, io, ub = unit_flops(m, n, 0, 0), unit_i8_ops(m, n), unit_bytes(m, n, 0, 0)
+    if nms:   # A2nuclear m-space iteration: g = G T on the f64 matrix cores and m-vectors only
+        return {"f64": uf["apply_G"], "hbm": nms_bytes(m)} if k == "apply_G" else {}
     if pc:
         po = private_ops(m, n)
         return {"hbm": private_bytes(m, n), "int8": po["int8"], "f64": po["f64"]} if k == "apply_G" else {}
@@ -253,6 +263,7 @@ PMC_KERNEL = {  # kernel-class -> kernel name prefix in the PMC profiles, per wo
     "private": {"zstep": "zstep1w_kernel<false>", "apply_G": "pgk_kernel"},
     "nuclear": {"zstep": "zstep1w_kernel<false>", "apply_AH": "i8ah_kernel<false, false>", "apply_G": "gyk_kernel"},
 }
+PMC_KERNEL["nuclear"] = {"apply_G": "nms_kernel<false>"}   # the m-space iteration (ace_nucmsp.hip)
 PMC_KERNEL["config5"] = PMC_KERNEL["nuclear"]
 
 
@@ -438,8 +449,11 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         i8 = (not private) and os.environ.get("ACE_NO_I8") != "1"
         # the unit path runs as `nsplit` concurrent sub-batches (ace_admm.cpp::split_count, ACE_SPLIT):
         # every launch of an iteration kernel covers bsz / nsplit realisations
+        # A2nuclear r = 1 on a shared A runs the m-space iteration (ace_nucmsp.hip, one launch per
+        # iteration over the whole batch) unless ACE_NUC_MSP=0
+        nms = (not private) and variant == "A2nuclear" and m <= 256 and os.environ.get("ACE_NUC_MSP") != "0"
         nsplit = 1
-        if i8 and m <= 256:
+        if i8 and m <= 256 and not nms:
             nsplit = max(1, min(4, int(os.environ.get("ACE_SPLIT", "2"))))
             while nsplit > 1 and bsz // nsplit < 256:
                 nsplit -= 1
@@ -455,7 +469,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         msp_frac = msp_steps.value / float(args.steps * bsz * args.iters) if msp_on else 0.0
         # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
         pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
-        ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac)
+        ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac, nms=nms)
         timed = [k for k in kernels if k in ITER_CLASSES and unit_resources(k, m, n, **ctx)]
         # every timed class launches once per iteration: dominant = largest average launch
         dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
@@ -464,7 +478,12 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             res = {r: a * per_launch for r, a in unit_resources(k, m, n, **ctx).items()}
             name = "apply_G (gyf_kernel)" if (k == "apply_G" and gyf) else k
             note = None
-            if k == "apply_G" and gyf:
+            if nms:
+                name = "apply_G (nms_kernel)"
+                note = ("A2nuclear m-space iteration (ace_nucmsp.hip): T, g = G T (f64 3M; achieved counts 8 "
+                        "flops per complex MAC), K g = T - g, the Y-step and the m-space Z-step, one phase after "
+                        "another in each work-group; bytes: bench.nms_bytes")
+            elif k == "apply_G" and gyf:
                 note = ("gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per complex MAC), the "
                         "Y-step, then W = A^H g (int8 digit planes) with the certified Z-step pass (Z in, Z' out) "
                         "in its epilogue, one phase after another in each work-group; a realisation in m-space "
@@ -472,7 +491,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
                         "moves S in / S' out instead (bench.msp_bytes); bound = the resource with the largest "
                         "time at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time")
             elif variant == "A2nuclear" and i8:
-                note = ("A2nuclear unit path (bench.nuclear_bytes): A V in gyk_kernel every iteration, plain "
+                note = ("A2nuclear n-space unit path (bench.nuclear_bytes): A V in gyk_kernel every iteration, plain "
                         "apply_AH, the soft-threshold Z-step streams W, Z, N")
             r = roofline_from(name, kernels[k]["avg_ms"] * 1e-3, res, bounds={"f64": "valu"} if pc else None,
                               note=note)

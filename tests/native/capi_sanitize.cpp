@@ -1,0 +1,216 @@
+// Host AddressSanitizer / UndefinedBehaviorSanitizer exercise of the C-ABI.
+// Built by `make -C 2ace-mmwave-channel-estimation_amd/csrc sanitize`: the host side of every
+// translation unit is compiled with -fsanitize=address,undefined (device code is not
+// instrumented), linked with this driver into tests/native/ace_capi_sanitize.
+//
+//   ace_capi_sanitize cpu   host-only entry points and the argument checks that return before
+//                           any device call (runs without a GPU: tests/test_sanitize.py)
+//   ace_capi_sanitize gpu   the above plus small solves through every *_host wrapper, the driver
+//                           and the beamformer (tests/test_gpu_sanitize.py)
+// Any sanitizer report aborts with a non-zero exit; the program prints "OK" at the end.
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "ace.h"
+
+namespace {
+
+int g_fail = 0;
+#define CHECK(c)                                                                  \
+    do {                                                                          \
+        if (!(c)) {                                                               \
+            fprintf(stderr, "CHECK failed: %s (%s:%d) last_error=%s\n", #c, __FILE__, \
+                    __LINE__, ace_last_error());                                  \
+            ++g_fail;                                                             \
+        }                                                                         \
+    } while (0)
+
+uint64_t g_rng = 0x9E3779B97F4A7C15ull;
+uint64_t next_u64() {
+    g_rng ^= g_rng << 13;
+    g_rng ^= g_rng >> 7;
+    g_rng ^= g_rng << 17;
+    return g_rng;
+}
+double uni() { return (double)(next_u64() >> 11) * (1.0 / 9007199254740992.0); }
+
+// phase-code codebook rows j^k / sqrt(n) (complex row-major, interleaved)
+std::vector<double> codebook(int m, int n) {
+    std::vector<double> A(2 * (size_t)m * n);
+    const double s = 1.0 / std::sqrt((double)n);
+    const double re[4] = {1, 0, -1, 0}, im[4] = {0, 1, 0, -1};
+    for (size_t e = 0; e < (size_t)m * n; ++e) {
+        const int k = (int)(next_u64() & 3);
+        A[2 * e] = s * re[k];
+        A[2 * e + 1] = s * im[k];
+    }
+    return A;
+}
+std::vector<double> cvec(size_t n) {
+    std::vector<double> v(2 * n);
+    for (auto& x : v) x = uni() - 0.5;
+    return v;
+}
+// B[b][i] = |A x_b|
+std::vector<double> magnitudes(const std::vector<double>& A, const std::vector<double>& X, int batch, int m, int n) {
+    std::vector<double> B((size_t)batch * m);
+    for (int b = 0; b < batch; ++b)
+        for (int i = 0; i < m; ++i) {
+            std::complex<double> s = 0;
+            for (int k = 0; k < n; ++k)
+                s += std::complex<double>(A[2 * ((size_t)i * n + k)], A[2 * ((size_t)i * n + k) + 1]) *
+                     std::complex<double>(X[2 * ((size_t)b * n + k)], X[2 * ((size_t)b * n + k) + 1]);
+            B[(size_t)b * m + i] = std::abs(s);
+        }
+    return B;
+}
+bool finite(const std::vector<double>& v) {
+    for (double x : v)
+        if (!std::isfinite(x)) return false;
+    return true;
+}
+
+void host_only() {
+    int32_t M[8];
+    CHECK(ace_driver_m_sweep(4, 4, M) == 8);
+    CHECK(ace_driver_m_sweep(16, 16, M) == 8 && M[7] == 1024);
+    std::vector<int32_t> perm(64);
+    CHECK(ace_driver_randperm(7, 1, 64, 64, perm.data()) == 0);
+    std::vector<int> seen(64, 0);
+    for (int v : perm) seen[v]++;
+    for (int c : seen) CHECK(c == 1);
+    CHECK(ace_driver_randperm(7, 1, 8, 9, perm.data()) < 0);   // k > P
+    ace_admm_cfg ac;
+    ace_admm_cfg_default(&ac);
+    CHECK(ace_admm_workspace_size(&ac, 16, 64, 256) > 0);
+    ace_pipeline_cfg pc;
+    ace_pipeline_cfg_default(&pc, ACE_VARIANT_A2ONLY);
+    CHECK(pc.restarts == 3);
+    CHECK(ace_pipeline_workspace_size(&pc, 4, 64, 256) > 0);
+    ace_pipeline_cfg_default(&pc, ACE_VARIANT_NUCLEAR);
+    CHECK(pc.restarts == 1);
+    ace_phaselift_cfg fc;
+    ace_phaselift_cfg_default(&fc);
+    CHECK(ace_phaselift_workspace_size(&fc, 2, 16, 64) > 0);
+    // argument checks that return before any device work
+    double d = 0;
+    CHECK(ace_admm_solve_host(&ac, 1, 8, 15, 4, 4, &d, &d, &d, &d, &d, nullptr, nullptr, nullptr) == ACE_ERR_ARG);
+    CHECK(ace_recover_driver(9, 4, 4, 8, &d, &d, &d, 1, 0, nullptr, &d, &d) == ACE_ERR_ARG);
+    CHECK(ace_recover_driver(0, 4, 4, 8, &d, &d, &d, 0, 0, nullptr, &d, &d) == ACE_ERR_ARG);
+    CHECK(ace_recover_driver(0, 4, 4, 8, nullptr, &d, &d, 1, 0, nullptr, &d, &d) == ACE_ERR_ARG);
+    CHECK(strlen(ace_last_error()) > 0);
+    CHECK(strlen(ace_version()) > 0);
+}
+
+void gpu_solves() {
+    const int tx = 4, rx = 4, n = 16, m = 48, batch = 3;
+    const auto A = codebook(m, n);
+    const auto H = cvec((size_t)batch * n);
+    const auto B = magnitudes(A, H, batch, m, n);
+    // ---- InferADMM (r = 1), both variants, shared and private codebooks
+    for (int variant = 0; variant < 2; ++variant)
+        for (int shared = 0; shared < 2; ++shared) {
+            ace_admm_cfg c;
+            ace_admm_cfg_default(&c);
+            c.variant = variant;
+            c.a_shared = shared;
+            c.maxiter = 40;
+            std::vector<double> Ab = A;
+            if (!shared)
+                for (int b = 1; b < batch; ++b) Ab.insert(Ab.end(), A.begin(), A.end());
+            const auto X0 = cvec((size_t)batch * n);
+            std::vector<double> X(2 * (size_t)batch * n), Y(2 * (size_t)batch * m), mu(batch);
+            std::vector<int32_t> it(batch);
+            std::vector<uint32_t> st(batch);
+            CHECK(ace_admm_solve_host(&c, batch, m, n, tx, rx, Ab.data(), B.data(), X0.data(), X.data(), Y.data(),
+                                      it.data(), st.data(), mu.data()) == ACE_OK);
+            CHECK(finite(X) && finite(Y));
+            for (int v : it) CHECK(v >= 1 && v <= 40);
+        }
+    // ---- pipeline (3 restarts, A2only) and the nuclear pipeline (1 restart)
+    {
+        const int mp = 64, mt = 60;
+        const auto Ap = codebook(mp, n);
+        const auto Bp = magnitudes(Ap, H, batch, mp, n);
+        for (int variant = 0; variant < 2; ++variant) {
+            ace_pipeline_cfg c;
+            ace_pipeline_cfg_default(&c, variant);
+            c.maxiter = 40;
+            std::vector<int32_t> tr((size_t)c.restarts * mt);
+            for (int r = 0; r < c.restarts; ++r)
+                CHECK(ace_driver_randperm(11, r, mp, mt, tr.data() + (size_t)r * mt) == 0);
+            std::vector<double> X(2 * (size_t)batch * n), Y(2 * (size_t)batch * mp), q(batch);
+            std::vector<int32_t> si((size_t)batch * (4 * c.restarts + 1));
+            std::vector<uint32_t> st(batch);
+            CHECK(ace_pipeline_solve_host(&c, batch, mp, n, tx, rx, Ap.data(), Bp.data(), tr.data(), X.data(),
+                                          Y.data(), q.data(), si.data(), st.data()) == ACE_OK);
+            CHECK(finite(X) && finite(q));
+            // repeated rows are rejected
+            std::vector<int32_t> bad((size_t)c.restarts * mt, 0);
+            CHECK(ace_pipeline_solve_host(&c, batch, mp, n, tx, rx, Ap.data(), Bp.data(), bad.data(), X.data(),
+                                          Y.data(), q.data(), si.data(), st.data()) == ACE_ERR_ARG);
+        }
+    }
+    // ---- PhaseLift (m < n, full row rank)
+    {
+        const int mp = 12;
+        const auto Phi = cvec((size_t)mp * n);
+        std::vector<double> b((size_t)batch * mp);
+        const auto Bm = magnitudes(Phi, H, batch, mp, n);
+        for (size_t i = 0; i < b.size(); ++i) b[i] = Bm[i] * Bm[i];
+        ace_phaselift_cfg c;
+        ace_phaselift_cfg_default(&c);
+        c.maxIts = 30;
+        std::vector<double> sig(2 * (size_t)batch * n);
+        std::vector<int32_t> it(batch);
+        std::vector<uint32_t> st(batch);
+        CHECK(ace_phaselift_solve_host(&c, batch, mp, n, Phi.data(), b.data(), sig.data(), it.data(), st.data()) ==
+              ACE_OK);
+        CHECK(finite(sig));
+    }
+    // ---- driver (A2only and PhaseLift) on an amp/angle codebook of P = 64 beams
+    {
+        const int P = 64;
+        std::vector<double> amp((size_t)P * n, 1.0 / std::sqrt((double)n)), ang((size_t)P * n), rss(P);
+        for (auto& a : ang) a = (double)(next_u64() & 3) * M_PI / 2;
+        for (auto& r : rss) r = -60.0 + 10.0 * uni();
+        const int32_t Ms[2] = {25, 36};
+        for (int drv : {ACE_DRIVER_A2ONLY, ACE_DRIVER_PHASELIFT}) {
+            std::vector<double> ha(2 * (size_t)n), hg(2 * (size_t)n);
+            CHECK(ace_recover_driver(drv, tx, rx, P, amp.data(), ang.data(), rss.data(), 1, 2, Ms, ha.data(),
+                                     hg.data()) == 2);
+            CHECK(finite(ha) && finite(hg));
+        }
+    }
+    // ---- beamformer
+    {
+        const int bb = 4;
+        const auto Hb = cvec((size_t)bb * n);
+        std::vector<uint8_t> wr((size_t)bb * rx), wt((size_t)bb * tx);
+        std::vector<int32_t> idx(2 * bb);
+        std::vector<double> rss(bb);
+        std::vector<uint32_t> st(bb);
+        CHECK(ace_svd_beamformer_host(bb, tx, rx, Hb.data(), nullptr, wr.data(), wt.data(), idx.data(), rss.data(),
+                                      st.data(), nullptr, nullptr) == ACE_OK);
+        for (uint8_t c : wr) CHECK(c < 4);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const bool gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
+    host_only();
+    if (gpu) gpu_solves();
+    if (g_fail) {
+        fprintf(stderr, "%d checks failed\n", g_fail);
+        return 1;
+    }
+    printf("OK\n");
+    return 0;
+}

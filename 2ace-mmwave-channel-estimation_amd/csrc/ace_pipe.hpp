@@ -42,7 +42,15 @@ void launch_fill(long long count, double v, double* dst, hipStream_t st);
 // eigenvector of As^H As for lam scaled by sqrt(lam) -- exactly one column of
 // X = V(:, 1:r) * diag(sqrt(s(1:r))).  The kernels leave W[b][k] = D_b u_k (k-th largest
 // eigenvalue first) and X = A_t^H W is one GEMM over batch*r vectors.
-size_t spectral_scratch_bytes(int mt, int batch, int r);
+//
+// When m_t > n the n x n primal Gram As^H As is the smaller eigenproblem (the driver's large
+// sweep points, e.g. m_t = 972 at n = 256): launch_spectral_primal forms it per realisation with
+// one batched GEMM (A_t^H weighted by B_i^2/||a_i||^2), symmetrises it as the oracle does, and
+// writes X = V(:, 1:r) diag(sqrt(max(0, s))) directly ([batch][r][n]).
+bool spectral_primal(int mt, int n);
+size_t spectral_scratch_bytes(int mt, int n, int batch, int r);
+int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
+                           double* scratch, double* X, int* status, hipStream_t st);
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
                     int* status, hipStream_t st);
 

@@ -60,7 +60,7 @@ void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
     linops_carve(cv, true, d.batch, d.mt, d.n, &w->Lt);
     linops_carve(cv, true, d.batch, d.m, d.n, &w->Lf);
     w->W = cv.take(cz * B * d.r * d.mt);
-    w->spec = cv.take(spectral_scratch_bytes(d.mt, d.batch, d.r));
+    w->spec = cv.take(spectral_scratch_bytes(d.mt, d.n, d.batch, d.r));
     w->Xs = cv.take(cz * B * d.r * d.n);
     w->Xs_s = cv.take(cz * B * d.r * d.n);
     w->X1 = cv.take(cz * B * d.r * d.n);
@@ -103,7 +103,8 @@ int validate_dims(const ace_pipeline_cfg* c, int batch, int m, int n, PipeDims* 
     if (mt < r)
         return fail(ACE_ERR_UNSUPPORTED, "floor(m*cc_frac) = %d train rows < r = %d: the spectral initialisation "
                     "would take eigenvectors of the null space (ill-posed, not supported)", mt, r);
-    if (mt > 1600) return fail(ACE_ERR_UNSUPPORTED, "train rows %d > 1600 (spectral tridiagonalisation LDS limit)", mt);
+    if (std::min(mt, n) > 1600)
+        return fail(ACE_ERR_UNSUPPORTED, "min(train rows %d, n %d) > 1600 (spectral tridiagonalisation LDS limit)", mt, n);
     if (n > 4096) return fail(ACE_ERR_UNSUPPORTED, "n must be <= 4096 (got %d)", n);
     *d = PipeDims{batch, m, n, 0, 0, r, mt, m - mt, c->restarts};
     return ACE_OK;
@@ -244,9 +245,14 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         // ---- :58 SpectralInitialize: W = D u_k, X = A_t^H W
         {
             ProfScope ps(ACE_K_SETUP, st);
-            if (launch_spectral(d.mt, d.r, batch, w.Lt.K, w.Bt, w.spec, w.W, w.status_dev, st))
-                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
-            launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
+            if (spectral_primal(d.mt, n)) {
+                if (launch_spectral_primal(d.mt, n, d.r, batch, w.Lt.K, w.Lt.AH, w.Bt, w.spec, w.Xs, w.status_dev, st))
+                    return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: n = %d too large", n);
+            } else {
+                if (launch_spectral(d.mt, d.r, batch, w.Lt.K, w.Bt, w.spec, w.W, w.status_dev, st))
+                    return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
+                launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
+            }
         }
         ACE_HIP(hipGetLastError());
         // ---- :65-68 impl (use_rank_one = false) and test quality

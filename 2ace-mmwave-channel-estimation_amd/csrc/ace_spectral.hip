@@ -24,8 +24,11 @@
 //
 // X = A_t^H W is then one MFMA GEMM over batch*r vectors (ace_pipeline.cpp).
 // Realisations are processed in chunks so the C matrices of a chunk stay in the L2/MALL.
+#include <algorithm>
+
 #include "ace_common.hpp"
 #include "ace_pipe.hpp"
+#include "ace_host.hpp"
 
 namespace ace {
 
@@ -503,10 +506,89 @@ int backxf_chunk(int mt) {
 }
 }  // namespace
 
-size_t spectral_scratch_bytes(int mt, int batch, int r) {
+namespace {
+// ---- primal form for m_t > n: the n x n Gram As^H As itself (a smaller eigenproblem)
+// Ast[b][i][k] = w_b[k] A_t^H[i][k], w_b[k] = B_t[b][k]^2 / ||a_k||^2 (0 for a zero row), so that
+// one batched GEMM C_b = conj(Ast_b) applied to the rows of A_t^H gives As^H As row by row.
+__global__ __launch_bounds__(256) void spec_weight_kernel(int mt, int n, int nb, const double* Kp, const double* AHp,
+                                                          const double* Bt, double* Astp) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x, per = (long long)n * mt;
+    if (e >= per * nb) return;
+    const int b = (int)(e / per), k = (int)(e % mt);
+    const double kkk = reinterpret_cast<const d2*>(Kp)[(long long)k * mt + k].x;
+    const double bk = Bt[(long long)b * mt + k];
+    const double wk = kkk > 0.0 ? bk * bk / kkk : 0.0;
+    const d2 a = reinterpret_cast<const d2*>(AHp)[e % per];
+    reinterpret_cast<d2*>(Astp)[e] = make_double2(wk * a.x, wk * a.y);
+}
+// C_b <- (C_b + C_b^H) / 2 in place (the oracle's symmetrisation), one thread per pair i <= j
+__global__ __launch_bounds__(256) void spec_herm_kernel(int n, double* scratch, SpecLayout lay) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 16 + threadIdx.x / 16, j = (int)(threadIdx.x % 16) + blockIdx.z * 16;
+    if (i >= n || j >= n || j < i) return;
+    d2* C = reinterpret_cast<d2*>(scratch + b * lay.stride + lay.C);
+    const d2 a = C[(long long)i * n + j], c = C[(long long)j * n + i];
+    const d2 h = make_double2(0.5 * (a.x + c.x), 0.5 * (a.y - c.y));
+    C[(long long)i * n + j] = i == j ? make_double2(h.x, 0.0) : h;
+    if (i != j) C[(long long)j * n + i] = make_double2(h.x, -h.y);
+}
+// X[b][k][:] *= sqrt(max(0, lam_k))  (SpectralInitialize :571-573)
+__global__ __launch_bounds__(256) void spec_sqrt_scale_kernel(int n, int r, const double* scratch, SpecLayout lay,
+                                                              double* Xp) {
+    const int b = blockIdx.y, k = blockIdx.x;
+    const double lam = scratch[b * lay.stride + lay.lam + k];
+    const double s = sqrt(lam > 0.0 ? lam : 0.0);
+    d2* x = reinterpret_cast<d2*>(Xp) + ((long long)b * r + k) * n;
+    for (int i = threadIdx.x; i < n; i += 256) x[i] = cscale(x[i], s);
+}
+constexpr size_t PRIMAL_AST_BYTES = 256ull << 20;   // weighted A_t^H images per chunk
+int primal_chunk(int mt, int n, int batch) {
+    long long c = (long long)(PRIMAL_AST_BYTES / (16ull * n * mt));
+    if (c < 1) c = 1;
+    if (c > SPEC_CHUNK) c = SPEC_CHUNK;
+    return (int)(c < batch ? c : batch);
+}
+}  // namespace
+
+bool spectral_primal(int mt, int n) { return mt > n; }
+
+size_t spectral_scratch_bytes(int mt, int n, int batch, int r) {
+    if (spectral_primal(mt, n)) {
+        const SpecLayout lay(n, r);
+        const int chunk = primal_chunk(mt, n, batch);
+        return (sizeof(double) * (size_t)lay.stride + 16ull * n * mt + 256) * chunk;
+    }
     const SpecLayout lay(mt, r);
     const int chunk = batch < SPEC_CHUNK ? batch : SPEC_CHUNK;
     return sizeof(double) * (size_t)lay.stride * chunk;
+}
+
+int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
+                           double* scratch, double* X, int* status, hipStream_t st) {
+    const SpecLayout lay(n, r);
+    const size_t sm_h = (size_t)n * (16 + 16 + 8), sm_t = (size_t)n * 16;
+    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+    const int chunk = primal_chunk(mt, n, batch);
+    double* Ast = scratch + (((size_t)lay.stride * chunk + 31) & ~(size_t)31);
+    for (int b0 = 0; b0 < batch; b0 += chunk) {
+        const int nb = batch - b0 < chunk ? batch - b0 : chunk;
+        const long long elems = (long long)nb * n * mt;
+        hipLaunchKernelGGL(spec_weight_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, st, mt, n, nb, K, AH,
+                           Bt + (long long)b0 * mt, Ast);
+        // C_b[v][i] = sum_k w_k A_t[k][i] conj(A_t[k][v]) = (As^H As)[v][i]
+        launch_zgemm(0, true, n, mt, n, Ast, mt, (long long)n * mt, AH, mt, 0, scratch + lay.C, nullptr, n,
+                     lay.stride / 2, nb, st);
+        hipLaunchKernelGGL(spec_herm_kernel, dim3((n + 15) / 16, nb, (n + 15) / 16), dim3(256), 0, st, n, scratch, lay);
+        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
+                           nullptr);
+        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, n, nullptr, scratch, lay, status, b0, nullptr);
+        const int cv = backxf_chunk(n);
+        double* Xb = X + 2LL * b0 * r * n;
+        hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * n * 16, st, n, r, scratch, lay, Xb, 0,
+                           nullptr, cv);
+        hipLaunchKernelGGL(spec_sqrt_scale_kernel, dim3(r, nb), dim3(256), 0, st, n, r, scratch, lay, Xb);
+    }
+    return ACE_OK;
 }
 
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
@@ -526,12 +608,128 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
     return ACE_OK;
 }
 
+// ---- blocked (compact-WY) back-transform for many eigenvectors (PhaseLift's prox_trace keeps
+// 100-256 of d = 256).  zhetrd's Q = H_0 H_1 ... H_{d-2}; per block of WY_NB consecutive
+// reflectors Q_j = I - V_j T_j V_j^H (LAPACK zlarft, forward, columnwise), and
+// Q z = Q_0 (Q_1 ( ... Q_last z)) is three batched MFMA GEMMs per block over all vectors:
+//   W1 = V_j^H Z,  W2 = T_j W1,  Z -= V_j W2.
+// V_j^H reads the reflectors where hetrd left them (row k of C, C[k][k+1] = 1; the stale entries
+// left of it are zeroed by wy_pack_kernel), V_j comes from a transposed copy (VT_j), and the
+// Gram V_j^H V_j that zlarft needs is one more GEMM.
+namespace {
+constexpr int WY_NB = 64;
+struct WyLayout {            // per realisation, in doubles
+    long long VT, Tm, Gm, W1, W2, stride;
+    int nblk;
+    WyLayout(int d, int kmax) {
+        nblk = (d - 1 + WY_NB - 1) / WY_NB;
+        long long o = 0;
+        auto take = [&](long long nd) { long long p = o; o += (nd + 31) & ~31LL; return p; };
+        VT = take(2LL * nblk * d * WY_NB);     // block j: [L_j][WY_NB] at VT + 2 j d WY_NB
+        Tm = take(2LL * nblk * WY_NB * WY_NB);
+        Gm = take(2LL * nblk * WY_NB * WY_NB);
+        W1 = take(2LL * kmax * WY_NB);
+        W2 = take(2LL * kmax * WY_NB);
+        stride = o;
+    }
+};
+bool wy_path(int d, int kmax) { return d >= 96 && kmax >= 32; }
+
+// zero what is not reflector in rows 0..d-2 of C (left of C[k][k+1] within the row's block, and the
+// whole row when tau_k = 0: H_k = I) and write VT_j[p][a] = v_{j0+a}[j0+1+p]
+__global__ __launch_bounds__(256) void wy_pack_kernel(int d, double* scratch, SpecLayout lay, double* wy, WyLayout wl,
+                                                      const int* active) {
+    const int b = blockIdx.x;
+    if (active && !active[b]) return;
+    double* base = scratch + b * lay.stride;
+    d2* C = reinterpret_cast<d2*>(base + lay.C);
+    const d2* taus = reinterpret_cast<const d2*>(base + lay.tau);
+    d2* VT = reinterpret_cast<d2*>(wy + b * wl.stride + wl.VT);
+    for (int j = 0; j < wl.nblk; ++j) {
+        const int j0 = j * WY_NB, L = d - j0 - 1;
+        d2* vt = VT + (long long)j * d * WY_NB;
+        for (long long e = threadIdx.x; e < (long long)L * WY_NB; e += 256) {
+            const int p = (int)(e / WY_NB), a = (int)(e % WY_NB), k = j0 + a;
+            d2 v = make_double2(0.0, 0.0);
+            if (k < d - 1) {
+                const d2 tk = taus[k];
+                d2& c = C[(long long)k * d + j0 + 1 + p];
+                if (p < a || (tk.x == 0.0 && tk.y == 0.0)) c = make_double2(0.0, 0.0);
+                else v = c;
+            }
+            vt[e] = v;
+        }
+    }
+}
+
+// T_j (upper triangular, row-major [a][c]) from the Gram G[v][i] = (V^H V)[i][v] (zlarft):
+// T[i][i] = tau_i,  T[0:i][i] = -tau_i T[0:i][0:i] (V^H V)[0:i][i]
+__global__ __launch_bounds__(64) void wy_larft_kernel(int d, const double* scratch, SpecLayout lay, double* wy,
+                                                      WyLayout wl, const int* active) {
+    const int j = blockIdx.x, b = blockIdx.y, a = threadIdx.x;
+    if (active && !active[b]) return;
+    __shared__ d2 T[WY_NB][WY_NB + 1];
+    __shared__ d2 y[WY_NB];
+    const d2* taus = reinterpret_cast<const d2*>(scratch + b * lay.stride + lay.tau);
+    const d2* G = reinterpret_cast<const d2*>(wy + b * wl.stride + wl.Gm) + (long long)j * WY_NB * WY_NB;
+    d2* Tg = reinterpret_cast<d2*>(wy + b * wl.stride + wl.Tm) + (long long)j * WY_NB * WY_NB;
+    const int j0 = j * WY_NB, nbj = min(WY_NB, d - 1 - j0);
+    for (int c = 0; c < WY_NB; ++c) T[a][c] = make_double2(0.0, 0.0);
+    __syncthreads();
+    for (int i = 0; i < nbj; ++i) {
+        const d2 ti = taus[j0 + i];
+        if (a < i) y[a] = cscale(cmul(ti, G[(long long)i * WY_NB + a]), -1.0);
+        __syncthreads();
+        if (a < i) {
+            d2 acc = make_double2(0.0, 0.0);
+            for (int c = a; c < i; ++c) acc = cadd(acc, cmul(T[a][c], y[c]));
+            T[a][i] = acc;
+        }
+        if (a == 0) T[i][i] = ti;
+        __syncthreads();
+    }
+    for (int c = 0; c < WY_NB; ++c) Tg[(long long)a * WY_NB + c] = T[a][c];
+}
+
+// V[b][q][:] = z_q (real tridiagonal eigenvector) for q < k_b, 0 for k_b <= q < kuse
+__global__ __launch_bounds__(256) void wy_expand_kernel(int d, int kuse, const double* scratch, SpecLayout lay,
+                                                        double* Vout, int ldv, const int* active) {
+    const int b = blockIdx.y;
+    if (active && !active[b]) return;
+    const double* base = scratch + b * lay.stride;
+    const int k = (int)base[lay.misc];
+    d2* V = reinterpret_cast<d2*>(Vout) + (long long)b * ldv * d;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < (long long)kuse * d; e += 256LL * gridDim.x) {
+        const int q = (int)(e / d);
+        V[e] = make_double2(q < k ? base[lay.z + e] : 0.0, 0.0);
+    }
+}
+
+// kmax_out[0] = max over active realisations of k_b
+__global__ __launch_bounds__(256) void wy_kmax_kernel(int batch, const double* scratch, SpecLayout lay,
+                                                      const int* active, int* kmax_out) {
+    int k = 0;
+    for (int b = threadIdx.x; b < batch; b += 256)
+        if (!active || active[b]) k = max(k, (int)scratch[b * lay.stride + lay.misc]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k = max(k, __shfl_xor(k, o, 64));
+    __shared__ int s[4];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) kmax_out[0] = max(max(s[0], s[1]), max(s[2], s[3]));
+}
+}  // namespace
+
 // ---- thresholded / top-k Hermitian eigen (PhaseLift prox_trace and its final eig): see ace_pipe.hpp
 HeevLayout heev_layout(int d, int kmax) {
     const SpecLayout lay(d, kmax);
     return HeevLayout{lay.stride, lay.C, lay.misc, lay.lam};
 }
-size_t heev_scratch_bytes(int d, int kmax, int batch) { return sizeof(double) * (size_t)SpecLayout(d, kmax).stride * batch; }
+size_t heev_scratch_bytes(int d, int kmax, int batch) {
+    size_t b = sizeof(double) * (size_t)SpecLayout(d, kmax).stride * batch;
+    if (wy_path(d, kmax)) b += sizeof(double) * (size_t)WyLayout(d, kmax).stride * batch + 256;
+    return b;
+}
 
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
                 const int* active, hipStream_t st) {
@@ -540,9 +738,41 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
     hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
-    const int cv = backxf_chunk(d);
-    hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), (size_t)cv * d * 16, st, d, kmax, scratch, lay, V, 0,
-                       active, cv);
+    if (!wy_path(d, kmax)) {
+        const int cv = backxf_chunk(d);
+        hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), (size_t)cv * d * 16, st, d, kmax, scratch, lay, V, 0,
+                           active, cv);
+        return ACE_OK;
+    }
+    const WyLayout wl(d, kmax);
+    double* wy = scratch + (size_t)lay.stride * batch;
+    int* kdev = reinterpret_cast<int*>(wy + (size_t)wl.stride * batch);
+    hipLaunchKernelGGL(wy_kmax_kernel, dim3(1), dim3(256), 0, st, batch, scratch, lay, active, kdev);
+    int kuse = 0;
+    if (read_back(&kuse, kdev, sizeof(int), st) != hipSuccess) return ACE_ERR_HIP;
+    if (kuse <= 0) return ACE_OK;   // nothing above the threshold anywhere (callers read k_b = 0)
+    if (kuse > kmax) kuse = kmax;
+    hipLaunchKernelGGL(wy_pack_kernel, dim3(batch), dim3(256), 0, st, d, scratch, lay, wy, wl, active);
+    const long long sC = lay.stride / 2, sW = wl.stride / 2, sV = (long long)kmax * d;
+    for (int j = 0; j < wl.nblk; ++j) {   // Gram V_j^H V_j
+        const int j0 = j * WY_NB, nbj = std::min(WY_NB, d - 1 - j0), L = d - j0 - 1;
+        const double* Vr = scratch + lay.C + 2LL * ((long long)j0 * d + j0 + 1);
+        launch_zgemm(0, true, nbj, L, nbj, Vr, d, sC, Vr, d, sC, wy + wl.Gm + 2LL * j * WY_NB * WY_NB, nullptr, WY_NB,
+                     sW, batch, st);
+    }
+    hipLaunchKernelGGL(wy_larft_kernel, dim3(wl.nblk, batch), dim3(64), 0, st, d, scratch, lay, wy, wl, active);
+    hipLaunchKernelGGL(wy_expand_kernel, dim3((kuse * d + 255) / 256 < 64 ? (kuse * d + 255) / 256 : 64, batch),
+                       dim3(256), 0, st, d, kuse, scratch, lay, V, kmax, active);
+    for (int j = wl.nblk - 1; j >= 0; --j) {
+        const int j0 = j * WY_NB, nbj = std::min(WY_NB, d - 1 - j0), L = d - j0 - 1;
+        const double* Vr = scratch + lay.C + 2LL * ((long long)j0 * d + j0 + 1);
+        double* Zj = V + 2LL * (j0 + 1);
+        launch_zgemm(0, true, nbj, L, kuse, Vr, d, sC, Zj, d, sV, wy + wl.W1, nullptr, WY_NB, sW, batch, st);
+        launch_zgemm(0, false, nbj, nbj, kuse, wy + wl.Tm + 2LL * j * WY_NB * WY_NB, WY_NB, sW, wy + wl.W1, WY_NB, sW,
+                     wy + wl.W2, nullptr, WY_NB, sW, batch, st);
+        launch_zgemm(1, false, L, nbj, kuse, wy + wl.VT + 2LL * j * d * WY_NB, WY_NB, sW, wy + wl.W2, WY_NB, sW, Zj,
+                     Zj, d, sV, batch, st);
+    }
     return ACE_OK;
 }
 

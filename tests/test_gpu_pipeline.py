@@ -29,12 +29,12 @@ def _codebook(codes):
     return (1j ** codes.astype(np.int64)) / math.sqrt(n)
 
 
-def _check(res, X, q, its, rb, tol=TOL):
+def _check(res, X, q, its, rb, tol=TOL, qtol=1e-9):
     for b in range(X.shape[0]):
         e = O.phase_aligned_rel_err(res.X[b], X[b])
         assert e <= tol, (b, e)
     assert np.array_equal(res.stage_iters, np.asarray(its)), (res.stage_iters, its)
-    assert np.allclose(res.quality, q, rtol=0, atol=1e-9), (res.quality, q)
+    assert np.allclose(res.quality, q, rtol=0, atol=qtol), (res.quality, q)
     assert np.array_equal(res.rolled_back, np.asarray(rb))
 
 
@@ -85,6 +85,20 @@ def test_pipeline_recovers_channel_16ant_m4n(gpu):
         # stops one iteration before the oracle in one of 26 stages); every other count is equal
         d = np.abs(res.stage_iters[b] - np.asarray(refs[b].stage_iters))
         assert d.max() <= 1 and (d > 0).sum() <= 1, (res.stage_iters[b], refs[b].stage_iters)
+
+
+def test_pipeline_32ant_primal_spectral(gpu):
+    """m_t = 1216 > n = 1024: SpectralInitialize through the n x n primal Gram (ace_spectral.hip
+    launch_spectral_primal) on a 60-iteration horizon, one restart.  This case is sensitive: the
+    oracle's own X moves 1.6e-7 and its quality 7e-9 under a 1e-15 relative change of B, and its
+    quality differs by 6e-8 between two hosts (the r = 20 spectral columns end in a cluster of
+    eigenvalues 0.3 % apart, and the stages stop at the 60-iteration cap).  X is held to the
+    north_star 1e-5, the quality to 2e-6."""
+    from ace_amd import infer_low_rank_pipeline_host
+    A, B, tr, refs = _live(53, 32, 1280, 1, 1, maxiter=60)
+    res = infer_low_rank_pipeline_host(A, B, 32, 32, tr, variant="A2only", maxiter=60)
+    _check(res, np.stack([r.X for r in refs]), [r.quality for r in refs], [r.stage_iters for r in refs],
+           [r.rolled_back for r in refs], qtol=2e-6)
 
 
 def test_pipeline_batch_invariance(gpu):

@@ -558,10 +558,11 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
     a.Kf = L.Kfr;
     a.B = B;
     a.M = w.M;
-    a.Zs = w.Sg[0];
-    a.Ns = w.Sg[1];
-    a.KZ = w.KY[0];
-    a.KN = w.KY[1];
+    double *Eb[2] = {w.Sg[0], w.Sg[1]}, *KEb[2] = {w.KY[0], w.KY[1]};   // e, K e ping-pong
+    a.Eo = Eb[0];
+    a.En = Eb[1];
+    a.KEo = KEb[0];
+    a.KEn = KEb[1];
     a.P0 = w.T;
     a.optW = w.optS;
     a.optY = w.optY;
@@ -579,6 +580,10 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
     for (; it <= p.maxiter; ++it) {
         a.Yo = w.Y[q];
         a.Yn = w.Y[1 - q];
+        a.Eo = Eb[q];
+        a.En = Eb[1 - q];
+        a.KEo = KEb[q];
+        a.KEn = KEb[1 - q];
         za.it = it;
         {
             ProfScope ps(ACE_K_APPLY_G, st);

@@ -77,7 +77,9 @@ struct RealState {
     int32_t msp, mzit, z0id, msp_pad;   // msp_pad: the entry iteration it0
     // A2nuclear m-space iteration (ace_nucmsp.hip): Z = na X_init + A^H zeta, N = nbeta X_init +
     // A^H nu; nx0 = ||X_init||^2; the X_init coefficients of the best / last iterate
-    double na, nbeta, nx0, nopt_a, ncur_a, npad_;
+    // A2nuclear m-space iteration (ace_nucmsp.hip): E_prev = na X_init + A^H e, Z = naz E_prev,
+    // N = nbeta E_prev, nep2 = ||E_prev||^2, nx0 = ||X_init||^2; best / current iterate's X_init coefficient
+    double na, nbeta, nx0, nopt_a, ncur_a, naz, nep2, npad2_;
 };
 static_assert(sizeof(RealState) % 16 == 0, "RealState alignment");
 
@@ -320,10 +322,10 @@ struct NmsArgs {
     const double* Yo;   // Y of the previous iterate (read)
     double* Yn;         // Y_new (written)
     double* M;
-    double* Zs;         // zeta: Z = na X_init + A^H zeta
-    double* Ns;         // nu:   N = nbeta X_init + A^H nu
-    double* KZ;         // K zeta
-    double* KN;         // K nu
+    double* Eo;         // e of E_prev = na X_init + A^H e (read)
+    double* En;         // e of E_new (written; Eo / En ping-pong)
+    double* KEo;        // K e (read)
+    double* KEn;        // K e_new (written)
     const double* P0;   // A X_init
     double* optW;       // best iterate X = nopt_a X_init + A^H optW
     double* optY;

@@ -2,34 +2,33 @@
 // (inferLowRank_Nuclear.m:269-383 with the Z-prox of :411-439).
 //
 // At r = 1 the nuclear Z-prox is a scaling, Z' = s E with s = max(0, ||E|| - 1/mu) / ||E||
-// (Shrink of the one singular value of the n x 1 iterate).  Every n-vector of the iteration then
-// stays in span{X_init} + range(A^H):
-//   init (:309): X = X_init, Z = s0 X_init (prox at mu = 1, N = 0), N = 0;
-//   V = Z - N/mu,  X = V + A^H g  (ArgMinX in Woodbury form, g = G T, G = (I + K)^-1, K = A A^H),
-//   E = X + N/mu = Z + A^H g,  Z' = s E,  N' = N + mu (X - Z')           (:325, :333, :341).
-// So Z = alpha X_init + A^H zeta and N = beta X_init + A^H nu with real scalars alpha, beta and
-// m-vectors zeta, nu, and the iteration needs only m-space quantities:
-//   A V    = (alpha - beta/mu) P0 + K zeta - K nu / mu        (P0 = A X_init, from the init)
-//   T      = (Y - M/mu) - A V,  g = G T,  K g = T - g         ((I + K) G = I: no second product)
-//   e      = zeta + g,  x = zeta - nu/mu + g,  a_x = alpha - beta/mu   (E = alpha X_init + A^H e,
-//            X = a_x X_init + A^H x)
-//   ||a X_init + A^H w||^2 = a^2 ||X_init||^2 + 2 a Re(P0^H w) + Re(w^H K w)
-//   zeta' = s e,  nu' = nu + mu (x - s e),  alpha' = s alpha,  beta' = beta + mu (a_x - s alpha),
-// with K zeta and K nu carried along by the same linear updates (K e = K zeta + K g, ...).  The
-// Y-step (:326-337) is the reference's, on AX = (Y - M/mu) - g.  The residual norms of the
-// convergence test (:364-370: ||X||, ||Z'||, ||X - Z'||, ||Z' - Z||) are quadratic forms of
-// these pairs, reduced per realisation in a fixed order; the dual terms ||A^H (Y - Y0)||^2 and
-// ||A^H Y||^2 are formed only when the test needs them (lazy dual residual),
-// here on the f64 matrix cores with K in fragment order.  The best iterate is kept as
-// (opt_a, opt_w); X = opt_a X_init + A^H opt_w is formed once after the loop.
+// (Shrink of the one singular value of the n x 1 iterate), E = X + N/mu.  Then
+//   N' = N + mu (X - Z') = mu (E - Z') = mu (1 - s) E,
+// so after every iteration Z and N are both multiples of the same n-vector E, which stays in
+// span{X_init} + range(A^H).  The state is E_prev = alpha X_init + A^H e (a real scalar and one
+// m-vector, with K e alongside) and the two multiples Z = a_z E_prev, N = a_n E_prev:
+//   init (:309): E_prev = X_init (alpha = 1, e = 0), a_z = the prox scale at mu = 1, a_n = 0;
+//   V = Z - N/mu = c_v E_prev (c_v = a_z - a_n/mu),  A V = c_v (alpha P0 + K e)   (P0 = A X_init)
+//   T = (Y - M/mu) - A V,  g = G T (ArgMinX in Woodbury form),  K g = T - g    ((I + K) G = I)
+//   X = c_v E_prev + A^H g,   E_new = X + N/mu = a_z E_prev + A^H g:
+//       e_new = a_z e + g,  K e_new = a_z K e + K g,  alpha_new = a_z alpha
+//   s = Shrink(||E_new||),  a_z' = s,  a_n' = mu (1 - s).
+// The norms of the convergence test (:364-370: ||X||, ||Z'||, ||X - Z'||, ||Z' - Z||) are
+// quadratic forms in ||E_prev||^2 (carried), <E_prev, A^H g> = Re((alpha P0 + K e)^H g) and
+// ||A^H g||^2 = Re(g^H K g), reduced per realisation in a fixed order.  The Y-step (:326-337) is
+// the reference's, on AX = (Y - M/mu) - g.  The dual terms ||A^H (Y - Y0)||^2 and ||A^H Y||^2 are
+// formed only when the test needs them (lazy dual residual), here on the f64
+// matrix cores with K in fragment order.  The best iterate is kept as (opt_a, opt_w) with
+// X = c_v alpha X_init + A^H (c_v e + g), materialised once after the loop.
 //
 // One launch per iteration and 16 realisations per 512-thread work-group, as gyk_kernel
 // (ace_i8gemm.hip): T in LDS, g = G T on v_mfma_f64_16x16x4_f64 (3M form, G streamed from L2 in
-// fragment order), then the Y-step and the m-space Z-step on each lane's 2 x 4 outputs.
-// Per realisation and iteration it moves Y, M, B, P0, zeta, nu, K zeta, K nu in and Y', M', zeta',
-// nu', K zeta', K nu' out (no n-vector at all) and runs 8 m^2 flops on the matrix cores.
-// In exact arithmetic this is the reference iteration; in floating point the products are formed
-// in another order (the nuclear refinement is rounding-chaotic beyond ~60 iterations: DESIGN §6).
+// fragment order), then the Y-step and the E update on each lane's 2 x 4 outputs; a second pass
+// only for realisations whose iterate is recorded.  Per realisation and iteration it moves Y, M,
+// B, P0, e, K e in and Y', M', e', K e' out (no n-vector at all) and runs 8 m^2 flops on the
+// matrix cores.  In exact arithmetic this is the reference iteration; in floating point the
+// products are formed in another order (the nuclear refinement is rounding-chaotic beyond ~60
+// iterations: DESIGN §6).
 #include "ace_common.hpp"
 #include "ace_zcommon.hpp"
 
@@ -109,7 +108,7 @@ __device__ __forceinline__ d2 frag_out(const d4v (&p1)[2], const d4v (&p2)[2], c
 }
 __device__ __forceinline__ double cdotr(d2 a, d2 b) { return a.x * b.x + a.y * b.y; }   // Re(conj(a) b)
 
-constexpr int NSUM = 13;   // Y-step: obj2 nAX2 nY2 nJM2 dY2; m-space: p_x p_e p_z q_xx q_ee q_zz q_xe q_ez
+constexpr int NSUM = 7;    // Y-step: obj2 nAX2 nY2 nJM2 dY2; m-space: <E_prev, A^H g>, ||A^H g||^2
 
 // FIN: only finish the convergence tests the last iteration left pending (no iteration).
 template <bool FIN>
@@ -117,7 +116,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ double red[8][GRB][NSUM];
     __shared__ int live_s[GRB], pend_s[GRB], imp_s[GRB], cur_s[GRB];
-    __shared__ double mu_s[GRB], al_s[GRB], be_s[GRB], s_s[GRB];
+    __shared__ double mu_s[GRB], al_s[GRB], az_s[GRB], an_s[GRB], s_s[GRB];
     const int mp = nms_mp(m), tst = mp + 1, nct = mp / 16;
     d2* Ts = reinterpret_cast<d2*>(smem);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB;
@@ -128,7 +127,8 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
         pend_s[t] = lv && a.rs[j].dpend;
         mu_s[t] = lv ? a.rs[j].mu : 1.0;
         al_s[t] = lv ? a.rs[j].na : 0.0;
-        be_s[t] = lv ? a.rs[j].nbeta : 0.0;
+        az_s[t] = lv ? a.rs[j].naz : 0.0;
+        an_s[t] = lv ? a.rs[j].nbeta : 0.0;
     }
     __syncthreads();
     // ---- pending convergence tests of the previous iteration: ||A^H Y_k||^2 = Y_k^H K Y_k and
@@ -178,18 +178,17 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     }
     if constexpr (FIN) return;
 
-    // ---- T = (Y - M/mu) - A V,  A V = (alpha - beta/mu) P0 + K zeta - K nu / mu
+    // ---- T = (Y - M/mu) - A V,  V = c_v E_prev,  A E_prev = alpha P0 + K e
     for (int idx = t; idx < GRB * tst; idx += NT) {
         const int jl = idx / tst, k = idx - jl * tst;
         d2 v = make_double2(0.0, 0.0);
         if (k < m && live_s[jl]) {
             const long long o = (long long)(j0 + jl) * m + k;
-            const double imu = 1.0 / mu_s[jl], av = al_s[jl] - be_s[jl] * imu;
+            const double imu = 1.0 / mu_s[jl], cv = az_s[jl] - an_s[jl] * imu, al = al_s[jl];
             const d2 y = reinterpret_cast<const d2*>(a.Yo)[o], mm = reinterpret_cast<const d2*>(a.M)[o];
-            const d2 p0 = reinterpret_cast<const d2*>(a.P0)[o], kz = reinterpret_cast<const d2*>(a.KZ)[o],
-                     kn = reinterpret_cast<const d2*>(a.KN)[o];
-            const d2 avv = make_double2(fma(av, p0.x, fma(-kn.x, imu, kz.x)), fma(av, p0.y, fma(-kn.y, imu, kz.y)));
-            v = make_double2(fma(-mm.x, imu, y.x) - avv.x, fma(-mm.y, imu, y.y) - avv.y);
+            const d2 p0 = reinterpret_cast<const d2*>(a.P0)[o], ke = reinterpret_cast<const d2*>(a.KEo)[o];
+            const d2 aep = make_double2(fma(al, p0.x, ke.x), fma(al, p0.y, ke.y));
+            v = make_double2(fma(-mm.x, imu, y.x) - cv * aep.x, fma(-mm.y, imu, y.y) - cv * aep.y);
         }
         Ts[idx] = v;
     }
@@ -198,7 +197,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     d4v p1[2], p2[2], p3[2];
     frag_mv(reinterpret_cast<const d2*>(a.Gf), Ts, tst, mp, lane, w, p1, p2, p3);
 
-    // ---- pass 1: the Y-step and the m-space sums on the lane's 2 x 4 outputs
+    // ---- pass 1: the Y-step, E_new = a_z E_prev + A^H g as (e_new, K e_new), and the sums
     double v[4][NSUM];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -213,7 +212,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             if (ct >= nct || i >= m || !live_s[jl]) continue;
             const long long off = (long long)(j0 + jl) * m + i;
             const d2 gv = frag_out(p1, p2, p3, c, r), tv = Ts[jl * tst + i];
-            const double mu = mu_s[jl], imu = 1.0 / mu;
+            const double mu = mu_s[jl], imu = 1.0 / mu, az = az_s[jl], al = al_s[jl];
             const d2 mii = reinterpret_cast<const d2*>(a.M)[off], yo = reinterpret_cast<const d2*>(a.Yo)[off];
             const double Bi = a.B[off];
             // Y-step (:326-337), the reference's expressions
@@ -235,22 +234,15 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             v[r][2] += cabs2(y);
             v[r][3] += cabs2(jv);
             v[r][4] += cabs2(csub(y, yo));
-            // m-space Z-step operands
-            const d2 z = reinterpret_cast<const d2*>(a.Zs)[off], nu = reinterpret_cast<const d2*>(a.Ns)[off];
-            const d2 kz = reinterpret_cast<const d2*>(a.KZ)[off], kn = reinterpret_cast<const d2*>(a.KN)[off];
+            // E_new = a_z E_prev + A^H g:  e_new = a_z e + g,  K e_new = a_z K e + (T - g)
+            const d2 e = reinterpret_cast<const d2*>(a.Eo)[off], ke = reinterpret_cast<const d2*>(a.KEo)[off];
             const d2 p0 = reinterpret_cast<const d2*>(a.P0)[off];
             const d2 kg = csub(tv, gv);
-            const d2 e = cadd(z, gv), ke = cadd(kz, kg);
-            const d2 x = make_double2(fma(-nu.x, imu, z.x) + gv.x, fma(-nu.y, imu, z.y) + gv.y);
-            const d2 kx = make_double2(fma(-kn.x, imu, kz.x) + kg.x, fma(-kn.y, imu, kz.y) + kg.y);
-            v[r][5] += cdotr(p0, x);
-            v[r][6] += cdotr(p0, e);
-            v[r][7] += cdotr(p0, z);
-            v[r][8] += cdotr(x, kx);
-            v[r][9] += cdotr(e, ke);
-            v[r][10] += cdotr(z, kz);
-            v[r][11] += cdotr(x, ke);
-            v[r][12] += cdotr(e, kz);
+            reinterpret_cast<d2*>(a.En)[off] = make_double2(fma(az, e.x, gv.x), fma(az, e.y, gv.y));
+            reinterpret_cast<d2*>(a.KEn)[off] = make_double2(fma(az, ke.x, kg.x), fma(az, ke.y, kg.y));
+            const d2 aep = make_double2(fma(al, p0.x, ke.x), fma(al, p0.y, ke.y));
+            v[r][5] += cdotr(aep, gv);   // <E_prev, A^H g> = Re((A E_prev)^H g)
+            v[r][6] += cdotr(gv, kg);    // ||A^H g||^2 = Re(g^H K g)
         }
     }
 #pragma unroll
@@ -267,7 +259,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     // ---- the Z-step of each realisation on one thread: prox, residual norms, control
     if (t < GRB) {
         int imp = 0, cur = 0;
-        double s = 0.0;
+        double cvo = 0.0;
         if (live_s[t]) {
             double q[NSUM];
 #pragma unroll
@@ -281,56 +273,50 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             rs.nY2 = q[2];
             rs.nJM2 = q[3];
             rs.dY2 = q[4];
-            const double mu = mu_s[t], imu = 1.0 / mu, x0n = rs.nx0, al = al_s[t], be = be_s[t];
-            const double px = q[5], pe = q[6], pz = q[7], qxx = q[8], qee = q[9], qzz = q[10], qxe = q[11], qez = q[12];
-            const double ax_ = al - be * imu;                                     // X's X_init coefficient
-            const double nE = sqrt(fmax(0.0, al * al * x0n + 2.0 * al * pe + qee));   // ||E||, E = alpha X_init + A^H e
-            s = nE > 0.0 ? fmax(0.0, nE - imu) / nE : 0.0;                         // Shrink (:421-439)
-            const double nX2 = fmax(0.0, ax_ * ax_ * x0n + 2.0 * ax_ * px + qxx);
-            const double nZ2 = s * s * nE * nE;
-            const double ua = ax_ - s * al;                                        // X - Z'
-            const double jn2 = fmax(0.0, ua * ua * x0n + 2.0 * ua * (px - s * pe) + qxx - 2.0 * s * qxe + s * s * qee);
-            const double wa = (s - 1.0) * al;                                      // Z' - Z
-            const double dZ2 = fmax(0.0, wa * wa * x0n + 2.0 * wa * (s * pe - pz) + s * s * qee - 2.0 * s * qez + qzz);
+            const double mu = mu_s[t], imu = 1.0 / mu, az = az_s[t], al = al_s[t];
+            const double cv = az - an_s[t] * imu;        // V = Z - N/mu = c_v E_prev
+            const double ne = rs.nep2, hp = q[5], hh = fmax(0.0, q[6]);
+            // X = c_v E_prev + A^H g,  E = X + N/mu = a_z E_prev + A^H g,  Z' = s E (Shrink, :421-439)
+            const double nE2 = fmax(0.0, az * az * ne + 2.0 * az * hp + hh);
+            const double nE = sqrt(nE2);
+            const double s = nE > 0.0 ? fmax(0.0, nE - imu) / nE : 0.0;
+            const double nX2 = fmax(0.0, cv * cv * ne + 2.0 * cv * hp + hh);
+            const double nZ2 = s * s * nE2;
+            const double u = cv - s * az, u1 = 1.0 - s;   // X - Z' = u E_prev + (1 - s) A^H g
+            const double jn2 = fmax(0.0, u * u * ne + 2.0 * u * u1 * hp + u1 * u1 * hh);
+            const double wz = az * (s - 1.0);              // Z' - Z = wz E_prev + s A^H g
+            const double dZ2 = fmax(0.0, wz * wz * ne + 2.0 * wz * s * hp + s * s * hh);
             const int ctl = iter_control_in(za, &rs, iter_in(&rs), mu, nX2, nZ2, jn2, dZ2, 0.0, 0.0);
             imp = ctl & 1;
-            rs.na = s * al;
-            rs.nbeta = be + mu * ua;
-            if (imp) rs.nopt_a = ax_;
+            // Z' = s E_new, N' = N + mu (X - Z') = mu (1 - s) E_new  (E_new's X_init coefficient a_z alpha)
+            rs.na = az * al;
+            rs.naz = s;
+            rs.nbeta = mu * (1.0 - s);
+            rs.nep2 = nE2;
+            if (imp) rs.nopt_a = cv * al;
             // the last iterate stands in for opt_X while no objective was finite (finalize's fallback)
             cur = !(rs.opt_obj < INFINITY);
-            if (cur) rs.ncur_a = ax_;
+            if (cur) rs.ncur_a = cv * al;
+            cvo = cv;
         }
         imp_s[t] = imp;
         cur_s[t] = cur;
-        s_s[t] = s;
+        s_s[t] = cvo;
     }
     __syncthreads();
-    // ---- pass 2: zeta' = s e, nu' = nu + mu (x - s e), K zeta', K nu'; opt_w / opt_Y
+    // ---- pass 2 (realisations whose iterate is recorded): X's m-part c_v e + g, opt_Y
+    if (!__syncthreads_or(t < GRB && (imp_s[t] || cur_s[t]))) return;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int ct = 2 * w + c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int jl = (lane >> 4) + 4 * r, i = 16 * ct + (lane & 15);
-            if (ct >= nct || i >= m || !live_s[jl]) continue;
+            if (ct >= nct || i >= m || !live_s[jl] || !(imp_s[jl] || cur_s[jl])) continue;
             const long long off = (long long)(j0 + jl) * m + i;
-            const d2 gv = frag_out(p1, p2, p3, c, r), tv = Ts[jl * tst + i];
-            const double mu = mu_s[jl], imu = 1.0 / mu, s = s_s[jl];
-            d2* zp = reinterpret_cast<d2*>(a.Zs) + off;
-            d2* np = reinterpret_cast<d2*>(a.Ns) + off;
-            d2* kzp = reinterpret_cast<d2*>(a.KZ) + off;
-            d2* knp = reinterpret_cast<d2*>(a.KN) + off;
-            const d2 z = *zp, nu = *np, kz = *kzp, kn = *knp;
-            const d2 kg = csub(tv, gv);
-            const d2 e = cadd(z, gv), ke = cadd(kz, kg);
-            const d2 x = make_double2(fma(-nu.x, imu, z.x) + gv.x, fma(-nu.y, imu, z.y) + gv.y);
-            const d2 kx = make_double2(fma(-kn.x, imu, kz.x) + kg.x, fma(-kn.y, imu, kz.y) + kg.y);
-            const d2 se = cscale(e, s), ske = cscale(ke, s);
-            *zp = se;
-            *kzp = ske;
-            *np = cadd(nu, cscale(csub(x, se), mu));
-            *knp = cadd(kn, cscale(csub(kx, ske), mu));
+            const d2 gv = frag_out(p1, p2, p3, c, r), e = reinterpret_cast<const d2*>(a.Eo)[off];
+            const double cv = s_s[jl];
+            const d2 x = make_double2(fma(cv, e.x, gv.x), fma(cv, e.y, gv.y));
             if (imp_s[jl]) {
                 reinterpret_cast<d2*>(a.optW)[off] = x;
                 reinterpret_cast<d2*>(a.optY)[off] = reinterpret_cast<const d2*>(a.Yn)[off];
@@ -340,8 +326,8 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     }
 }
 
-// P0 = A X_init is formed by the caller; here ||X_init||^2, alpha_0 = the prox scale at mu = 1
-// (:309, Z = ArgMinZ(X, 0, 1)), beta_0 = 0 and zeta = nu = K zeta = K nu = 0.
+// P0 = A X_init is formed by the caller; here E_prev = X_init (alpha = 1, e = K e = 0), Z = a_z E_prev
+// with a_z the prox scale at mu = 1 (:309, Z = ArgMinZ(X, 0, 1)), N = 0 (a_n = 0), ||E_prev||^2.
 __global__ __launch_bounds__(256) void nms_init_kernel(int n, int m, const double* __restrict__ Xi, NmsArgs a) {
     __shared__ double red[16];
     const int b = blockIdx.x;
@@ -352,16 +338,16 @@ __global__ __launch_bounds__(256) void nms_init_kernel(int n, int m, const doubl
     const long long o = (long long)b * m;
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const d2 z = make_double2(0.0, 0.0);
-        reinterpret_cast<d2*>(a.Zs)[o + i] = z;
-        reinterpret_cast<d2*>(a.Ns)[o + i] = z;
-        reinterpret_cast<d2*>(a.KZ)[o + i] = z;
-        reinterpret_cast<d2*>(a.KN)[o + i] = z;
+        reinterpret_cast<d2*>(a.Eo)[o + i] = z;
+        reinterpret_cast<d2*>(a.KEo)[o + i] = z;
     }
     if (threadIdx.x == 0) {
         RealState& rs = a.rs[b];
         const double nz = sqrt(s[0]);
         rs.nx0 = s[0];
-        rs.na = nz > 0.0 ? fmax(0.0, nz - 1.0) / nz : 0.0;
+        rs.nep2 = s[0];
+        rs.na = 1.0;
+        rs.naz = nz > 0.0 ? fmax(0.0, nz - 1.0) / nz : 0.0;
         rs.nbeta = 0.0;
         rs.nopt_a = 0.0;
         rs.ncur_a = 0.0;

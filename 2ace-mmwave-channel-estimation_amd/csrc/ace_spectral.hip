@@ -20,7 +20,8 @@
 //                    solves), one thread per eigenvalue cluster (relative separation
 //                    < 1e-3, as dstein) with the cluster's earlier vectors projected out
 //   backxf_kernel    one work-group per realisation: u_k = H_0 H_1 ... H_{m_t-2} z_k,
-//                    W_k = D u_k
+//                    W_k = D u_k  (few vectors; PhaseLift's prox, which keeps 100-256 of 256,
+//                    takes the compact-WY blocked back-transform on the MFMA GEMM instead)
 //
 // X = A_t^H W is then one MFMA GEMM over batch*r vectors (ace_pipeline.cpp).
 // Realisations are processed in chunks so the C matrices of a chunk stay in the L2/MALL.
@@ -321,67 +322,90 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         const int q0 = (int)cl[c], q1 = (int)cl[c + 1];
         for (int q = q0; q < q1; ++q) {
             const double lq = lam[q];
-            for (int i = 0; i < mt; ++i) {
-                at(0, i) = e[i];
-                at(1, i) = d[i] - lq;
-                at(2, i) = e[i];
-                at(3, i) = 0.0;
-                at(4, i) = 0.0;
-                at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * q);  // start vector
-            }
-            for (int i = 0; i + 1 < mt; ++i) {  // dgttrf
-                const double di = at(1, i), dli = at(0, i);
-                if (fabs(di) >= fabs(dli)) {
-                    if (di != 0.0) {
-                        const double f = dli / di;
-                        at(0, i) = f;
-                        at(1, i + 1) -= f * at(2, i);
+            // dgttrf on T - lq I with the running diagonal / superdiagonal entries carried in
+            // registers (every entry is final once its row is passed; the near-zero pivot guard of
+            // dlagts is applied as the diagonal entry is stored)
+            double cur_d = d[0] - lq, cur_du = e[0];
+            for (int i = 0; i + 1 < mt; ++i) {
+                const double dli = e[i], nd = d[i + 1] - lq, ndu = e[i + 1];
+                double f = dli, u1 = cur_d, u2 = cur_du, u3 = 0.0, piv = 0.0;
+                if (fabs(cur_d) >= fabs(dli)) {
+                    if (cur_d != 0.0) {
+                        f = dli / cur_d;
+                        cur_d = nd - f * cur_du;
+                    } else {
+                        cur_d = nd;
                     }
+                    cur_du = ndu;
                 } else {
-                    const double f = di / dli;
-                    at(1, i) = dli;
-                    at(0, i) = f;
-                    const double tmp = at(2, i);
-                    at(2, i) = at(1, i + 1);
-                    at(1, i + 1) = tmp - f * at(1, i + 1);
+                    f = cur_d / dli;
+                    u1 = dli;
+                    u2 = nd;
+                    cur_d = cur_du - f * nd;
                     if (i + 2 < mt) {
-                        at(3, i) = at(2, i + 1);
-                        at(2, i + 1) = -f * at(2, i + 1);
+                        u3 = ndu;
+                        cur_du = -f * ndu;
+                    } else {
+                        cur_du = ndu;
                     }
-                    at(4, i) = 1.0;
+                    piv = 1.0;
                 }
+                at(0, i) = f;
+                at(1, i) = fabs(u1) < tiny ? (u1 < 0.0 ? -tiny : tiny) : u1;
+                at(2, i) = u2;
+                at(3, i) = u3;
+                at(4, i) = piv;
             }
-            for (int i = 0; i < mt; ++i) {
-                const double di = at(1, i);
-                if (fabs(di) < tiny) at(1, i) = di < 0.0 ? -tiny : tiny;
-            }
+            at(1, mt - 1) = fabs(cur_d) < tiny ? (cur_d < 0.0 ? -tiny : tiny) : cur_d;
+            at(2, mt - 1) = cur_du;
+            at(3, mt - 1) = 0.0;
+            at(4, mt - 1) = 0.0;
+            for (int i = 0; i < mt; ++i) at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * q);  // start vector
             double* zq = Z + (long long)q * mt;
             for (int sweep = 0; sweep < 3; ++sweep) {
-                for (int i = 0; i + 1 < mt; ++i) {  // dgttrs
+                double cur = at(5, 0);
+                for (int i = 0; i + 1 < mt; ++i) {  // dgttrs, L
+                    const double nxt = at(5, i + 1), f = at(0, i);
                     if (at(4, i) == 0.0) {
-                        at(5, i + 1) -= at(0, i) * at(5, i);
+                        at(5, i) = cur;
+                        cur = nxt - f * cur;
                     } else {
-                        const double tb = at(5, i);
-                        at(5, i) = at(5, i + 1);
-                        at(5, i + 1) = tb - at(0, i) * at(5, i);
+                        at(5, i) = nxt;
+                        cur = cur - f * nxt;
                     }
                 }
-                at(5, mt - 1) /= at(1, mt - 1);
-                if (mt > 1) at(5, mt - 2) = (at(5, mt - 2) - at(2, mt - 2) * at(5, mt - 1)) / at(1, mt - 2);
-                for (int i = mt - 3; i >= 0; --i)
-                    at(5, i) = (at(5, i) - at(2, i) * at(5, i + 1) - at(3, i) * at(5, i + 2)) / at(1, i);
-                for (int p = q0; p < q; ++p) {  // project out the cluster's earlier vectors
-                    const double* zp = Z + (long long)p * mt;
-                    double s = 0.0;
-                    for (int i = 0; i < mt; ++i) s += zp[i] * at(5, i);
-                    for (int i = 0; i < mt; ++i) at(5, i) -= s * zp[i];
+                // U back substitution, y_{i+1} and y_{i+2} carried in registers
+                double y2 = cur / at(1, mt - 1), y1 = y2;
+                double nrm = y2 * y2;
+                at(5, mt - 1) = y2;
+                if (mt > 1) {
+                    y1 = (at(5, mt - 2) - at(2, mt - 2) * y2) / at(1, mt - 2);
+                    at(5, mt - 2) = y1;
+                    nrm += y1 * y1;
                 }
-                double nrm = 0.0;
-                for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
+                for (int i = mt - 3; i >= 0; --i) {
+                    const double y = (at(5, i) - at(2, i) * y1 - at(3, i) * y2) / at(1, i);
+                    at(5, i) = y;
+                    nrm += y * y;
+                    y2 = y1;
+                    y1 = y;
+                }
+                if (q > q0) {   // project out the cluster's earlier vectors
+                    for (int p = q0; p < q; ++p) {
+                        const double* zp = Z + (long long)p * mt;
+                        double sp = 0.0;
+                        for (int i = 0; i < mt; ++i) sp += zp[i] * at(5, i);
+                        for (int i = 0; i < mt; ++i) at(5, i) -= sp * zp[i];
+                    }
+                    nrm = 0.0;
+                    for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
+                }
                 const double inv = 1.0 / sqrt(nrm);
-                for (int i = 0; i < mt; ++i) at(5, i) *= inv;
+                if (sweep < 2)
+                    for (int i = 0; i < mt; ++i) at(5, i) *= inv;
+                else
+                    for (int i = 0; i < mt; ++i) zq[i] = at(5, i) * inv;
             }
-            for (int i = 0; i < mt; ++i) zq[i] = at(5, i);
         }
     }
     if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);

@@ -558,11 +558,11 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
     a.Kf = L.Kfr;
     a.B = B;
     a.M = w.M;
-    double *Eb[2] = {w.Sg[0], w.Sg[1]}, *KEb[2] = {w.KY[0], w.KY[1]};   // e, K e ping-pong
+    double *Eb[2] = {w.Sg[0], w.Sg[1]}, *AEb[2] = {w.KY[0], w.KY[1]};   // e, A E ping-pong
     a.Eo = Eb[0];
     a.En = Eb[1];
-    a.KEo = KEb[0];
-    a.KEn = KEb[1];
+    a.AEo = AEb[0];
+    a.AEn = AEb[1];
     a.P0 = w.T;
     a.optW = w.optS;
     a.optY = w.optY;
@@ -582,8 +582,8 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
         a.Yn = w.Y[1 - q];
         a.Eo = Eb[q];
         a.En = Eb[1 - q];
-        a.KEo = KEb[q];
-        a.KEn = KEb[1 - q];
+        a.AEo = AEb[q];
+        a.AEn = AEb[1 - q];
         za.it = it;
         {
             ProfScope ps(ACE_K_APPLY_G, st);

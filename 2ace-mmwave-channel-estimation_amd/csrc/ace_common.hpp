@@ -324,9 +324,9 @@ struct NmsArgs {
     double* M;
     double* Eo;         // e of E_prev = na X_init + A^H e (read)
     double* En;         // e of E_new (written; Eo / En ping-pong)
-    double* KEo;        // K e (read)
-    double* KEn;        // K e_new (written)
-    const double* P0;   // A X_init
+    double* AEo;        // A E_prev (read)
+    double* AEn;        // A E_new (written)
+    const double* P0;   // A X_init (init only)
     double* optW;       // best iterate X = nopt_a X_init + A^H optW
     double* optY;
     double* curW;       // the last iterate's m-part while no objective was finite

@@ -6,15 +6,15 @@
 //   N' = N + mu (X - Z') = mu (E - Z') = mu (1 - s) E,
 // so after every iteration Z and N are both multiples of the same n-vector E, which stays in
 // span{X_init} + range(A^H).  The state is E_prev = alpha X_init + A^H e (a real scalar and one
-// m-vector, with K e alongside) and the two multiples Z = a_z E_prev, N = a_n E_prev:
+// m-vector e) with its image A E_prev, and the two multiples Z = a_z E_prev, N = a_n E_prev:
 //   init (:309): E_prev = X_init (alpha = 1, e = 0), a_z = the prox scale at mu = 1, a_n = 0;
-//   V = Z - N/mu = c_v E_prev (c_v = a_z - a_n/mu),  A V = c_v (alpha P0 + K e)   (P0 = A X_init)
+//   V = Z - N/mu = c_v E_prev (c_v = a_z - a_n/mu),  A V = c_v A E_prev   (A E_0 = P0 = A X_init)
 //   T = (Y - M/mu) - A V,  g = G T (ArgMinX in Woodbury form),  K g = T - g    ((I + K) G = I)
 //   X = c_v E_prev + A^H g,   E_new = X + N/mu = a_z E_prev + A^H g:
-//       e_new = a_z e + g,  K e_new = a_z K e + K g,  alpha_new = a_z alpha
+//       e_new = a_z e + g,  A E_new = a_z A E_prev + K g,  alpha_new = a_z alpha
 //   s = Shrink(||E_new||),  a_z' = s,  a_n' = mu (1 - s).
 // The norms of the convergence test (:364-370: ||X||, ||Z'||, ||X - Z'||, ||Z' - Z||) are
-// quadratic forms in ||E_prev||^2 (carried), <E_prev, A^H g> = Re((alpha P0 + K e)^H g) and
+// quadratic forms in ||E_prev||^2 (carried), <E_prev, A^H g> = Re((A E_prev)^H g) and
 // ||A^H g||^2 = Re(g^H K g), reduced per realisation in a fixed order.  The Y-step (:326-337) is
 // the reference's, on AX = (Y - M/mu) - g.  The dual terms ||A^H (Y - Y0)||^2 and ||A^H Y||^2 are
 // formed only when the test needs them (lazy dual residual), here on the f64
@@ -25,7 +25,7 @@
 // (ace_i8gemm.hip): T in LDS, g = G T on v_mfma_f64_16x16x4_f64 (3M form, G streamed from L2 in
 // fragment order), then the Y-step and the E update on each lane's 2 x 4 outputs; a second pass
 // only for realisations whose iterate is recorded.  Per realisation and iteration it moves Y, M,
-// B, P0, e, K e in and Y', M', e', K e' out (no n-vector at all) and runs 8 m^2 flops on the
+// B, e, A E in and Y', M', e', A E' out (no n-vector at all) and runs 8 m^2 flops on the
 // matrix cores.  In exact arithmetic this is the reference iteration; in floating point the
 // products are formed in another order (the nuclear refinement is rounding-chaotic beyond ~60
 // iterations: DESIGN §6).
@@ -178,16 +178,15 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     }
     if constexpr (FIN) return;
 
-    // ---- T = (Y - M/mu) - A V,  V = c_v E_prev,  A E_prev = alpha P0 + K e
+    // ---- T = (Y - M/mu) - A V,  V = c_v E_prev
     for (int idx = t; idx < GRB * tst; idx += NT) {
         const int jl = idx / tst, k = idx - jl * tst;
         d2 v = make_double2(0.0, 0.0);
         if (k < m && live_s[jl]) {
             const long long o = (long long)(j0 + jl) * m + k;
-            const double imu = 1.0 / mu_s[jl], cv = az_s[jl] - an_s[jl] * imu, al = al_s[jl];
+            const double imu = 1.0 / mu_s[jl], cv = az_s[jl] - an_s[jl] * imu;
             const d2 y = reinterpret_cast<const d2*>(a.Yo)[o], mm = reinterpret_cast<const d2*>(a.M)[o];
-            const d2 p0 = reinterpret_cast<const d2*>(a.P0)[o], ke = reinterpret_cast<const d2*>(a.KEo)[o];
-            const d2 aep = make_double2(fma(al, p0.x, ke.x), fma(al, p0.y, ke.y));
+            const d2 aep = reinterpret_cast<const d2*>(a.AEo)[o];
             v = make_double2(fma(-mm.x, imu, y.x) - cv * aep.x, fma(-mm.y, imu, y.y) - cv * aep.y);
         }
         Ts[idx] = v;
@@ -212,7 +211,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             if (ct >= nct || i >= m || !live_s[jl]) continue;
             const long long off = (long long)(j0 + jl) * m + i;
             const d2 gv = frag_out(p1, p2, p3, c, r), tv = Ts[jl * tst + i];
-            const double mu = mu_s[jl], imu = 1.0 / mu, az = az_s[jl], al = al_s[jl];
+            const double mu = mu_s[jl], imu = 1.0 / mu, az = az_s[jl];
             const d2 mii = reinterpret_cast<const d2*>(a.M)[off], yo = reinterpret_cast<const d2*>(a.Yo)[off];
             const double Bi = a.B[off];
             // Y-step (:326-337), the reference's expressions
@@ -234,13 +233,11 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             v[r][2] += cabs2(y);
             v[r][3] += cabs2(jv);
             v[r][4] += cabs2(csub(y, yo));
-            // E_new = a_z E_prev + A^H g:  e_new = a_z e + g,  K e_new = a_z K e + (T - g)
-            const d2 e = reinterpret_cast<const d2*>(a.Eo)[off], ke = reinterpret_cast<const d2*>(a.KEo)[off];
-            const d2 p0 = reinterpret_cast<const d2*>(a.P0)[off];
+            // E_new = a_z E_prev + A^H g:  e_new = a_z e + g,  A E_new = a_z A E_prev + K g,  K g = T - g
+            const d2 e = reinterpret_cast<const d2*>(a.Eo)[off], aep = reinterpret_cast<const d2*>(a.AEo)[off];
             const d2 kg = csub(tv, gv);
             reinterpret_cast<d2*>(a.En)[off] = make_double2(fma(az, e.x, gv.x), fma(az, e.y, gv.y));
-            reinterpret_cast<d2*>(a.KEn)[off] = make_double2(fma(az, ke.x, kg.x), fma(az, ke.y, kg.y));
-            const d2 aep = make_double2(fma(al, p0.x, ke.x), fma(al, p0.y, ke.y));
+            reinterpret_cast<d2*>(a.AEn)[off] = make_double2(fma(az, aep.x, kg.x), fma(az, aep.y, kg.y));
             v[r][5] += cdotr(aep, gv);   // <E_prev, A^H g> = Re((A E_prev)^H g)
             v[r][6] += cdotr(gv, kg);    // ||A^H g||^2 = Re(g^H K g)
         }
@@ -326,7 +323,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     }
 }
 
-// P0 = A X_init is formed by the caller; here E_prev = X_init (alpha = 1, e = K e = 0), Z = a_z E_prev
+// P0 = A X_init is formed by the caller; here E_prev = X_init (alpha = 1, e = 0, A E_prev = P0), Z = a_z E_prev
 // with a_z the prox scale at mu = 1 (:309, Z = ArgMinZ(X, 0, 1)), N = 0 (a_n = 0), ||E_prev||^2.
 __global__ __launch_bounds__(256) void nms_init_kernel(int n, int m, const double* __restrict__ Xi, NmsArgs a) {
     __shared__ double red[16];
@@ -337,9 +334,8 @@ __global__ __launch_bounds__(256) void nms_init_kernel(int n, int m, const doubl
     block_sum<1>(s, red);
     const long long o = (long long)b * m;
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
-        const d2 z = make_double2(0.0, 0.0);
-        reinterpret_cast<d2*>(a.Eo)[o + i] = z;
-        reinterpret_cast<d2*>(a.KEo)[o + i] = z;
+        reinterpret_cast<d2*>(a.Eo)[o + i] = make_double2(0.0, 0.0);
+        reinterpret_cast<d2*>(a.AEo)[o + i] = reinterpret_cast<const d2*>(a.P0)[o + i];   // A E_prev = A X_init
     }
     if (threadIdx.x == 0) {
         RealState& rs = a.rs[b];

@@ -148,11 +148,11 @@ def nuclear_bytes(m, n):
 
 def nms_bytes(m):
     """A2nuclear at r = 1 in m-space (ace_nucmsp.hip::nms_kernel, one launch per iteration).  Z and N
-    are both multiples of E_prev = alpha X_init + A^H e, so the state is one m-vector pair (e, K e)
-    and no n-vector moves.  Per realisation and iteration: read Y, M, P0 = A X_init, e, K e (c128)
-    and B (f64); write Y_new, M, e_new, K e_new (opt_w / opt_Y on an improved objective are
+    are both multiples of E_prev = alpha X_init + A^H e, so the state is one m-vector e and the
+    image A E_prev; no n-vector moves.  Per realisation and iteration: read Y, M, e, A E (c128) and
+    B (f64); write Y_new, M, e_new, A E_new (opt_w / opt_Y on an improved objective are
     bookkeeping copies, not counted)."""
-    return 16.0 * 9 * m + 8.0 * m
+    return 16.0 * 8 * m + 8.0 * m
 
 
 def private_bytes(m, n):

@@ -102,8 +102,8 @@ def test_pmc_traffic_is_keyed_by_workload(tmp_path, monkeypatch):
 def test_nms_bytes():
     b = _bench()
     m = 256
-    # read Y, M, P0, e, K e (c128) and B (f64); write Y, M, e, K e
-    assert b.nms_bytes(m) == 16 * 9 * m + 8 * m
+    # read Y, M, e, A E (c128) and B (f64); write Y, M, e, A E
+    assert b.nms_bytes(m) == 16 * 8 * m + 8 * m
     r = b.unit_resources("apply_G", m, 1024, variant="A2nuclear", pc=False, gyf=False, gyk=True, i8=True,
                          msp_frac=0.0, nms=True)
     assert r == {"f64": 8 * m * m, "hbm": b.nms_bytes(m)}

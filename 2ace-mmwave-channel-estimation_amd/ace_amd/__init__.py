@@ -11,7 +11,7 @@ from .solver import (InferADMM, infer_admm_batch, infer_admm_host, synth_problem
 from ._lib import path_counts  # noqa: F401
 from .pipeline import (inferLowRankV4_multi, inferLowRankV4, inferLowRank_Nuclear,  # noqa: F401
                        infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, draw_partitions,
-                       PipelineResult)
+                       PipelineResult, SpectralInitialize)
 from .phaselift import MyPhaseLift, phaselift_host, phaselift_batch, PhaseLiftResult  # noqa: F401
 from .beamformer import (svd_beamformer, svd_beamformer_compensation, codebook_beams,  # noqa: F401
                          svd_beamformer_host, svd_beamformer_batch, BeamResult)

@@ -118,6 +118,8 @@ def _load():
     lib.ace_prof_work.restype = C.c_int
     lib.ace_nuclear_prox_batch.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]
     lib.ace_nuclear_prox_batch.restype = C.c_int
+    lib.ace_spectral_init_host.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]
+    lib.ace_spectral_init_host.restype = C.c_int
     lib.ace_path_counts.argtypes = [C.POINTER(C.c_int64), C.c_int]
     lib.ace_path_counts.restype = C.c_int
     lib.ace_last_error.argtypes = []

@@ -190,3 +190,25 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
                                        out.Y.data_ptr(), out.quality.data_ptr(), out.stage_iters.data_ptr(),
                                        out.status.data_ptr(), ws.data_ptr(), ws.numel(), stream.cuda_stream))
     return out
+
+
+def SpectralInitialize(A, B, r):
+    """X = SpectralInitialize(A, B, r) (inferLowRankV4_multi.m:561-574) on the GPU, the kernels of
+    the pipeline's own initialisation.  A: [m, n] complex; B: [m] or [batch, m] magnitudes.
+    Returns [n, r] (or [batch, n, r]) complex128: column k = sqrt(s_k) v_k, eigenvectors up to a
+    unit phase each."""
+    A = np.ascontiguousarray(A, dtype=np.complex128)
+    B = np.asarray(B, dtype=np.float64)
+    single = B.ndim == 1
+    Bb = np.ascontiguousarray(B[None, :] if single else B)
+    m, n = A.shape
+    batch = Bb.shape[0]
+    if Bb.shape[1] != m:
+        raise ValueError("B must have m entries per realisation")
+    X = np.empty((batch, r, n), np.complex128)
+    st = np.zeros(batch, np.uint32)
+    check(LIB.ace_spectral_init_host(batch, m, n, int(r), A.ctypes.data, Bb.ctypes.data, X.ctypes.data,
+                                     st.ctypes.data))
+    X = np.transpose(X, (0, 2, 1))
+    return X[0] if single else X
+

@@ -145,6 +145,61 @@ int run_impl(const PipeDims& d, PipeWs& w, const AdmmParams& base, int nb, const
 
 extern "C" {
 
+int ace_spectral_init_host(int batch, int m, int n, int r, const double* A, const double* B, double* X,
+                           uint32_t* status) {
+    g_err.clear();
+    if (!A || !B || !X) return fail(ACE_ERR_ARG, "NULL buffer");
+    if (batch < 1 || m < 1 || n < 1 || r < 1) return fail(ACE_ERR_ARG, "batch/m/n/r must be >= 1");
+    if (r > 32 || r > m || r > n) return fail(ACE_ERR_UNSUPPORTED, "r must be <= min(32, m, n) (got %d)", r);
+    if (std::min(m, n) > 1600) return fail(ACE_ERR_UNSUPPORTED, "min(m, n) = %d > 1600 (LDS limit)", std::min(m, n));
+    const bool primal = spectral_primal(m, n);
+    const size_t nA = 16 * (size_t)m * n, nK = 16 * (size_t)m * m, nB = 8 * (size_t)batch * m,
+                 nW = 16 * (size_t)batch * r * m, nX = 16 * (size_t)batch * r * n,
+                 nS = spectral_scratch_bytes(m, n, batch, r);
+    std::vector<void*> bufs;
+    struct Free {
+        std::vector<void*>& b;
+        hipStream_t st = nullptr;
+        ~Free() {
+            if (st) {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
+            for (void* p : b) (void)hipFree(p);
+        }
+    } guard{bufs};
+    auto dalloc = [&](size_t bytes) -> double* {
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return static_cast<double*>(p);
+    };
+    double *dA = dalloc(nA), *dAH = dalloc(nA), *dK = dalloc(nK), *dB = dalloc(nB), *dW = dalloc(primal ? 16 : nW),
+           *dX = dalloc(nX), *dS = dalloc(nS);
+    int* dst = reinterpret_cast<int*>(dalloc(4 * (size_t)batch));
+    if (!dA || !dAH || !dK || !dB || !dW || !dX || !dS || !dst) return fail(ACE_ERR_HIP, "device allocation failed");
+    ACE_HIP(hipStreamCreateWithFlags(&guard.st, hipStreamNonBlocking));
+    hipStream_t st = guard.st;
+    ACE_HIP(upload(dA, A, nA, st));
+    ACE_HIP(upload(dB, B, nB, st));
+    ACE_HIP(hipMemsetAsync(dst, 0, 4 * (size_t)batch, st));
+    launch_conj_transpose(m, n, dA, dAH, st);
+    launch_zgemm(0, true, m, n, m, dA, n, 0, dA, n, 0, dK, nullptr, m, 0, 1, st);   // K = A A^H
+    if (primal) {
+        if (launch_spectral_primal(m, n, r, batch, dK, dAH, dB, dS, dX, dst, st))
+            return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: n = %d too large", n);
+    } else {
+        if (launch_spectral(m, r, batch, dK, dB, dS, dW, dst, st))
+            return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m = %d too large", m);
+        launch_zgemm(0, false, n, m, batch * r, dAH, m, 0, dW, m, 0, dX, nullptr, n, 0, 1, st);
+    }
+    ACE_HIP(hipGetLastError());
+    ACE_HIP(read_back(X, dX, nX, st));
+    if (status) ACE_HIP(read_back(status, dst, 4 * (size_t)batch, st));
+    return ACE_OK;
+}
+
+
 void ace_pipeline_cfg_default(ace_pipeline_cfg* c, int variant) {
     std::memset(c, 0, sizeof *c);
     c->variant = variant;

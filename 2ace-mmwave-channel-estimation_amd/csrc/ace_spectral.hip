@@ -67,14 +67,20 @@ constexpr int HT_THREADS = 1024;
 constexpr int HT_COLS = 256;                 // threads per row quarter
 constexpr int HT_RB = HT_THREADS / HT_COLS;  // row quarters
 
+// The rank-2 update of step k is applied in the same sweep over the trailing matrix as the
+// Hermitian matrix-vector product of step k + 1 (one read and one write per element and step
+// instead of a read for the product plus a read and a write for the update).  Row k + 1, which
+// the next reflector comes from, takes the pending update on the fly; column k + 1 is never read
+// again.  Every element gets the same update expression and every product the same summation
+// order as in the two-sweep form.
 __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
                                                            SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
     extern __shared__ double smem[];
-    d2* v = reinterpret_cast<d2*>(smem);   // reflector / x (mt)
-    d2* w = v + mt;                        // p, w (mt)
-    double* dvs = reinterpret_cast<double*>(w + mt);
+    d2* vb[2] = {reinterpret_cast<d2*>(smem), reinterpret_cast<d2*>(smem) + 2 * mt};   // reflector / x
+    d2* wb[2] = {vb[0] + mt, vb[1] + mt};                                              // p, w
+    double* dvs = reinterpret_cast<double*>(vb[1] + 2 * mt);
     __shared__ double red[16 * 2];
     __shared__ d2 part[HT_RB][HT_COLS];
     __shared__ d2 s_tau, s_scal;
@@ -106,13 +112,21 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
     }
     __syncthreads();
 
+    bool pend = false;   // the update of step k - 1 (pv, pw; index 0 = row k) is not yet applied
+    int cur = 0;
     for (int k = 0; k + 1 < mt; ++k) {
         const int L = mt - k - 1;
+        d2 *v = vb[cur], *w = wb[cur];
+        const d2 *pv = vb[1 - cur], *pw = wb[1 - cur];
         const long long r0 = (long long)(k + 1) * mt + (k + 1);   // C22 origin
-        // x = C(k+1:m, k) = conj(C(k, k+1:m))
+        // x = C(k+1:m, k) = conj(C(k, k+1:m)), with the pending update
         double s1[1] = {0.0};
         for (int i = t; i < L; i += HT_THREADS) {
-            const d2 c = C[(long long)k * mt + k + 1 + i];
+            d2 c = C[(long long)k * mt + k + 1 + i];
+            if (pend) {
+                const d2 cwj = make_double2(pw[1 + i].x, -pw[1 + i].y), cvj = make_double2(pv[1 + i].x, -pv[1 + i].y);
+                c = csub(c, cadd(cmul(pv[0], cwj), cmul(pw[0], cvj)));
+            }
             v[i] = make_double2(c.x, -c.y);
             if (i > 0) s1[0] += cabs2(c);
         }
@@ -132,42 +146,79 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
             s_tau = tau;
             s_scal = scal;
             ee[k] = beta;
-            dd[k] = C[(long long)k * mt + k].x;
+            d2 ckk = C[(long long)k * mt + k];
+            if (pend) {
+                const d2 cw0 = make_double2(pw[0].x, -pw[0].y), cv0 = make_double2(pv[0].x, -pv[0].y);
+                ckk = csub(ckk, cadd(cmul(pv[0], cw0), cmul(pw[0], cv0)));
+            }
+            dd[k] = ckk.x;
             taus[k] = tau;
         }
         __syncthreads();
         const d2 tau = s_tau;
-        if (tau.x == 0.0 && tau.y == 0.0) continue;  // H = I (uniform branch)
-        const d2 scal = s_scal;
-        for (int i = t; i < L; i += HT_THREADS) {
-            const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
-            v[i] = vi;
-            C[(long long)k * mt + k + 1 + i] = vi;  // reflector k kept in row k (for the back transform)
+        const bool refl = !(tau.x == 0.0 && tau.y == 0.0);   // H = I otherwise (uniform branch)
+        if (refl) {
+            const d2 scal = s_scal;
+            for (int i = t; i < L; i += HT_THREADS) {
+                const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
+                v[i] = vi;
+                C[(long long)k * mt + k + 1 + i] = vi;  // reflector k kept in row k (for the back transform)
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        // p = tau C22 v: p_i = tau sum_j conj(C22[j][i]) v_j (Hermitian; column reads are row-coalesced);
-        // thread (col, rb) sums rows j = rb, rb + 4, ...
+        if (!refl && !pend) continue;
+        // one sweep over C22: the pending update (rows / columns 1.. of step k - 1), and
+        // p = tau C22 v: p_i = tau sum_j conj(C22[j][i]) v_j (thread (col, rb) sums rows j = rb, rb + 4, ...)
         for (int i0 = 0; i0 < L; i0 += HT_COLS) {
             const int i = i0 + col;
             double ar = 0.0, ai = 0.0;
             if (i < L) {
-                const d2* cc = C + r0 + i;
+                d2* cc = C + r0 + i;
+                if (pend) {
+                    const d2 cwj = make_double2(pw[1 + i].x, -pw[1 + i].y), cvj = make_double2(pv[1 + i].x, -pv[1 + i].y);
+                    if (refl) {
 #pragma unroll 4
-                for (int j = rb; j < L; j += HT_RB) {
-                    const d2 c = cc[(long long)j * mt], vj = v[j];
-                    ar += c.x * vj.x + c.y * vj.y;
-                    ai += c.x * vj.y - c.y * vj.x;
+                        for (int j = rb; j < L; j += HT_RB) {
+                            d2 c = cc[(long long)j * mt];
+                            c = csub(c, cadd(cmul(pv[1 + j], cwj), cmul(pw[1 + j], cvj)));
+                            cc[(long long)j * mt] = c;
+                            const d2 vj = v[j];
+                            ar += c.x * vj.x + c.y * vj.y;
+                            ai += c.x * vj.y - c.y * vj.x;
+                        }
+                    } else {
+#pragma unroll 4
+                        for (int j = rb; j < L; j += HT_RB) {
+                            d2 c = cc[(long long)j * mt];
+                            c = csub(c, cadd(cmul(pv[1 + j], cwj), cmul(pw[1 + j], cvj)));
+                            cc[(long long)j * mt] = c;
+                        }
+                    }
+                } else {
+#pragma unroll 4
+                    for (int j = rb; j < L; j += HT_RB) {
+                        const d2 c = cc[(long long)j * mt], vj = v[j];
+                        ar += c.x * vj.x + c.y * vj.y;
+                        ai += c.x * vj.y - c.y * vj.x;
+                    }
                 }
             }
-            part[rb][col] = make_double2(ar, ai);
-            __syncthreads();
-            if (rb == 0 && i < L) {
-                d2 acc = part[0][col];
+            if (refl) {
+                part[rb][col] = make_double2(ar, ai);
+                __syncthreads();
+                if (rb == 0 && i < L) {
+                    d2 acc = part[0][col];
 #pragma unroll
-                for (int q = 1; q < HT_RB; ++q) acc = cadd(acc, part[q][col]);
-                w[i] = cmul(tau, acc);
+                    for (int q = 1; q < HT_RB; ++q) acc = cadd(acc, part[q][col]);
+                    w[i] = cmul(tau, acc);
+                }
+                __syncthreads();
             }
+        }
+        pend = refl;
+        if (!refl) {
             __syncthreads();
+            continue;
         }
         double s2[2] = {0.0, 0.0};  // p^H v
         for (int i = t; i < L; i += HT_THREADS) {
@@ -179,36 +230,31 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
         const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
         for (int i = t; i < L; i += HT_THREADS) w[i] = cadd(w[i], cmul(alpha2, v[i]));
         __syncthreads();
-        // C22 -= v w^H + w v^H  (thread (col, rb): column j, rows i = rb, rb + 4, ...)
-        for (int j = col; j < L; j += HT_COLS) {
-            const d2 vj = v[j], wj = w[j];
-            const d2 cvj = make_double2(vj.x, -vj.y), cwj = make_double2(wj.x, -wj.y);
-            d2* cc = C + r0 + j;
-#pragma unroll 4
-            for (int i = rb; i < L; i += HT_RB) {
-                d2 c = cc[(long long)i * mt];
-                c = csub(c, cadd(cmul(v[i], cwj), cmul(w[i], cvj)));
-                cc[(long long)i * mt] = c;
-            }
-        }
-        __syncthreads();
+        cur = 1 - cur;   // (v, w) of step k become the pending update of step k + 1
     }
+    __syncthreads();
     if (t == 0) {
-        dd[mt - 1] = C[(long long)(mt - 1) * mt + mt - 1].x;
+        d2 c = C[(long long)(mt - 1) * mt + mt - 1];
+        if (pend) {
+            const d2 *pv = vb[1 - cur], *pw = wb[1 - cur];
+            const d2 cw0 = make_double2(pw[0].x, -pw[0].y), cv0 = make_double2(pv[0].x, -pv[0].y);
+            c = csub(c, cadd(cmul(pv[0], cw0), cmul(pw[0], cv0)));
+        }
+        dd[mt - 1] = c.x;
         ee[mt - 1] = 0.0;
     }
-#ifdef ACE_DEBUG_SPEC
-    __syncthreads();
-    if (t == 0 && b < 2) {
-        int nd = 0, ne = 0, nt0 = 0, f = -1;
-        for (int i = 0; i < mt; ++i) {
-            if (!isfinite(dd[i])) { ++nd; if (f < 0) f = i; }
-            if (!isfinite(ee[i])) ++ne;
-            if (i + 1 < mt && taus[i].x == 0.0 && taus[i].y == 0.0) ++nt0;
-        }
-        printf("hetrd b %d mt %d nan dd %d ee %d first %d tau0 %d dd0 %g ee0 %g\n", b, mt, nd, ne, f, nt0, dd[0], ee[0]);
-    }
-#endif
+}
+size_t hetrd_lds(int mt) { return (size_t)mt * (4 * 16 + 8); }
+constexpr size_t HT_MAXDYN = 140 * 1024;   // dynamic LDS above the static part (160 KiB per CU)
+bool hetrd_lds_ok(int mt) {
+    static const bool attr = [] {
+        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&hetrd_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)HT_MAXDYN) == hipSuccess;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    const size_t need = hetrd_lds(mt);
+    return need <= 64 * 1024 || (attr && need <= HT_MAXDYN);
 }
 
 // Sturm count: number of eigenvalues of the tridiagonal (d, e) below x.
@@ -590,8 +636,8 @@ size_t spectral_scratch_bytes(int mt, int n, int batch, int r) {
 int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
                            double* scratch, double* X, int* status, hipStream_t st) {
     const SpecLayout lay(n, r);
-    const size_t sm_h = (size_t)n * (16 + 16 + 8), sm_t = (size_t)n * 16;
-    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+    const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 16;
+    if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
     const int chunk = primal_chunk(mt, n, batch);
     double* Ast = scratch + (((size_t)lay.stride * chunk + 31) & ~(size_t)31);
     for (int b0 = 0; b0 < batch; b0 += chunk) {
@@ -618,8 +664,8 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
                     int* status, hipStream_t st) {
     const SpecLayout lay(mt, r);
-    const size_t sm_h = (size_t)mt * (16 + 16 + 8), sm_t = (size_t)mt * 16;
-    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+    const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 16;
+    if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
         hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay,
@@ -758,8 +804,8 @@ size_t heev_scratch_bytes(int d, int kmax, int batch) {
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
                 const int* active, hipStream_t st) {
     const SpecLayout lay(d, kmax);
-    const size_t sm_h = (size_t)d * (16 + 16 + 8), sm_t = (size_t)d * 16;
-    if (sm_h > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+    const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 16;
+    if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
     hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
     if (!wy_path(d, kmax)) {

@@ -165,6 +165,18 @@ int ace_pipeline_solve_host(const ace_pipeline_cfg* cfg, int batch, int m, int n
                             const double* A, const double* B, const int32_t* train_idx,
                             double* X, double* Y, double* quality, int32_t* stage_iters, uint32_t* status);
 
+/* ---- SpectralInitialize (inferLowRankV4_multi.m:561-574) ----------------------------------
+ *   X = SpectralInitialize(A, B, r)
+ * for a batch of magnitude vectors B [batch][m] (f64) sharing one A [m][n] (c128, row-major,
+ * HOST arrays): X [batch][r][n] c128, column k = sqrt(s_k) v_k for the k-th largest eigenpair of
+ * As^H As (As = rows of A scaled by B_i/||a_i||); eigenvectors are defined up to a unit phase
+ * (MATLAB's eig and LAPACK pick one; the GPU picks another).  The pipeline's own initialisation
+ * (ace_pipeline_solve_batch, :58) runs the same kernels: through the m x m dual Gram when m <= n,
+ * the n x n primal Gram otherwise.  status [batch] (may be NULL): ACE_ST_EIG_NOCONV bits.
+ * Synchronous; allocates its own device memory. */
+int ace_spectral_init_host(int batch, int m, int n, int r, const double* A, const double* B, double* X,
+                           uint32_t* status);
+
 /* ---- PhaseLift (MyPhaseLift.m:69-107 via TFOCS solver_TraceLS / tfocs_AT) ----------------
  *   recoveredSig = MyPhaseLift(measurements, measurementMat)
  *   main/src/my_recovery_algorithms/MyPhaseLift.m:69 (called by Recover_Channel.m:34 with

@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include <thread>
+
 #include "ace_host.hpp"
 #include "ace_pipe.hpp"
 
@@ -32,33 +34,51 @@ struct PipeDims {
     int batch, m, n, tx, rx, r, mt, mte, restarts;
 };
 
-struct PipeWs {
-    double *anorm, *bnorm, *Bn, *Bt, *Bte, *Bt_s, *Bte_s;
-    double *An, *At, *Ate;
-    LinOps Lt, Lf;
+// The pieces one restart (:42-77) works on.  Restarts are independent until the best of them is
+// taken (:79-83), so a small batch (the driver's one realisation per sweep point) runs them
+// concurrently, each on its own stream and workspace copy; a large batch, which fills the GPU on
+// its own, runs them one after another in one copy.
+struct RestartWs {
+    double *Bt, *Bte, *Bt_s, *Bte_s, *At, *Ate;
+    LinOps Lt;
     double *W, *spec, *Xs, *Xs_s;
     double *X1, *Y1;                 // stage-1 output (r columns), reused by both stages' chains
     double *X2, *Y2, *X2_s, *Y2_s;   // impl outputs (best column)
-    double *q, *q_s, *qmax, *qlast, *Xmax, *Ymax, *Xr, *Yr;
-    int *iters, *stat, *idx_rows, *idx_sub, *stage_dev, *status_dev;
+    double *q, *q_s;
+    int *iters, *stat, *idx_rows, *idx_sub, *status_dev;
     unsigned char* rank_one;
-    AdmmState sr, s1;                // r-column state (m_t rows), refinement state (r = 1, m rows)
+    AdmmState sr;                    // r-column state (m_t rows)
 };
 
-void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
+constexpr int kConcurrentBatch = 16;   // restarts run concurrently up to this batch size
+int restart_copies(const PipeDims& d) {
+    static const bool serial = [] {
+        const char* e = getenv("ACE_PIPE_SERIAL");
+        return e && e[0] == '1';
+    }();
+    return (!serial && d.restarts > 1 && d.batch <= kConcurrentBatch) ? d.restarts : 1;
+}
+
+struct PipeWs {
+    double *anorm, *bnorm, *Bn, *An;
+    LinOps Lf;
+    double *qmax, *qlast, *Xmax, *Ymax, *Xr, *Yr;
+    int *iters, *stat, *idx_all, *stage_dev, *status_dev;
+    unsigned char* rank_one;         // the refinement's use_rank_one (the last restart's)
+    AdmmState s1;                    // refinement state (r = 1, m rows)
+    int nrw;
+    RestartWs rw[16];
+};
+
+void restart_carve(Carver& cv, const PipeDims& d, RestartWs* w) {
     const size_t cz = 16, B = (size_t)d.batch;
-    w->anorm = cv.take(256);
-    w->bnorm = cv.take(8 * B);
-    w->Bn = cv.take(8 * B * d.m);
     w->Bt = cv.take(8 * B * d.mt);
     w->Bte = cv.take(8 * B * std::max(d.mte, 1));
     w->Bt_s = cv.take(8 * B * d.mt);
     w->Bte_s = cv.take(8 * B * std::max(d.mte, 1));
-    w->An = cv.take(cz * d.m * d.n);
     w->At = cv.take(cz * d.mt * d.n);
     w->Ate = cv.take(cz * std::max(d.mte, 1) * d.n);
     linops_carve(cv, true, d.batch, d.mt, d.n, &w->Lt);
-    linops_carve(cv, true, d.batch, d.m, d.n, &w->Lf);
     w->W = cv.take(cz * B * d.r * d.mt);
     w->spec = cv.take(spectral_scratch_bytes(d.mt, d.n, d.batch, d.r));
     w->Xs = cv.take(cz * B * d.r * d.n);
@@ -71,6 +91,22 @@ void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
     w->Y2_s = cv.take(cz * B * d.mt);
     w->q = cv.take(8 * B);
     w->q_s = cv.take(8 * B);
+    w->iters = cv.take<int>(4 * B);
+    w->stat = cv.take<int>(4 * B);
+    w->idx_rows = cv.take<int>(4 * (size_t)d.m);
+    w->idx_sub = cv.take<int>(4 * B);
+    w->status_dev = cv.take<int>(4 * B);
+    w->rank_one = cv.take<unsigned char>(B);
+    admm_state_carve(cv, d.batch, d.mt, d.n, d.r, &w->sr);
+}
+
+void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
+    const size_t cz = 16, B = (size_t)d.batch;
+    w->anorm = cv.take(256);
+    w->bnorm = cv.take(8 * B);
+    w->Bn = cv.take(8 * B * d.m);
+    w->An = cv.take(cz * d.m * d.n);
+    linops_carve(cv, true, d.batch, d.m, d.n, &w->Lf);
     w->qmax = cv.take(8 * B);
     w->qlast = cv.take(8 * B);
     w->Xmax = cv.take(cz * B * d.n);
@@ -79,13 +115,13 @@ void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
     w->Yr = cv.take(cz * B * d.m);
     w->iters = cv.take<int>(4 * B);
     w->stat = cv.take<int>(4 * B);
-    w->idx_rows = cv.take<int>(4 * (size_t)d.m);
-    w->idx_sub = cv.take<int>(4 * B);
+    w->idx_all = cv.take<int>(4 * (size_t)d.m);
     w->stage_dev = cv.take<int>(4 * B * (4 * d.restarts + 1));
     w->status_dev = cv.take<int>(4 * B);
     w->rank_one = cv.take<unsigned char>(B);
-    admm_state_carve(cv, d.batch, d.mt, d.n, d.r, &w->sr);
     admm_state_carve(cv, d.batch, d.m, d.n, 1, &w->s1);
+    w->nrw = restart_copies(d);
+    for (int i = 0; i < w->nrw; ++i) restart_carve(cv, d, &w->rw[i]);
 }
 
 int validate_dims(const ace_pipeline_cfg* c, int batch, int m, int n, PipeDims* d) {
@@ -123,20 +159,81 @@ int validate(const ace_pipeline_cfg* c, int batch, int m, int n, int tx, int rx,
 // inferLowRankImpl (:111-271) for `nb` realisations: Xs [nb][r][n], Bt [nb][mt] ->
 // X2 [nb][n], Y2 [nb][mt] (best column of the per-column stage); iteration counts of the
 // two stages into stage_dev columns col, col + 1 (rows idx[k] or k).
-int run_impl(const PipeDims& d, PipeWs& w, const AdmmParams& base, int nb, const double* Xs, const double* Bt,
-             double* X2, double* Y2, const int* idx, int col, hipStream_t st) {
+int run_impl(const PipeDims& d, RestartWs& w, int* stage_dev, const AdmmParams& base, int nb, const double* Xs,
+             const double* Bt, double* X2, double* Y2, const int* idx, int col, hipStream_t st) {
     const int ld = 4 * d.restarts + 1;
     AdmmParams p = base;
     p.r = d.r;
     p.row_mode = 1;                                               // :258 scale_by_row = true
     ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, Xs, w.X1, w.Y1, w.iters, (uint32_t*)w.stat, nullptr, st));
-    launch_put_col(nb, w.iters, idx, w.stage_dev, ld, col, 0, st);
+    launch_put_col(nb, w.iters, idx, stage_dev, ld, col, 0, st);
     launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
     launch_gram_rotate(d.n, d.r, nb, w.X1, nullptr, st);         // :263-264
     p.row_mode = 0;                                               // :270 scale_by_row = false
     ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, w.X1, X2, Y2, w.iters, (uint32_t*)w.stat, nullptr, st));
-    launch_put_col(nb, w.iters, idx, w.stage_dev, ld, col + 1, 0, st);
+    launch_put_col(nb, w.iters, idx, stage_dev, ld, col + 1, 0, st);
     launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+// One restart (:42-77) for the whole batch on stream st: partition, K_t / G_t, SpectralInitialize,
+// inferLowRankImpl, test quality, rank-one retry.  Leaves q, X2, Y2, rank_one and the restart's
+// status bits in w.
+int run_restart(int i, const PipeDims& d, const double* A, const double* anorm, const double* Bn,
+                const std::vector<int>& rows, const AdmmParams& base, RestartWs& w, int* stage_dev, hipStream_t st) {
+    const int batch = d.batch, n = d.n, m = d.m;
+    ACE_HIP(hipMemsetAsync(w.status_dev, 0, 4 * (size_t)batch, st));
+    // ---- :47-53 partition
+    ACE_HIP(upload(w.idx_rows, rows.data(), 4 * (size_t)m, st));
+    launch_gather_rows(d.mt, n, A, w.idx_rows, anorm, w.At, st);
+    launch_gather_rows(d.mte, n, A, w.idx_rows + d.mt, anorm, w.Ate, st);
+    launch_gather_b(m, d.mt, batch, Bn, w.idx_rows, w.Bt, st);
+    launch_gather_b(m, d.mte, batch, Bn, w.idx_rows + d.mt, w.Bte, st);
+    w.Lt.A = w.At;
+    ACE_TRY(linops_setup(w.Lt, batch, st));                          // K_t, G_t (U, :242), A_t^H
+    // ---- :58 SpectralInitialize: X = V(:, 1:r) diag(sqrt(s))
+    {
+        ProfScope ps(ACE_K_SETUP, st);
+        if (spectral_primal(d.mt, n)) {
+            if (launch_spectral_primal(d.mt, n, d.r, batch, w.Lt.K, w.Lt.AH, w.Bt, w.spec, w.Xs, w.status_dev, st))
+                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: n = %d too large", n);
+        } else {
+            if (launch_spectral(d.mt, d.r, batch, w.Lt.K, w.Bt, w.spec, w.W, w.status_dev, st))
+                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
+            launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
+        }
+    }
+    ACE_HIP(hipGetLastError());
+    // ---- :65-68 impl (use_rank_one = false) and test quality
+    AdmmParams p = base;
+    p.use_rank_one = 0;
+    p.rank_one = nullptr;
+    ACE_TRY(run_impl(d, w, stage_dev, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
+    launch_quality(n, d.mte, batch, w.Ate, w.X2, w.Bte, w.q, st);
+    // ---- :73-77 rank-one retry on the realisations with quality < 0.6
+    std::vector<double> hq(batch);
+    std::vector<unsigned char> ro(batch);
+    std::vector<int> fails;
+    ACE_HIP(read_back(hq.data(), w.q, 8 * (size_t)batch, st));
+    for (int b = 0; b < batch; ++b) {
+        ro[b] = hq[b] < 0.6;
+        if (ro[b]) fails.push_back(b);
+    }
+    ACE_HIP(upload(w.rank_one, ro.data(), batch, st));
+    const int nf = (int)fails.size();
+    if (nf > 0) {
+        ACE_HIP(upload(w.idx_sub, fails.data(), 4 * (size_t)nf, st));
+        launch_move_rows(nf, 2LL * d.r * n, w.Xs, w.Xs_s, w.idx_sub, false, st);
+        launch_move_rows(nf, d.mt, w.Bt, w.Bt_s, w.idx_sub, false, st);
+        launch_move_rows(nf, std::max(d.mte, 1), w.Bte, w.Bte_s, w.idx_sub, false, st);
+        p.use_rank_one = 1;
+        ACE_TRY(run_impl(d, w, stage_dev, p, nf, w.Xs_s, w.Bt_s, w.X2_s, w.Y2_s, w.idx_sub, 4 * i + 2, st));
+        launch_quality(n, d.mte, nf, w.Ate, w.X2_s, w.Bte_s, w.q_s, st);
+        launch_move_rows(nf, 2LL * n, w.X2_s, w.X2, w.idx_sub, true, st);
+        launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
+        launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
+    }
     ACE_HIP(hipGetLastError());
     return ACE_OK;
 }
@@ -276,84 +373,99 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     std::vector<int> iota(m);
     for (int i = 0; i < m; ++i) iota[i] = i;
     launch_anorm(m, n, A, cfg->tol_abs, w.anorm, st);
-    ACE_HIP(upload(w.idx_rows, iota.data(), 4 * (size_t)m, st));
-    launch_gather_rows(m, n, A, w.idx_rows, w.anorm, w.An, st);
+    ACE_HIP(upload(w.idx_all, iota.data(), 4 * (size_t)m, st));
+    launch_gather_rows(m, n, A, w.idx_all, w.anorm, w.An, st);
     launch_bnorm(m, batch, B, cfg->tol_abs, w.bnorm, w.Bn, st);
     launch_fill(batch, -1.0, w.qmax, st);                                 // max_quality = -1 (:40)
     ACE_HIP(hipMemsetAsync(w.stage_dev, 0, 4 * (size_t)batch * ld, st));
     ACE_HIP(hipMemsetAsync(w.status_dev, 0, 4 * (size_t)batch, st));
-    std::vector<double> hq(batch);
-    std::vector<int> fails;
-    std::vector<unsigned char> ro(batch);
-
+    std::vector<std::vector<int>> rows(d.restarts);
     for (int i = 0; i < d.restarts; ++i) {
-        // ---- :47-53 partition
-        std::vector<int> rows(tr[i]);
-        rows.insert(rows.end(), te[i].begin(), te[i].end());
-        ACE_HIP(upload(w.idx_rows, rows.data(), 4 * (size_t)m, st));
-        launch_gather_rows(d.mt, n, A, w.idx_rows, w.anorm, w.At, st);
-        launch_gather_rows(d.mte, n, A, w.idx_rows + d.mt, w.anorm, w.Ate, st);
-        launch_gather_b(m, d.mt, batch, w.Bn, w.idx_rows, w.Bt, st);
-        launch_gather_b(m, d.mte, batch, w.Bn, w.idx_rows + d.mt, w.Bte, st);
-        w.Lt.A = w.At;
-        ACE_TRY(linops_setup(w.Lt, batch, st));                          // K_t, G_t (U, :242), A_t^H
-        // ---- :58 SpectralInitialize: W = D u_k, X = A_t^H W
-        {
-            ProfScope ps(ACE_K_SETUP, st);
-            if (spectral_primal(d.mt, n)) {
-                if (launch_spectral_primal(d.mt, n, d.r, batch, w.Lt.K, w.Lt.AH, w.Bt, w.spec, w.Xs, w.status_dev, st))
-                    return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: n = %d too large", n);
-            } else {
-                if (launch_spectral(d.mt, d.r, batch, w.Lt.K, w.Bt, w.spec, w.W, w.status_dev, st))
-                    return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
-                launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
-            }
-        }
-        ACE_HIP(hipGetLastError());
-        // ---- :65-68 impl (use_rank_one = false) and test quality
-        AdmmParams p = base;
-        p.use_rank_one = 0;
-        p.rank_one = nullptr;
-        ACE_TRY(run_impl(d, w, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
-        launch_quality(n, d.mte, batch, w.Ate, w.X2, w.Bte, w.q, st);
-        // ---- :73-77 rank-one retry on the realisations with quality < 0.6
-        ACE_HIP(read_back(hq.data(), w.q, 8 * (size_t)batch, st));
-        fails.clear();
-        for (int b = 0; b < batch; ++b) {
-            ro[b] = hq[b] < 0.6;
-            if (ro[b]) fails.push_back(b);
-        }
-        ACE_HIP(upload(w.rank_one, ro.data(), batch, st));
-        const int nf = (int)fails.size();
-        if (nf > 0) {
-            ACE_HIP(upload(w.idx_sub, fails.data(), 4 * (size_t)nf, st));
-            launch_move_rows(nf, 2LL * d.r * n, w.Xs, w.Xs_s, w.idx_sub, false, st);
-            launch_move_rows(nf, d.mt, w.Bt, w.Bt_s, w.idx_sub, false, st);
-            launch_move_rows(nf, std::max(d.mte, 1), w.Bte, w.Bte_s, w.idx_sub, false, st);
-            p.use_rank_one = 1;
-            ACE_TRY(run_impl(d, w, p, nf, w.Xs_s, w.Bt_s, w.X2_s, w.Y2_s, w.idx_sub, 4 * i + 2, st));
-            launch_quality(n, d.mte, nf, w.Ate, w.X2_s, w.Bte_s, w.q_s, st);
-            launch_move_rows(nf, 2LL * n, w.X2_s, w.X2, w.idx_sub, true, st);
-            launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
-            launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
-        }
-        // ---- :79-83 best of restarts (A2only); the nuclear pipeline keeps the last X
+        rows[i] = tr[i];
+        rows[i].insert(rows[i].end(), te[i].begin(), te[i].end());
+    }
+    // ---- :79-83 best of restarts (A2only; the nuclear pipeline keeps the last X), in restart order
+    auto take_restart = [&](int i, RestartWs& rw) -> int {
         if (cfg->variant == ACE_VARIANT_A2ONLY) {
-            launch_keep_best(n, d.mt, batch, i == 0, w.q, w.qmax, w.X2, w.Y2, w.Xmax, w.Ymax, st);
+            launch_keep_best(n, d.mt, batch, i == 0, rw.q, w.qmax, rw.X2, rw.Y2, w.Xmax, w.Ymax, st);
         } else {
-            ACE_HIP(hipMemcpyAsync(w.Xmax, w.X2, 16 * (size_t)batch * n, hipMemcpyDeviceToDevice, st));
-            ACE_HIP(hipMemcpyAsync(w.Ymax, w.Y2, 16 * (size_t)batch * d.mt, hipMemcpyDeviceToDevice, st));
+            ACE_HIP(hipMemcpyAsync(w.Xmax, rw.X2, 16 * (size_t)batch * n, hipMemcpyDeviceToDevice, st));
+            ACE_HIP(hipMemcpyAsync(w.Ymax, rw.Y2, 16 * (size_t)batch * d.mt, hipMemcpyDeviceToDevice, st));
         }
-        ACE_HIP(hipMemcpyAsync(w.qlast, w.q, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+        ACE_HIP(hipMemcpyAsync(w.qlast, rw.q, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
+        ACE_HIP(hipMemcpyAsync(w.rank_one, rw.rank_one, batch, hipMemcpyDeviceToDevice, st));
+        launch_put_col(batch, rw.status_dev, nullptr, w.status_dev, 1, 0, ~0u, st);
         ACE_HIP(hipGetLastError());
+        return ACE_OK;
+    };
+    if (w.nrw == 1 || g_prof.on) {   // one after another (the kernel timer is not thread-safe)
+        for (int i = 0; i < d.restarts; ++i) {
+            ACE_TRY(run_restart(i, d, A, w.anorm, w.Bn, rows[i], base, w.rw[0], w.stage_dev, st));
+            ACE_TRY(take_restart(i, w.rw[0]));
+        }
+    } else {                         // concurrently, one host thread and stream each
+        const int R = d.restarts;
+        hipEvent_t ev0 = nullptr;
+        std::vector<hipEvent_t> done(R, nullptr);
+        std::vector<hipStream_t> ss(R, nullptr);
+        std::vector<int> rc(R, ACE_OK);
+        std::vector<std::string> err(R);
+        auto cleanup = [&]() {
+            for (int i = 0; i < R; ++i) {
+                if (ss[i]) (void)hipStreamDestroy(ss[i]);
+                if (done[i]) (void)hipEventDestroy(done[i]);
+            }
+            if (ev0) (void)hipEventDestroy(ev0);
+        };
+        hipError_t e = hipEventCreateWithFlags(&ev0, hipEventDisableTiming);
+        for (int i = 0; i < R && e == hipSuccess; ++i) {
+            e = hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
+        }
+        if (e == hipSuccess) e = hipEventRecord(ev0, st);   // the normalisation is done
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(ACE_ERR_HIP, "restart streams: %s", hipGetErrorString(e));
+        }
+        int dev = 0;
+        (void)hipGetDevice(&dev);   // (the current device is per thread)
+        std::vector<std::thread> th;
+        for (int i = 0; i < R; ++i)
+            th.emplace_back([&, i]() {
+                hipError_t ei = hipSetDevice(dev);
+                if (ei == hipSuccess) ei = hipStreamWaitEvent(ss[i], ev0, 0);
+                rc[i] = ei == hipSuccess ? run_restart(i, d, A, w.anorm, w.Bn, rows[i], base, w.rw[i], w.stage_dev, ss[i])
+                                         : fail(ACE_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(ei));
+                if (rc[i] == ACE_OK && (ei = hipEventRecord(done[i], ss[i])) != hipSuccess)
+                    rc[i] = fail(ACE_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(ei));
+                err[i] = g_err;
+            });
+        for (auto& t : th) t.join();
+        for (int i = 0; i < R; ++i)
+            if (rc[i] != ACE_OK) {
+                for (int k = 0; k < R; ++k) (void)hipStreamSynchronize(ss[k]);
+                cleanup();
+                g_err = err[i];
+                return rc[i];
+            }
+        for (int i = 0; i < R; ++i) e = e == hipSuccess ? hipStreamWaitEvent(st, done[i], 0) : e;
+        if (e != hipSuccess) {
+            for (int k = 0; k < R; ++k) (void)hipStreamSynchronize(ss[k]);
+            cleanup();
+            return fail(ACE_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+        }
+        int rct = ACE_OK;
+        for (int i = 0; i < R && rct == ACE_OK; ++i) rct = take_restart(i, w.rw[i]);
+        cleanup();   // (streams and events are released once their queued work has completed)
+        ACE_TRY(rct);
     }
 
     if (cfg->stop_before_refine) {   // X_max and Y_max (on the train rows), rescaled; no rollback test
-        launch_fill(batch, -1.0, w.q_s, st);
+        launch_fill(batch, -1.0, w.rw[0].q_s, st);
         ACE_HIP(hipMemsetAsync(w.Yr, 0, 16 * (size_t)batch * m, st));
         ACE_HIP(hipMemcpy2DAsync(w.Yr, 16 * (size_t)m, w.Ymax, 16 * (size_t)d.mt, 16 * (size_t)d.mt, batch,
                                  hipMemcpyDeviceToDevice, st));
-        launch_finish(n, m, d.mt, batch, w.q_s, w.Xmax, w.Yr, w.Xmax, w.Ymax, w.anorm, w.bnorm, Xo, Yo, nullptr, st);
+        launch_finish(n, m, d.mt, batch, w.rw[0].q_s, w.Xmax, w.Yr, w.Xmax, w.Ymax, w.anorm, w.bnorm, Xo, Yo, nullptr, st);
         if (quality) ACE_HIP(hipMemcpyAsync(quality, w.qlast, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
         if (stage_iters)
             ACE_HIP(hipMemcpyAsync(stage_iters, w.stage_dev, 4 * (size_t)batch * ld, hipMemcpyDeviceToDevice, st));

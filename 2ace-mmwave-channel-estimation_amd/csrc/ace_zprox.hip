@@ -45,6 +45,20 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
     // accumulators: nX2, nZ2, nJN2, dZ2
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     VMax vz, vn;   // max |Z|, |N| of the outputs: the next apply's bound on |Z - N/mu|
+    auto emit_pre = [&](int k, d2 znew, d2 x, d2 zo, d2 nold) {  // per-element update + reductions
+        vz.add(znew);
+        if (!INIT) {
+            const d2 d = csub(x, znew);
+            const d2 nnew = cadd(nold, cscale(d, mu));
+            N[k] = nnew;
+            vn.add(nnew);
+            acc[0] += cabs2(x);
+            acc[1] += cabs2(znew);
+            acc[2] += cabs2(d);
+            acc[3] += cabs2(csub(znew, zo));
+        }
+        Z[k] = znew;
+    };
     auto emit = [&](int k, d2 znew) {  // per-element update + reductions
         const d2 x = X[k];
         vz.add(znew);
@@ -143,17 +157,31 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         __shared__ double rs2[TXMAX];
         __shared__ int ord[TXMAX], ascp[TXMAX];
         const ZProfile pf = z_profile(a, b);
-        auto stage_E = [&](int j) {  // E_j into L0, zero padded to 32 x 32
+        // E_j (zero padded to 32 x 32) is fetched into registers one block ahead of its use, so
+        // the loads of block j + 1 are in flight during block j's barrier and matrix-core step
+        // (a barrier waits for LDS traffic only); 256 threads x 4 slots = one 32 x 32 tile.
+        auto fetchE = [&](int j, d2 (&o)[4]) {
             const int base = j * n;
-            for (int e = t; e < TXMAX * TXMAX; e += nt) {
-                const int i = e & 31, c = e >> 5;
-                L0[i * HS + c] = (i < tx && c < rx) ? evalE(base + i + tx * c) : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = t + 256 * u, i = e & 31, c = e >> 5;
+                o[u] = (i < tx && c < rx) ? evalE(base + i + tx * c) : make_double2(0.0, 0.0);
             }
         };
+        auto putE = [&](const d2 (&o)[4]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = t + 256 * u;
+                L0[(e & 31) * HS + (e >> 5)] = o[u];
+            }
+        };
+        d2 eb[4];
         cr = d4v{0.0, 0.0, 0.0, 0.0};
         ci = d4v{0.0, 0.0, 0.0, 0.0};
+        fetchE(0, eb);
         for (int j = 0; j < r; ++j) {
-            stage_E(j);
+            putE(eb);
+            if (j + 1 < r) fetchE(j + 1, eb);
             __syncthreads();
             mm32_acc<false, true>(L0, L0, cr, ci, lane, w);  // H += E_j E_j^H  (:428)
             __syncthreads();
@@ -245,18 +273,52 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             __syncthreads();
             store32(L1, cr, ci, lane, w);
             __syncthreads();
+            // the emit inputs (X, old Z, old N) of block j are requested with block j + 1's E
+            d2 px[4], pz[4], pn[4];
+            auto fetchP = [&](int j) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = t + nt * u;
+                    if (k < n) {
+                        px[u] = X[j * n + k];
+                        pz[u] = INIT ? make_double2(0.0, 0.0) : Z[j * n + k];
+                        pn[u] = N[j * n + k];
+                    }
+                }
+            };
+            fetchE(0, eb);
+            fetchP(0);
             for (int j = 0; j < r; ++j) {
-                stage_E(j);
+                putE(eb);
+                if (j + 1 < r) fetchE(j + 1, eb);
                 __syncthreads();
                 mm32<false, false>(L1, L0, cr, ci, lane, w);  // W E_j
                 __syncthreads();
                 store32(L0, cr, ci, lane, w);
                 __syncthreads();
-                for (int k = t; k < n; k += nt) emit(j * n + k, L0[(k % tx) * HS + k / tx]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = t + nt * u;
+                    if (k < n) emit_pre(j * n + k, L0[(k % tx) * HS + k / tx], px[u], pz[u], pn[u]);
+                }
+                if (j + 1 < r) fetchP(j + 1);
                 __syncthreads();
             }
         } else {
-            for (int k = t; k < rn; k += nt) emit(k, evalE(k));
+            // Z = E: the element stream in batches of 4 per thread, loads issued before the stores
+            for (int k0 = 0; k0 < rn; k0 += 4 * nt) {
+                d2 ev[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + t + nt * u;
+                    ev[u] = k < rn ? evalE(k) : make_double2(0.0, 0.0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + t + nt * u;
+                    if (k < rn) emit(k, ev[u]);
+                }
+            }
         }
     }
 #undef ACE_ZSTEP_LDS

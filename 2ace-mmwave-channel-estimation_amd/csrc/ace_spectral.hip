@@ -271,28 +271,6 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     return cnt;
 }
 
-// Sturm counts at four points in one pass: four independent recurrences per step, so the division
-// latency of one hides behind the others (multisection, see trieig_kernel).
-__device__ __forceinline__ void sturm_count4(const double* d, const double* e, int n, const double (&x)[4],
-                                             double pivmin, int (&cnt)[4]) {
-    double q[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        q[s] = d[0] - x[s];
-        if (fabs(q[s]) < pivmin) q[s] = -pivmin;
-        cnt[s] = q[s] < 0.0;
-    }
-    for (int i = 1; i < n; ++i) {
-        const double di = d[i], e2 = e[i - 1] * e[i - 1];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            q[s] = di - x[s] - e2 / q[s];
-            if (fabs(q[s]) < pivmin) q[s] = -pivmin;
-            cnt[s] += q[s] < 0.0;
-        }
-    }
-}
-
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
@@ -354,29 +332,9 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
-    for (int q = t; q < k; q += 256) {  // the (mt-1-q)-th ascending eigenvalue
+    for (int q = t; q < k; q += 256) {  // bisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
-        // multisection: Sturm counts at 4 interior points cut the interval 5x per pass, ...
-        for (int it = 0; it < 200; ++it) {
-            const double w = hi - lo;
-            if (w <= 64.0 * (2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin)) break;
-            double x[4];
-            int c[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) x[s] = lo + w * (0.2 * (s + 1));
-            sturm_count4(d, e, mt, x, pivmin, c);
-            double nlo = lo, nhi = hi;
-#pragma unroll
-            for (int s = 3; s >= 0; --s)
-                if (c[s] > j) nhi = x[s];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                if (c[s] <= j) nlo = x[s];
-            lo = nlo;
-            hi = nhi;
-        }
-        // ... then bisection to full precision (LAPACK dstebz's stopping rule)
         for (int it = 0; it < 200; ++it) {
             if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
             const double mid = 0.5 * (lo + hi);

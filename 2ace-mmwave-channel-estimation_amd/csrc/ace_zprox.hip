@@ -178,15 +178,52 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         d2 eb[4];
         cr = d4v{0.0, 0.0, 0.0, 0.0};
         ci = d4v{0.0, 0.0, 0.0, 0.0};
-        fetchE(0, eb);
-        for (int j = 0; j < r; ++j) {
-            putE(eb);
-            if (j + 1 < r) fetchE(j + 1, eb);
+        // tx, rx <= 16 (the driver's 16 x 16 arrays): E E^H is one 16 x 16 tile, so each wave
+        // accumulates the blocks j = w, w + 4, ... straight from memory (16 MFMAs per block, no
+        // LDS staging or barrier per block) and the four partial tiles are summed in LDS.
+        const bool small = tx <= 16 && rx <= 16;
+        if (small) {
+            for (int j = w; j < r; j += 4) {
+                d2 ev[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {   // lane: E_j[l & 15][4u + (l >> 4)]
+                    const int i = lane & 15, kk = 4 * u + (lane >> 4);
+                    ev[u] = (i < tx && kk < rx) ? evalE(j * n + i + tx * kk) : make_double2(0.0, 0.0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {   // A = E_j, B = E_j^H: the lane's operands are e and conj(e)
+                    const d2 av = ev[u];
+                    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, av.x, cr, 0, 0, 0);
+                    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, -av.y, cr, 0, 0, 0);
+                    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, -av.y, ci, 0, 0, 0);
+                    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, av.x, ci, 0, 0, 0);
+                }
+            }
+            d2* part = L1;   // [4][16][16] partial tiles (exactly the L1 tile's 32 x 33 budget)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+                part[w * 256 + ((lane >> 4) + 4 * rr) * 16 + (lane & 15)] = make_double2(cr[rr], ci[rr]);
             __syncthreads();
-            mm32_acc<false, true>(L0, L0, cr, ci, lane, w);  // H += E_j E_j^H  (:428)
+            for (int e = t; e < TXMAX * TXMAX; e += nt) {   // H (zero padded), waves summed in order
+                const int i = e >> 5, c = e & 31;
+                d2 h = make_double2(0.0, 0.0);
+                if (i < 16 && c < 16)
+#pragma unroll
+                    for (int ww = 0; ww < 4; ++ww) h = cadd(h, part[ww * 256 + i * 16 + c]);
+                L0[i * HS + c] = h;
+            }
             __syncthreads();
+        } else {
+            fetchE(0, eb);
+            for (int j = 0; j < r; ++j) {
+                putE(eb);
+                if (j + 1 < r) fetchE(j + 1, eb);
+                __syncthreads();
+                mm32_acc<false, true>(L0, L0, cr, ci, lane, w);  // H += E_j E_j^H  (:428)
+                __syncthreads();
+            }
+            store32(L0, cr, ci, lane, w);
         }
-        store32(L0, cr, ci, lane, w);
         const bool warm = (!INIT) && a.warm && a.Q;
         d2* Qg = a.Q ? reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx : nullptr;
         for (int e = t; e < TXMAX * TXMAX; e += nt) {
@@ -273,6 +310,33 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             __syncthreads();
             store32(L1, cr, ci, lane, w);
             __syncthreads();
+            if (small) {   // Z_j = W E_j per wave, block j = w, w + 4, ..., emitted from the MFMA outputs
+                d2 wa[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) wa[u] = L1[(lane & 15) * HS + 4 * u + (lane >> 4)];   // A = W
+                for (int j = w; j < r; j += 4) {
+                    d2 ev[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {   // B = E_j: lane E_j[4u + (l >> 4)][l & 15]
+                        const int kk = 4 * u + (lane >> 4), c = lane & 15;
+                        ev[u] = (kk < tx && c < rx) ? evalE(j * n + kk + tx * c) : make_double2(0.0, 0.0);
+                    }
+                    d4v zr = d4v{0.0, 0.0, 0.0, 0.0}, zi = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const d2 av = wa[u], bv = ev[u];
+                        zr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, zr, 0, 0, 0);
+                        zr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, zr, 0, 0, 0);
+                        zi = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, zi, 0, 0, 0);
+                        zi = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, zi, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {   // lane l, reg rr -> Z_j[(l >> 4) + 4 rr][l & 15]
+                        const int i = (lane >> 4) + 4 * rr, c = lane & 15;
+                        if (i < tx && c < rx) emit(j * n + i + tx * c, make_double2(zr[rr], zi[rr]));
+                    }
+                }
+            } else {
             // the emit inputs (X, old Z, old N) of block j are requested with block j + 1's E
             d2 px[4], pz[4], pn[4];
             auto fetchP = [&](int j) {
@@ -303,6 +367,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
                 }
                 if (j + 1 < r) fetchP(j + 1);
                 __syncthreads();
+            }
             }
         } else {
             // Z = E: the element stream in batches of 4 per thread, loads issued before the stores

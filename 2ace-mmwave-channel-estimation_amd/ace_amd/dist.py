@@ -51,3 +51,43 @@ def gather_to_root(local, counts, group=None):
         return torch.cat([b[:c] for b, c in zip(bufs, counts)])
     dist.gather(send, gather_list=None, dst=0, group=group)
     return None
+
+
+class PendingGather:
+    """An in-flight gather_to_root (async_op): ``wait()`` orders the caller's stream after it and
+    returns the concatenation on rank 0 (None elsewhere)."""
+
+    def __init__(self, work, bufs, counts, complex_view):
+        self.work, self.bufs, self.counts, self.complex_view = work, bufs, counts, complex_view
+
+    def wait(self):
+        import torch
+        self.work.wait()
+        if self.bufs is None:
+            return None
+        out = torch.cat([b[:c] for b, c in zip(self.bufs, self.counts)])
+        return torch.view_as_complex(out.contiguous()) if self.complex_view else out
+
+
+def gather_to_root_async(local, counts, group=None):
+    """gather_to_root as an asynchronous collective, so that the transfer of one batch's results
+    overlaps the next batch's solve (the caller keeps ``local`` unchanged until ``wait()``)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(counts) != world:
+        raise ValueError("counts must have one entry per rank")
+    if local.shape[0] != counts[rank]:
+        raise ValueError(f"rank {rank}: local batch {local.shape[0]} != counts[{rank}] {counts[rank]}")
+    cplx = local.is_complex()
+    x = torch.view_as_real(local.contiguous()) if cplx else local
+    cmax = max(counts)
+    if x.shape[0] < cmax:
+        pad = torch.zeros((cmax - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        send = torch.cat([x, pad])
+    else:
+        send = x.contiguous()
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    work = dist.gather(send, gather_list=bufs, dst=0, group=group, async_op=True)
+    return PendingGather(work, bufs, counts, cplx)

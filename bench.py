@@ -266,6 +266,10 @@ PMC_KERNEL = {  # kernel-class -> kernel name prefix in the PMC profiles, per wo
 }
 PMC_KERNEL["nuclear"] = {"apply_G": "nms_kernel<false>"}   # the m-space iteration (ace_nucmsp.hip)
 PMC_KERNEL["config5"] = PMC_KERNEL["nuclear"]
+# pipeline / PhaseLift: the dominant class's largest kernel (one launch per class launch)
+PMC_KERNEL["pipeline"] = {"apply_AH": "zgemm3m_kernel<2, false", "apply_A": "zgemm3m_kernel<1, false",
+                          "apply_G": "zgemm3m_kernel<0, false", "zstep": "zstep_kernel<0, false, false>"}
+PMC_KERNEL["phaselift"] = {"zstep": "hetrd_kernel"}
 
 
 def _cpu_model():
@@ -315,10 +319,11 @@ def _prof_read(nclass=10):
     return list(kt), list(kn), list(kw)
 
 
-def work_roofline(kt, kn, kw, note):
+def work_roofline(kt, kn, kw, note, tag=None):
     """Roofline of the dominant kernel class among those whose launches carry an algorithmic flop
     count (ace_prof_work: the f64 GEMM-shaped applies and prox steps), plus every class's share
-    of the device time."""
+    of the device time.  With `tag`, `traffic` is the PMC HBM bytes per launch of the class's
+    largest kernel (PMC_KERNEL[tag]) from a profile of the same workload."""
     from ace_amd._lib import KERNEL_CLASSES
     tot = sum(kt)
     shares = {KERNEL_CLASSES[i]: round(kt[i] / tot, 4) for i in range(len(kt)) if kn[i]}
@@ -330,6 +335,11 @@ def work_roofline(kt, kn, kw, note):
     r = roofline_from(KERNEL_CLASSES[i], avg_s, {"f64": kw[i] / kn[i]}, note=note)
     r["launches"] = kn[i]
     r["device_time_share"] = shares[KERNEL_CLASSES[i]]
+    pmc = PMC_KERNEL.get(tag, {}).get(KERNEL_CLASSES[i]) if tag else None
+    tr = _pmc_traffic(pmc, tag) if pmc else None
+    if tr:
+        r["traffic"], r["traffic_source"] = tr
+        r["traffic_kernel"] = pmc
     return r, shares
 
 
@@ -389,7 +399,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     import ace_amd
     from ace_amd import infer_admm_batch, synth_problem
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
-    from ace_amd.dist import gather_to_root
+    from ace_amd.dist import gather_to_root_async
     import ctypes as C
 
     wl = workload or {}
@@ -403,17 +413,31 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     if wl.get("X0") is not None:
         X0 = wl["X0"]
     ws = ace_amd.solver.Workspace()
-    out = None
+    outs, pend, nstep = [None, None], [None, None], [0]
 
+    # The single result gather of recovered channels over RCCL/xGMI (north_star), asynchronous: the
+    # gather of step k overlaps the solve of step k + 1 (outputs double-buffered; a buffer is
+    # reused only after its gather has completed, and the timed region waits for the last one).
     def step():
-        nonlocal out
-        out = infer_admm_batch(A, B, X0, tx, tx, variant=variant, maxiter=args.iters, fixed_iters=True,
-                               out=out, workspace=ws)
-        if world > 1:   # the single result gather of recovered channels over RCCL/xGMI (north_star)
-            gather_to_root(out.X, counts)
+        i = nstep[0] & 1
+        if pend[i] is not None:
+            pend[i].wait()
+            pend[i] = None
+        outs[i] = infer_admm_batch(A, B, X0, tx, tx, variant=variant, maxiter=args.iters, fixed_iters=True,
+                                   out=outs[i], workspace=ws)
+        if world > 1:
+            pend[i] = gather_to_root_async(outs[i].X, counts)
+        nstep[0] += 1
+
+    def drain():
+        for i in range(2):
+            if pend[i] is not None:
+                pend[i].wait()
+                pend[i] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     _barrier(world)
     prof = not args.no_prof
@@ -425,9 +449,11 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     _barrier(world)
     elapsed = time.perf_counter() - t0
+    out = outs[(nstep[0] - 1) & 1]
     msp_steps = C.c_longlong(0)
     if prof:
         kt, kn, _ = _prof_read()
@@ -658,7 +684,7 @@ def bench_pipeline(args, dev, rank, world):
     if not args.no_prof:
         kt, kn, kw = _prof_read()
         roof, shares = work_roofline(kt, kn, kw, "f64 flops of the GEMM-shaped applies as launched (all batch*r "
-                                     "vectors of the stage, 8 per complex MAC; ace_prof_work)")
+                                     "vectors of the stage, 8 per complex MAC; ace_prof_work)", tag="pipeline")
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return
@@ -745,7 +771,7 @@ def bench_phaselift(args, dev, rank, world):
         roof, shares = work_roofline(
             kt, kn, kw, "algorithmic f64 flops per realisation in the backtracking step (8 per complex MAC) in "
             "the d = min(m, n) reduced coordinates: prox eig 17.3 d^3 (SURVEY.md §8d's count for a dense Hermitian "
-            "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2")
+            "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2", tag="phaselift")
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return

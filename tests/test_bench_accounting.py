@@ -109,3 +109,20 @@ def test_nms_bytes():
     assert r == {"f64": 8 * m * m, "hbm": b.nms_bytes(m)}
     assert b.unit_resources("zstep", m, 1024, variant="A2nuclear", pc=False, gyf=False, gyk=True, i8=True,
                             msp_frac=0.0, nms=True) == {}
+
+
+def test_work_roofline_attaches_class_kernel_traffic(tmp_path, monkeypatch):
+    import json
+    b = _bench()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r03_v9_phaselift_pmc_hbm.json").write_text(json.dumps({"hetrd_kernel": {"hbm_bytes": 5.0}}))
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    kt = [0.0] * 10
+    kn = [0] * 10
+    kw = [0.0] * 10
+    kt[8], kn[8], kw[8] = 100.0, 10, 1e12        # zstep class: the prox eig
+    r, shares = b.work_roofline(kt, kn, kw, "note", tag="phaselift")
+    assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "hetrd_kernel"
+    r, _ = b.work_roofline(kt, kn, kw, "note", tag="pipeline")
+    assert r["traffic"] is None

@@ -110,3 +110,44 @@ def test_config5_sharding_two_ranks_gloo():
     A = synth.multires_codebook(58659179, 32, rows)
     ref = np.stack([synth.measurements(7, c, A, synth.channel(7, c, 32, 32)) for c in range(total)])
     np.testing.assert_array_equal(got, ref)
+
+
+def _async_worker(rank, world, port, total, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ace_amd import synth
+        from ace_amd.dist import gather_to_root_async
+        counts = [shard_range(total, world, r)[1] for r in range(world)]
+        first, count = shard_range(total, world, rank)
+        _, _, _, H = synth.problem(4242, first, count, 16, 4, 4)
+        pend = [gather_to_root_async(torch.from_numpy(H), counts),              # two in flight at once
+                gather_to_root_async(torch.from_numpy(2 * H), counts)]
+        res = [p.wait() for p in pend]
+        if rank == 0:
+            out_q.put((res[0].numpy(), res[1].numpy()))
+        else:
+            assert res == [None, None]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_gather_two_ranks_gloo():
+    """bench.py's overlapped result gather (gather_to_root_async): two gathers in flight, ragged
+    shards, the same concatenation as the synchronous gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    total = 7
+    procs = [ctx.Process(target=_async_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    a, b = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from ace_amd import synth
+    _, _, _, H = synth.problem(4242, 0, total, 16, 4, 4)
+    np.testing.assert_array_equal(a, H)
+    np.testing.assert_array_equal(b, 2 * H)

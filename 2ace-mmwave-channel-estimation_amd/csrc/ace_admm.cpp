@@ -79,9 +79,10 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //   ACE_LEAN=0          the full one-wave Z-step every iteration (no zlean / certified pass)
 //   ACE_NUC_MSP=0       A2nuclear r = 1 in n-space (gyk / apply_AH / Z-step) instead of the m-space
 //                       iteration of ace_nucmsp.hip
+//   ACE_I8_STAGES=0     the r-column stages' A V, A^H g, K Y as f64 GEMMs instead of int8 digit planes
 struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1;
-    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true;
+    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true;
     double msp_room = 32.0;
 };
 static Knobs read_knobs() {
@@ -105,6 +106,7 @@ static Knobs read_knobs() {
     k.lazy_dual = on("ACE_LAZY_DUAL");
     k.lean = on("ACE_LEAN");
     k.nuc_msp = on("ACE_NUC_MSP");
+    k.i8r = on("ACE_I8_STAGES");
     return k;
 }
 static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192; }
@@ -631,7 +633,10 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // private phase-code codebooks: T, g = G T, Y-step, W = A^H g and the dual terms in one kernel
     const bool pc = !L.shared && L.pc_ok && r == 1 && zstep_takes_w(p.variant, r);
     const bool wmode = i8 || pc;
-    g_path[i8 ? 0 : pc ? 1 : L.shared ? 2 : 3].fetch_add(1, std::memory_order_relaxed);
+    // r-column stages on a shared phase-code A: A V, A^H g and K Y as exact int8 digit planes over
+    // the batch * r vectors (vector j of realisation j / r), G T and the rest unchanged
+    const bool i8r = !fast && L.shared && L.i8ok && kn.i8r && nv >= 256;
+    g_path[(i8 || i8r) ? 0 : pc ? 1 : L.shared ? 2 : 3].fetch_add(1, std::memory_order_relaxed);
     // pc_ok means K and G hold the code-image path's tiles, not the m x m matrices the generic path reads
     if (L.pc_ok && !pc) return fail(ACE_ERR_UNSUPPORTED, "private phase-code setup without its iteration path");
 
@@ -725,8 +730,17 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             ProfScope ps(ACE_K_APPLY_A, st, fl_mn);
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
         } else {
-            { ProfScope ps(ACE_K_PRE, st); launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, w.V, w.S, w.st, st); }
-            { ProfScope ps(ACE_K_APPLY_A, st, fl_mn); applyA(1, w.V, w.T, w.S); }   // T = S - A V
+            {
+                ProfScope ps(ACE_K_PRE, st);
+                launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, i8r ? nullptr : w.V, w.S, w.st, st);
+            }
+            if (i8r) {   // T = (Y - M/mu) - A (Z - N/mu) per vector, digit planes
+                ProfScope ps(ACE_K_APPLY_A, st);
+                launch_i8_apply_A(nv, n, m, L.LA8, w.Z, w.N, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, nullptr, st, r);
+            } else {
+                ProfScope ps(ACE_K_APPLY_A, st, fl_mn);
+                applyA(1, w.V, w.T, w.S);   // T = S - A V
+            }
         }
         if (pc) {
             // g, the Y-step, W = A^H g and the dual terms came from pgk_kernel
@@ -749,12 +763,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             }
         }
         if (!gyk && !pc) {   // K Y
-            ProfScope ps(ACE_K_APPLY_K, st, i8 ? 0.0 : fl_mm);
+            ProfScope ps(ACE_K_APPLY_K, st, (i8 || i8r) ? 0.0 : fl_mm);
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
+            else if (i8r) launch_i8_apply_K(nv, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st, r);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
         }
         if (!pc) {
-            ProfScope ps(ACE_K_APPLY_AH, st, wmode ? 0.0 : fl_mn);               // X = V + A^H g
+            ProfScope ps(ACE_K_APPLY_AH, st, (wmode || i8r) ? 0.0 : fl_mn);      // X = V + A^H g
             if (wmode) {
                 za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && kn.lean &&
                            it != p.maxiter && fuse_ok(kn, m);
@@ -769,7 +784,14 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 launch_i8_apply_AH(batch, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st, za.xfuse ? &za : nullptr);
             }
             else if (fused) launch_zgemm_fused(false, n, m, batch, L.AH, m, w.g, nullptr, m, w.X, w.Z, w.N, n, w.st, st);
-            else applyAH(w.g, w.X, w.V);
+            else if (i8r) {
+                ZArgs zv{};
+                zv.r = r;
+                zv.xzn = 1;
+                zv.Z = w.Z;
+                zv.N = w.N;
+                launch_i8_apply_AH(nv, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st, nullptr, &zv);
+            } else applyAH(w.g, w.X, w.V);
         }
         za.it = it;
         za.wmode = wmode;

@@ -191,9 +191,10 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
 // T = (Y - M/mu) - c A (Z - N/mu)   (A: m x n phase code, c = *cmax).  With AX != nullptr, a
 // 16-realisation block whose realisations all have RealState::avok takes A V = AX (the previous
 // Y-step's A X, X = V exactly) and skips the product.
+// rcols > 1: nb = batch * rcols vectors, vector j of realisation j / rcols (the r-column stages)
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
-                       const double* AX, hipStream_t st);
+                       const double* AX, hipStream_t st, int rcols = 1);
 // W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
 // fuse != nullptr: the steady-state Z-step runs in the epilogue (i8ah_kernel<false, true>)
 struct ZArgs;
@@ -267,7 +268,7 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);
 void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
-                       const RealState* rs, hipStream_t st);
+                       const RealState* rs, hipStream_t st, int rcols = 1);
 // Newton-Schulz start: Ap = I + K, Id = I, X0 = 2/(1 + b) I with b the Gershgorin bound of I + K.
 void launch_ns_prep(int m, const double* K, double* Ap, double* Id, double* X0, hipStream_t st, double* bnd);
 // out[0] = max |x_i| over n doubles
@@ -397,6 +398,7 @@ struct ZArgs {
     const double* optS;
     int matz;              // (launch_i8_msp_optx) the apply_AH launch forms opt_X = Z0 + A^H opt_S
     int msp_fail_it;       // (tests: ACE_MSP_FAIL_IT) the bound of m-space iterates fails at this iteration
+    int xzn;               // (apply_AH of the r-column stages) write X = (Z - N/mu) + A^H g instead of W
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

@@ -151,16 +151,18 @@ __device__ __forceinline__ void i8a_block(int nb, int Kc, int Mc, int nks, const
                                           double* __restrict__ Tp, int ldt, const double* __restrict__ cptr,
                                           const RealState* __restrict__ rs, const double* __restrict__ zeros,
                                           const double* __restrict__ AXp, int8_t (*As)[ROWS * RSA], double* sc_s,
-                                          double* imu_s, int* live_s, const int* avok_s, int j0, int cb) {
+                                          double* imu_s, int* live_s, const int* avok_s, int j0, int cb, int rc = 1) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: realisation bl, entry 32 s + cq
-    const bool live = jb < nb && !rs[jb].done;
-    const double imu = live ? 1.0 / rs[jb].mu : 0.0;
+    const int bl = t >> 5, cq = t & 31, jb = j0 + bl;   // staging role: vector bl, entry 32 s + cq
+    // vector jb belongs to realisation jb / rc (rc columns per realisation: the r-column stages)
+    const RealState* rj = rs + (jb < nb ? jb / rc : 0);
+    const bool live = jb < nb && !rj->done;
+    const double imu = live ? 1.0 / rj->mu : 0.0;
     const d2* z = reinterpret_cast<const d2*>(Zp) + (long long)(live ? jb : 0) * Kc;
-    const d2* nn = (live && rs[jb].nzero) ? reinterpret_cast<const d2*>(zeros)
-                                          : reinterpret_cast<const d2*>(Np) + (long long)(live ? jb : 0) * Kc;
+    const d2* nn = (live && rj->nzero) ? reinterpret_cast<const d2*>(zeros)
+                                       : reinterpret_cast<const d2*>(Np) + (long long)(live ? jb : 0) * Kc;
     double p2, sc;
-    plane_scale(live ? rs[jb].vbound : 0.0, *cptr, p2, sc);
+    plane_scale(live ? rj->vbound : 0.0, *cptr, p2, sc);
     if (cq == 0) {
         sc_s[bl] = sc;
         imu_s[bl] = imu;
@@ -267,18 +269,18 @@ __global__ __launch_bounds__(NT, 1) void i8a_kernel(int nb, int Kc, int Mc, int 
                                                     const double* __restrict__ Yp, const double* __restrict__ Mp,
                                                     double* __restrict__ Tp, const double* __restrict__ cptr,
                                                     const RealState* __restrict__ rs, const double* __restrict__ zeros,
-                                                    const double* __restrict__ AXp) {
+                                                    const double* __restrict__ AXp, int rc) {
     __shared__ __attribute__((aligned(16))) int8_t As[2][ROWS * RSA];
     __shared__ double sc_s[RB], imu_s[RB];
     __shared__ int live_s[RB], avok_s[RB];
     const int t = threadIdx.x, j0 = blockIdx.x * RB;
-    if (t < RB) {   // per realisation (the result never depends on the block it shares)
+    if (t < RB) {   // per vector (the result never depends on the block it shares)
         const int j = j0 + t;
-        avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;
+        avok_s[t] = AXp && j < nb && !rs[j].done && rs[j].avok;   // (r = 1 only: AXp is null otherwise)
     }
     __syncthreads();
     i8a_block<false>(nb, Kc, Mc, nks, Bf, Zp, Np, Yp, Mp, Tp, 0, cptr, rs, zeros, AXp, As, sc_s, imu_s, live_s, avok_s,
-                     j0, blockIdx.y);
+                     j0, blockIdx.y, rc);
 }
 
 // apply_AH in the Z-step's wmode:  W = c A^H g  (K = m complex, outputs n complex).
@@ -314,7 +316,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                                           const double* __restrict__ Gp, double* __restrict__ Wp,
                                           const double* __restrict__ cptr, const RealState* __restrict__ rs,
                                           const ZArgs& za, int8_t* Ad, double* zsum, const d2* gl, int gst) {
-    __shared__ double sc_s[RB];
+    __shared__ double sc_s[RB], imu_s[RB];
     __shared__ int live_s[RB];
     __shared__ FuseState fs_s[FUSE ? RB : 1];
     __shared__ int z0_s[(!FUSE && !KY) ? RB : 1];
@@ -328,7 +330,10 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     // m-space realisations (RealState::mzit, set by gyk_body of this launch) need no pass; the
     // matz launch (launch_i8_msp_optx) takes exactly the realisations with opt_X in m-space form
     const bool matz = !FUSE && !KY && za.matz;
-    const bool live = jb < nb && (matz ? rs[jb].optsrc == 3 : (!rs[jb].done && !(za.msp && rs[jb].mzit == za.it)));
+    // r-column stages (za.r > 1, !FUSE): vector jb belongs to realisation jb / r
+    const int rc = (!FUSE && za.r > 1) ? za.r : 1;
+    const bool live = jb < nb && (matz ? rs[jb].optsrc == 3
+                                       : (!rs[jb / rc].done && !(za.msp && rs[jb / rc].mzit == za.it)));
     // a block none of whose realisations needs the pass (all settled in m-space, done, or past nb)
     // skips it whole (uniform across the work-group)
     if (!__syncthreads_or(live)) return;
@@ -391,6 +396,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     if (cp == 0) {
         sc_s[bl] = sc;
         live_s[bl] = live;
+        imu_s[bl] = (!KY && !FUSE && za.xzn && live) ? 1.0 / rs[jb / rc].mu : 0.0;
     }
     for (int s = 0; s < nst; ++s) {
         d2 x0, x1;
@@ -519,6 +525,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                     const long long off = (long long)j * ldo + col;
                     const double wv = scb * recombine(acc[R][c], q);
                     if (matz) Wp[off] = (z0_s[blo] == 1 ? za.Z : za.Zn)[off] + wv;   // Z0 + A^H opt_S
+                    else if (za.xzn) Wp[off] = fma(-za.N[off], imu_s[blo], za.Z[off]) + wv;   // X = V + A^H g
                     else Wp[off] = wv;
                 }
             }
@@ -1366,10 +1373,10 @@ size_t i8ah_fuse_lds_bytes() { return (size_t)8 * 8 * 2 * 64 * sizeof(double); }
 
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
-                       const double* AX, hipStream_t st) {
+                       const double* AX, hipStream_t st, int rcols) {
     dim3 grid((nb + RB - 1) / RB, i8_ncols(m) / NCB, 1), block(NT);
     hipLaunchKernelGGL(i8a_kernel, grid, block, 0, st, nb, n, m, i8_nks(n), reinterpret_cast<const i4v*>(LA), Z, N,
-                       Y, M, T, cmax, rs, zeros, AX);
+                       Y, M, T, cmax, rs, zeros, AX, rcols < 1 ? 1 : rcols);
 }
 size_t i8k_frag_bytes(int m) { return (size_t)2 * ((2 * m + NCB / 2 - 1) / (NCB / 2)) * (NCB / 2) * i8_nks(m) * 32; }
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st) {
@@ -1378,15 +1385,17 @@ void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, i
                        i8_nks(m), flag);
 }
 void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
-                       const RealState* rs, hipStream_t st) {
+                       const RealState* rs, hipStream_t st, int rcols) {
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<true, false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
     }();
     (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
+    ZArgs za{};
+    za.r = rcols;
     hipLaunchKernelGGL((i8ah_kernel<true, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
-                       reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs, ZArgs{});
+                       reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs, za);
 }
 size_t gyk_gfrag_bytes(int m) { return (size_t)gyk_mp(m) * gyk_mp(m) * 16; }
 size_t gyk_lds_bytes(int m) {   // Ts, then the Ad region: K Y digit planes, or apply_A's digit stages

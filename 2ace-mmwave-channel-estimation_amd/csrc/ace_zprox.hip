@@ -452,8 +452,10 @@ __global__ __launch_bounds__(256) void pre_kernel(int n, int m, const double* Zp
     const double imu = 1.0 / st[b].mu;
     const d2* Z = reinterpret_cast<const d2*>(Zp) + (long long)b * n;
     const d2* N = reinterpret_cast<const d2*>(Np) + (long long)b * n;
-    d2* V = reinterpret_cast<d2*>(Vp) + (long long)b * n;
-    for (int k = threadIdx.x; k < n; k += blockDim.x) V[k] = csub(Z[k], cscale(N[k], imu));
+    if (Vp) {   // (the int8 r-column stages form V inside their applies: S only)
+        d2* V = reinterpret_cast<d2*>(Vp) + (long long)b * n;
+        for (int k = threadIdx.x; k < n; k += blockDim.x) V[k] = csub(Z[k], cscale(N[k], imu));
+    }
     const d2* Y = reinterpret_cast<const d2*>(Yp) + (long long)b * m;
     const d2* M = reinterpret_cast<const d2*>(Mp) + (long long)b * m;
     d2* S = reinterpret_cast<d2*>(Sp) + (long long)b * m;

@@ -115,11 +115,13 @@ def test_pipeline_batch_invariance(gpu):
         assert np.array_equal(one.stage_iters[0], full.stage_iters[b])
 
 
-def test_pipeline_concurrent_restarts_match_serial(gpu):
+def test_pipeline_concurrent_restarts_match_serial(gpu, monkeypatch):
     """Up to 16 realisations the restarts run concurrently (own stream and workspace copy each,
     best of restarts taken in restart order afterwards); above, one after another.  A realisation's
-    result is the same bit for bit either way: batch 17 (serial) against batch 1 (concurrent)."""
+    result is the same bit for bit either way: batch 17 (serial) against batch 1 (concurrent), both
+    on the f64 stage applies (batch 17 x r 20 would otherwise take the int8 ones)."""
     from ace_amd import infer_low_rank_pipeline_host, synth, draw_partitions
+    monkeypatch.setenv("ACE_I8_STAGES", "0")
     A, B, _, _ = synth.problem(61, 0, 17, 64, 16, 16)
     tr = draw_partitions(np.random.default_rng(61), 64, 3)
     full = infer_low_rank_pipeline_host(A[0], B, 16, 16, tr)
@@ -128,6 +130,24 @@ def test_pipeline_concurrent_restarts_match_serial(gpu):
         assert np.array_equal(one.X[0], full.X[b])
         assert np.array_equal(one.stage_iters[0], full.stage_iters[b])
         assert one.quality[0] == full.quality[b] and one.status[0] == full.status[b]
+
+
+def test_pipeline_int8_stage_applies(gpu, monkeypatch):
+    """With at least 256 vectors (batch x r) on a phase-code codebook the r-column stages run A V,
+    A^H g and K Y as exact int8 digit planes (ACE_I8_STAGES, default on): the same results as the
+    f64 GEMMs to rounding, identical stage iteration counts (32-ant, m = 256, 16 realisations)."""
+    from ace_amd import infer_low_rank_pipeline_host, synth, draw_partitions, path_counts
+    A, B, _, _ = synth.problem(67, 0, 16, 256, 32, 32)
+    tr = draw_partitions(np.random.default_rng(67), 256, 3)
+    path_counts(reset=True)
+    a = infer_low_rank_pipeline_host(A[0], B, 32, 32, tr, maxiter=120)
+    assert path_counts()["int8_shared"] > 0
+    monkeypatch.setenv("ACE_I8_STAGES", "0")
+    f = infer_low_rank_pipeline_host(A[0], B, 32, 32, tr, maxiter=120)
+    assert np.array_equal(a.stage_iters, f.stage_iters), (a.stage_iters, f.stage_iters)
+    for b in range(16):
+        assert O.phase_aligned_rel_err(a.X[b], f.X[b]) <= 1e-8, b
+    np.testing.assert_allclose(a.quality, f.quality, rtol=0, atol=1e-10)
 
 
 def test_pipeline_matlab_signature(gpu):

@@ -26,7 +26,7 @@ ACE_ST_NO_OPT = 2
 ACE_ST_EIG_NOCONV = 4
 ACE_ST_ROLLBACK = 8
 
-KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final"]
+KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final", "msr"]
 
 
 class AceError(RuntimeError):

@@ -17,6 +17,7 @@
 #include "ace_host.hpp"
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <utility>
 #include <vector>
@@ -80,8 +81,12 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //   ACE_NUC_MSP=0       A2nuclear r = 1 in n-space (gyk / apply_AH / Z-step) instead of the m-space
 //                       iteration of ace_nucmsp.hip
 //   ACE_I8_STAGES=0     the r-column stages' A V, A^H g, K Y as f64 GEMMs instead of int8 digit planes
+//   ACE_MSR=0           no m-space runs (msr_kernel): every iteration as its own launches
+//   ACE_MSR_START=<it>  first iteration at which an m-space run is tried (default 56)
+//   ACE_MSR_RETRY=<k>   after a run stopped early, the next try k iterations after its resume point
 struct Knobs {
-    int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1;
+    int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8;
+    bool msr = true;
     bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true;
     double msp_room = 32.0;
 };
@@ -107,7 +112,19 @@ static Knobs read_knobs() {
     k.lean = on("ACE_LEAN");
     k.nuc_msp = on("ACE_NUC_MSP");
     k.i8r = on("ACE_I8_STAGES");
+    k.msr = on("ACE_MSR");
+    k.msr_start = (int)num("ACE_MSR_START", 56);
+    k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
+    if (k.msr_retry < 1) k.msr_retry = 1;
     return k;
+}
+// ACE_MSR_TRACE=1: one stderr line per m-space run (resume point, steps, exit reasons)
+static bool msr_trace() {
+    static const bool v = [] {
+        const char* e = getenv("ACE_MSR_TRACE");
+        return e && e[0] == '1';
+    }();
+    return v;
 }
 static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192; }
 static bool gyf_ok(const Knobs& k, int m) { return k.gyf && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN; }
@@ -443,8 +460,67 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 if (k != h) ACE_HIP(hipStreamWaitEvent(ss[h], cev[k], 0));
         return ACE_OK;
     };
+    // m-space runs (msr_kernel): from iteration msr_next on, a steady-state block of every sub-batch
+    // iterates inside one launch; the per-iteration launches resume where the runs left off
+    const bool msr = msp && kn.msr && kn.gyf_ctl && msr_supported(m) && gyf_ok(kn, m) && fuse_ok(kn, m);
+    int msr_next = kn.msr_start;
     int q = 0, rc = ACE_OK;
     for (int it = 1; it <= p.maxiter && rc == ACE_OK; ++it) {
+        // an m-space run starts only when every live realisation can enter it (a block left out would
+        // hold the per-iteration launches for itself while the run occupies the stream): the readiness
+        // count is read back (the host waits for iteration it - 1), else the next check comes later
+        bool run_msr = false;
+        if (msr && it >= msr_next && it < p.maxiter) {
+            for (int h = 1; h < nsplit; ++h) {
+                ACE_HIP(hipEventRecord(cev[h], ss[h]));
+                ACE_HIP(hipStreamWaitEvent(st, cev[h], 0));
+            }
+            ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 28), 0, 1, st));
+            launch_msr_ready(batch, w.st, it, w.done + 28, st);
+            int nr = 0;
+            ACE_HIP(read_back(&nr, w.done + 28, sizeof(int), st));
+            run_msr = nr == 0;
+            if (!run_msr) msr_next = it + kn.msr_retry;
+        }
+        if (run_msr) {
+            int pidx[4] = {-1, -1, -1, -1};
+            for (int h = 0; h < nsplit; ++h) {
+                if (nb[h] == 0) continue;
+                const AdmmState& wh = ws[h];
+                ZArgs za = za0;
+                za.it = it;
+                za.st = wh.st;
+                za.msp = 1;
+                za.msp_fail_it = kn.msp_fail_it;
+                za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
+                const MsrArgs ma{L.Gf, B + (long long)h * chunk * m, {wh.Y[0], wh.Y[1]}, wh.M, wh.AX,
+                                 {wh.Sg[0], wh.Sg[1]}, wh.optS, wh.optY, wh.st, w.done + 8 + h, w.done + 1,
+                                 w.done + 12 + 4 * h, nb[h], m, it, p.maxiter};
+                ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 8 + h), p.maxiter, 1, ss[h]));
+                ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 12 + 4 * h), 0, 4, ss[h]));
+                ProfScope ps(ACE_K_MSR, ss[h]);
+                pidx[h] = ps.idx;
+                launch_msr(ma, za, ss[h]);
+            }
+            for (int h = 1; h < nsplit; ++h) {   // (the caller's stream waits for the sub-batches)
+                ACE_HIP(hipEventRecord(cev[h], ss[h]));
+                ACE_HIP(hipStreamWaitEvent(st, cev[h], 0));
+            }
+            int rv[20] = {p.maxiter, p.maxiter, p.maxiter, p.maxiter};   // resume [4], then [4] per sub-batch
+            ACE_HIP(read_back(rv, w.done + 8, sizeof(int) * 20, st));
+            for (int h = 0; h < nsplit; ++h) {   // algorithmic flops of the run: 8 m^2 per realisation-iteration
+                if (pidx[h] >= 0) g_prof.work[pidx[h]] = 8.0 * m * m * rv[4 + 4 * h];
+                if (msr_trace())
+                    fprintf(stderr, "msr h %d it %d: resume %d steps %d notready %d fail %d pend %d\n", h, it, rv[h],
+                            rv[4 + 4 * h], rv[5 + 4 * h], rv[6 + 4 * h], rv[7 + 4 * h]);
+            }
+            int e = p.maxiter;
+            for (int h = 0; h < nsplit; ++h)
+                if (nb[h] > 0) e = std::min(e, std::max(it, rv[h]));
+            it = e;                 // the per-iteration launches run from here (blocks ahead skip)
+            q = (it - 1) & 1;
+            msr_next = e + kn.msr_retry;
+        }
         const bool csync = nsplit > 1 && it <= cold_sync;
       for (int phase = 0; phase < (csync ? 2 : 1); ++phase) {
         const int pmask = csync ? (1 << phase) : 3;   // bit 0: the g launch, bit 1: the Z-step

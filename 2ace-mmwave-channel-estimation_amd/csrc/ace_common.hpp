@@ -75,6 +75,9 @@ struct RealState {
     // optsrc = 3: opt_X = Z0 + A^H opt_S; 4 / 5: the same with opt_S still in the S ping-pong
     // buffer Sg[0] / Sg[1] (deferred like opt_Y: copied only before that buffer is overwritten).
     int32_t msp, mzit, z0id, msp_pad;   // msp_pad: the entry iteration it0
+    // m-space run (msr_kernel) that left this realisation's block ahead of the per-iteration launches:
+    // the first iteration those must run for the block (its resume point)
+    int32_t mres, mres_pad_[3];
     // A2nuclear m-space iteration (ace_nucmsp.hip): Z = na X_init + A^H zeta, N = nbeta X_init +
     // A^H nu; nx0 = ||X_init||^2; the X_init coefficients of the best / last iterate
     // A2nuclear m-space iteration (ace_nucmsp.hip): E_prev = na X_init + A^H e, Z = naz E_prev,
@@ -264,6 +267,30 @@ size_t gyf_lds_bytes(int m);
 // ctl = 0: the Z-step launch, not gyf_kernel, runs the m-space control (ACE_GYF_CTL, A/B)
 void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, int ctl,
                 hipStream_t st);
+// m-space run (ace_i8gemm.hip::msr_kernel): gyf_kernel's m-space iteration for iterations it0 ..
+// it_end - 1 in one launch, per 16-realisation block whose live realisations are all in the m-space
+// form; the state is read from / written back to the buffers of the per-iteration launches
+// (Y[it & 1], S[it & 1] hold iterate it), and *resume gets the first iteration they must run.
+struct MsrArgs {
+    const double* Gf;
+    const double* B;
+    double* Y[2];
+    double* M;
+    double* AX;
+    double* S[2];
+    double* optS;
+    double* optY;
+    RealState* rs;
+    int* resume;     // atomicMin target (the caller sets it to it_end)
+    int* mspcount;   // m-space step counter (ace_prof_msp_steps)
+    int* steps;      // [4]: realisation-iterations this launch ran (bench accounting); blocks not ready,
+                     // runs stopped by a failed bound, by a pending test (diagnostics); the caller zeroes them
+    int nb, m, it0, it_end;
+};
+bool msr_supported(int m);
+// *notready += live realisations of the batch an m-space run from `it` could not take
+void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStream_t st);
+void launch_msr(const MsrArgs& a, const ZArgs& za, hipStream_t st);
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);

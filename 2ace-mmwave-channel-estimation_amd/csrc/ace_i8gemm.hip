@@ -677,6 +677,51 @@ struct GSet {
     d2 f[GSK][2];
 };
 
+// One output of the fused Y-step (ArgMinY with its zero guard, inferLowRankV4_multi.m:511-533, and
+// the M update): g from the 3M accumulators, AX = (Y - M/mu) - g, Y', M', and the five sums plus the
+// max |Y'| (with its NaN-sticky term) into v[0..6].  Shared by gyk_body and msr_kernel, so that the
+// two kernels form every iterate with the same operations in the same order: no multiply-add
+// contraction here (the compiler's fusion choices depend on the basic blocks around an inlined copy).
+__device__ __forceinline__ void ystep_elem(double e1, double e2, double e3, double mu, d2 mii, d2 yo, double Bi,
+                                           d2& gv, d2& ax, d2& mn, d2& y, double (&v)[9]) {
+#pragma clang fp contract(off)
+    // (written out in scalars: the pragma governs only the operations spelled here, not those of
+    // the complex helpers)
+    gv = make_double2(e1 - e2, e3 - e1 - e2);
+    const double imu = 1.0 / mu;
+    const double pr = mii.x * imu, pi = mii.y * imu;   // M / mu
+    ax = make_double2((yo.x - pr) - gv.x, (yo.y - pi) - gv.y);
+    double cr = ax.x + pr, ci = ax.y + pi;
+    double d = sqrt(cr * cr + ci * ci);
+    if (d == 0.0) {   // ArgMinY zero guard (:516-520 / :524-528)
+        cr = 1.0;
+        ci = 0.0;
+        d = 1.0;
+    }
+    const double f = (Bi / d + mu) / (1.0 + mu);
+    y = make_double2(cr * f, ci * f);
+    const double jr = ax.x - y.x, ji = ax.y - y.y;
+    mn = make_double2(mii.x + jr * mu, mii.y + ji * mu);
+    const double aax = sqrt(ax.x * ax.x + ax.y * ax.y) - Bi;
+    v[0] += aax * aax;
+    v[1] += ax.x * ax.x + ax.y * ax.y;
+    v[2] += y.x * y.x + y.y * y.y;
+    v[3] += jr * jr + ji * ji;
+    const double dr = y.x - yo.x, di = y.y - yo.y;
+    v[4] += dr * dr + di * di;
+    const double ay = fmax(fabs(y.x), fabs(y.y));
+    v[5] = fmax(v[5], ay);
+    v[6] += 0.0 * (fabs(y.x) + fabs(y.y));   // NaN / Inf sticky
+}
+// m-space sums of one output (RealState::msp): Re (A Z)^H g with A Z = A V = (Y - M/mu) - T (T's
+// input), and g^H K g = Re g^H (T - g), into v[7], v[8] (no contraction, as ystep_elem)
+__device__ __forceinline__ void msp_sums_elem(d2 yo, d2 mii, double imu, d2 tv, d2 gv, double (&v)[9]) {
+#pragma clang fp contract(off)
+    const double ar = (yo.x - mii.x * imu) - tv.x, ai = (yo.y - mii.y * imu) - tv.y;
+    v[7] += ar * gv.x + ai * gv.y;
+    v[8] += gv.x * (tv.x - gv.x) + gv.y * (tv.y - gv.y);
+}
+
 template <bool GLDS>   // g stays in the LDS rows of T for the fused apply_AH (gyf_kernel) instead of a.g
 __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsigned char* smem, const ZArgs& za,
                                          int za_ctl) {
@@ -1026,31 +1071,17 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             const int jl = (lane >> 4) + 4 * r, j = j0 + jl, i = 16 * ct + (lane & 15);
             if (ct >= nct || i >= m || !live_s[jl]) continue;
             const long long off = (long long)j * m + i;
-            const double e1 = p1[c][r], e2 = p2[c][r];
-            const d2 gv = make_double2(e1 - e2, p3[c][r] - e1 - e2);
-            const double mu = muv[r], imu = 1.0 / mu;
+            const double mu = muv[r];
             const d2 mii = mi[c][r], yo = yov[c][r];
-            const double Bi = biv[c][r];
-            const d2 ax = csub(csub(yo, cscale(mii, imu)), gv);
-            d2 cc = cadd(ax, cscale(mii, imu));
-            double d = sqrt(cabs2(cc));
-            if (d == 0.0) {   // ArgMinY zero guard (:516-520 / :524-528)
-                cc = make_double2(1.0, 0.0);
-                d = 1.0;
-            }
-            const double f = (Bi / d + mu) / (1.0 + mu);
-            const d2 y = cscale(cc, f);
-            const d2 jv = csub(ax, y);
+            d2 gv, ax, mn, y;
+            ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mii, yo, biv[c][r], gv, ax, mn, y, v7[r]);
             if constexpr (!GLDS) reinterpret_cast<d2*>(a.g)[off] = gv;
             if (a.AX) reinterpret_cast<d2*>(a.AX)[off] = ax;
-            reinterpret_cast<d2*>(a.M)[off] = cadd(mii, cscale(jv, mu));
+            reinterpret_cast<d2*>(a.M)[off] = mn;
             reinterpret_cast<d2*>(a.Yn)[off] = y;
             if constexpr (GLDS) {
                 if (msp_s[jl]) {   // m-space candidate: Re (A Z)^H g, g^H K g = Re g^H (T - g), S' = S + g
-                    const d2 tv = Ts[jl * tst + i];
-                    const d2 av = csub(csub(yo, cscale(mii, imu)), tv);   // A V = A Z (T's input)
-                    v7[r][7] += av.x * gv.x + av.y * gv.y;
-                    v7[r][8] += gv.x * (tv.x - gv.x) + gv.y * (tv.y - gv.y);
+                    msp_sums_elem(yo, mii, 1.0 / mu, Ts[jl * tst + i], gv, v7[r]);
                     const d2 so = ent_s[jl] ? make_double2(0.0, 0.0) : sov[c][r];
                     d2* sn = reinterpret_cast<d2*>(a.Snew) + off;
                     // deferred opt_S (RealState::optsrc 4 / 5): the best iterate's S is the one this
@@ -1062,15 +1093,6 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             } else {
                 Ts[jl * tst + i] = y;
             }
-            const double aax = sqrt(cabs2(ax)) - Bi;
-            v7[r][0] += aax * aax;
-            v7[r][1] += cabs2(ax);
-            v7[r][2] += cabs2(y);
-            v7[r][3] += cabs2(jv);
-            v7[r][4] += cabs2(csub(y, yo));
-            const double ay = fmax(fabs(y.x), fabs(y.y));
-            v7[r][5] = fmax(v7[r][5], ay);
-            v7[r][6] += 0.0 * (fabs(y.x) + fabs(y.y));   // NaN / Inf sticky
         }
     }
 #ifdef ACE_GYK_PROBE_P1
@@ -1305,6 +1327,13 @@ __host__ __device__ __forceinline__ size_t gyf_ts_bytes(int m) { return ((size_t
 __global__ __launch_bounds__(NT, 1) void gyf_kernel(int nb, int m, int n, GykArgs a, const i4v* __restrict__ LAH,
                                                     double* __restrict__ Wp, ZArgs za, size_t ad_bytes, int za_ctl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // msr_kernel already ran this iteration (and possibly later ones) for every live realisation
+    // of the block (RealState::mzit >= it): nothing to do (never the case in the regular flow)
+    {
+        const int j = blockIdx.x * GRB + (int)threadIdx.x;
+        const bool behind = threadIdx.x < GRB && j < nb && !a.rs[j].done && a.rs[j].mzit < a.it;
+        if (!__syncthreads_or(behind)) return;
+    }
     gyk_body<true>(nb, m, a, smem, za, za_ctl);
     __syncthreads();
     const size_t ts = gyf_ts_bytes(m);
@@ -1312,6 +1341,341 @@ __global__ __launch_bounds__(NT, 1) void gyf_kernel(int nb, int m, int n, GykArg
     double* zsum = reinterpret_cast<double*>(ts >= (size_t)8 * 8 * 2 * 64 * sizeof(double) ? smem : smem + ts + ad_bytes);
     i8ah_body<false, true, true>(nb, m, n, i8_nks_dev(m), LAH, nullptr, Wp, a.c8, a.rs, za, Ad, zsum,
                                  reinterpret_cast<const d2*>(smem), gyk_mp(m) + 1);
+}
+
+// ---- m-space run (msr_kernel): the m-space steady state of gyf_kernel (RealState::msp) iterated
+// inside one launch.  Once every live realisation of a 16-realisation block is in the m-space form,
+// an iteration is T = (Y - M/mu) - AX, g = G T, the Y-step, S' = S + g and the certified control
+// (fused_control): no n-vector, no Z-step, and nothing of one realisation that another needs.  The
+// work-group keeps Y, M, AX and B of its 16 realisations in registers and S in LDS across
+// iterations, so an iteration moves no per-realisation state through HBM (only G, from L2), and there
+// is no launch boundary between iterations.  The arithmetic is gyf_kernel's (same T expression, the
+// same MFMA sequence for g, ystep_elem / msp_sums_elem, the same reduction order, fused_control), so
+// the iterates are bit-identical to the per-iteration launches.  The run stops at it_end, or after
+// the iteration in which some realisation's bound fails (its Z-step must run: resume = it) or its
+// convergence test is left pending (the next gyf_kernel finishes it: resume = it + 1); it then writes
+// the state back where the per-iteration launches expect it, and *resume gets the smallest
+// iteration the regular launches must run from.  A block that is not entirely in the m-space form
+// at it0 returns at once (resume = it0).  Stopped realisations (convergence mode) write their state
+// back at the stop and drop out.
+constexpr int MGSK = 2;   // G T pipeline depth here (registers hold the state; the k order is gyk_body's)
+__host__ __device__ __forceinline__ size_t msr_lds_bytes() { return (size_t)GRB * 257 * 16 + (size_t)8 * NT * 16; }
+__global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int mp = 256, tst = mp + 1, nct = mp / 16, nks = mp / 4, nstage = nks / MGSK;
+    d2* Ts = reinterpret_cast<d2*>(smem);        // [16][tst]: T
+    d2* Ss = Ts + GRB * tst;                     // [8][NT]: S of the thread's 8 outputs (thread-private)
+    __shared__ double red[8][GRB][9];
+    __shared__ double mu_s[GRB];
+    __shared__ int live_s[GRB], flg_s[GRB];
+    __shared__ RealState rsl[GRB];   // the block's control blocks for the run (written back at its end)
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, j0 = blockIdx.x * GRB, m = a.m;
+    int bad = 0, ahead = 0, res = 0x7fffffff;
+    if (t < GRB) {
+        const int j = j0 + t;
+        const bool lv = j < a.nb && !a.rs[j].done;
+        live_s[t] = lv;
+        mu_s[t] = lv ? a.rs[j].mu : 1.0;
+        int fl = 0;
+        if (lv) {
+            RealState& r = a.rs[j];
+            ahead = r.mzit >= a.it0;   // an earlier run took the block past it0: its resume point stands
+            res = r.mres;
+            bad = !r.msp || r.dpend || r.mzit != a.it0 - 1 || r.zit != a.it0 - 1;
+            // deferred best iterates (opt_Y in a Y buffer, opt_S in an S buffer) go to opt_Y / opt_S
+            // now: the run keeps Y and S on chip and writes an improved iterate straight there
+            if (!bad) {
+                if (r.optysrc == 1 || r.optysrc == 2) fl |= r.optysrc;
+                if (r.optsrc == 4 || r.optsrc == 5) fl |= (r.optsrc - 3) << 2;
+            }
+        }
+        flg_s[t] = fl;
+    }
+    if (__syncthreads_or(ahead)) {
+        if (t < GRB && ahead) atomicMin(a.resume, res);
+        return;
+    }
+    if (__syncthreads_or(bad)) {
+        if (t == 0) {
+            atomicMin(a.resume, a.it0);
+            atomicAdd(a.steps + 1, 1);   // (diagnostics: blocks not ready at it0)
+        }
+        return;
+    }
+    if (!__syncthreads_or(t < GRB && live_s[t])) return;
+    // the thread's outputs: realisation jl(r) = (lane >> 4) + 4 r, entry i(c) = 16 (2 w + c) + (lane & 15)
+    // (the f64 MFMA accumulator map of g = G T)
+    bool lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lv[r] = live_s[(lane >> 4) + 4 * r];
+    auto off = [&](int r, int c) -> long long {
+        return (long long)(lv[r] ? j0 + (lane >> 4) + 4 * r : j0) * m + 16 * (2 * w + c) + (lane & 15);
+    };
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int fl = flg_s[(lane >> 4) + 4 * r];
+        if (!lv[r] || !fl) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (fl & 3) reinterpret_cast<d2*>(a.optY)[off(r, c)] = reinterpret_cast<const d2*>(a.Y[(fl & 3) - 1])[off(r, c)];
+            if (fl >> 2) reinterpret_cast<d2*>(a.optS)[off(r, c)] = reinterpret_cast<const d2*>(a.S[(fl >> 2) - 1])[off(r, c)];
+        }
+    }
+    if (t < GRB && live_s[t]) {
+        rsl[t] = a.rs[j0 + t];
+        if (flg_s[t] & 3) rsl[t].optysrc = 0;
+        if (flg_s[t] >> 2) rsl[t].optsrc = 3;
+    }
+    // state of iterate it0 - 1
+    d2 yv[2][4], mv[2][4], xv[2][4];
+    double bv[2][4];
+    {
+        const int p = (a.it0 - 1) & 1;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long long o = off(r, c);
+                yv[c][r] = reinterpret_cast<const d2*>(a.Y[p])[o];
+                mv[c][r] = reinterpret_cast<const d2*>(a.M)[o];
+                xv[c][r] = reinterpret_cast<const d2*>(a.AX)[o];
+                bv[c][r] = a.B[o];
+                Ss[(4 * c + r) * NT + t] = reinterpret_cast<const d2*>(a.S[p])[o];
+            }
+    }
+    __syncthreads();   // (every thread is done with the flush flags)
+    if (t < GRB) flg_s[t] = 0;
+    const d2* gp0 = reinterpret_cast<const d2*>(a.Gf) + (long long)(2 * w) * 64 + lane;
+    const d2* gp1 = reinterpret_cast<const d2*>(a.Gf) + (long long)(2 * w + 1) * 64 + lane;
+    const d2* trow = Ts + (lane & 15) * tst + (lane >> 4);
+    int cnt = 0;   // m-space steps of realisation t (ace_prof_msp_steps)
+    bool mylive = t < GRB && live_s[t] && !(flg_s[t] & 4);
+    // best iterates, deferred like gyf_kernel's opt_Y / opt_S: the previous iterate's Y (in yv) and S
+    // (in Ss) are written out only when the next iterate does not improve on them (or the run ends)
+    bool pbY = false, pbS = false;
+#ifdef ACE_MSR_STAMPS   // phase times of block 5, summed over its iterations (10 ns units)
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memrealtime();
+#define MSR_STAMP(k) do { if (blockIdx.x == 5 && t == 0) { const unsigned long long tn = __builtin_amdgcn_s_memrealtime(); ph[k] += tn - tp; tp = tn; } } while (0)
+#else
+#define MSR_STAMP(k)
+#endif
+    for (int it = a.it0;; ++it) {
+        // T = (Y - M/mu) - AX (gyk_body's t_from expression)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int jl = (lane >> 4) + 4 * r;
+            const double im = lv[r] ? 1.0 / mu_s[jl] : 0.0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                d2 v = make_double2(0.0, 0.0);
+                if (lv[r])
+                    v = make_double2(fma(-mv[c][r].x, im, yv[c][r].x) - xv[c][r].x,
+                                     fma(-mv[c][r].y, im, yv[c][r].y) - xv[c][r].y);
+                Ts[jl * tst + 16 * (2 * w + c) + (lane & 15)] = v;
+            }
+        }
+        __syncthreads();
+        MSR_STAMP(0);
+        // g = G T: gyk_body's 3M product, the same k order
+        d4v p1[2], p2[2], p3[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) p1[c] = p2[c] = p3[c] = d4v{0.0, 0.0, 0.0, 0.0};
+        {
+            struct GS {
+                d2 f[MGSK][2];
+            };
+            struct TS {
+                d2 v[MGSK];
+            };
+            auto gload = [&](GS& gs, int s) {
+#pragma unroll
+                for (int kk = 0; kk < MGSK; ++kk) {
+                    const long long ks = min(MGSK * s + kk, nks - 1);
+                    gs.f[kk][0] = gp0[ks * nct * 64];
+                    gs.f[kk][1] = gp1[ks * nct * 64];
+                }
+            };
+            auto tload = [&](TS& ts, int s) {
+                const int s2 = min(s, nstage - 1);
+#pragma unroll
+                for (int kk = 0; kk < MGSK; ++kk) ts.v[kk] = trow[4 * (MGSK * s2 + kk)];
+            };
+            auto gcomp = [&](const GS& gs, const TS& ts) {
+#pragma unroll
+                for (int kk = 0; kk < MGSK; ++kk) {
+                    const d2 v = ts.v[kk];
+                    const double ar = v.x, ai = v.y, as = v.x + v.y;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const d2 l = gs.f[kk][c];
+                        p1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, l.x, p1[c], 0, 0, 0);
+                        p2[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, l.y, p2[c], 0, 0, 0);
+                        p3[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(as, l.x + l.y, p3[c], 0, 0, 0);
+                    }
+                }
+            };
+            GS gA, gB;
+            TS tA, tB;
+            gload(gA, 0);
+            tload(tA, 0);
+            for (int s = 0; s < nstage; s += 2) {
+                gload(gB, s + 1);
+                tload(tB, s + 1);
+                __builtin_amdgcn_sched_barrier(0);
+                gcomp(gA, tA);
+                __builtin_amdgcn_sched_barrier(0);
+                gload(gA, s + 2);
+                tload(tA, s + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                gcomp(gB, tB);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        MSR_STAMP(1);
+        MSR_STAMP(2);
+        // Y-step and m-space sums.  gyk_body runs c outer, r inner; each sum v7[r][k] still adds its
+        // c = 0 term first, so r outer (one r's sums live at a time) rounds identically.
+        d2 yn[2][4], sn[2][4];   // Y' and S' (S of the previous iterate stays in Ss until the control)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int jl = (lane >> 4) + 4 * r;
+            double v7[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) v7[k] = 0.0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int i = 16 * (2 * w + c) + (lane & 15);
+                yn[c][r] = sn[c][r] = make_double2(0.0, 0.0);
+                if (!lv[r]) continue;
+                const double mu = mu_s[jl];
+                d2 gv, ax, mn, y;
+                ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mv[c][r], yv[c][r], bv[c][r], gv, ax, mn, y, v7);
+                msp_sums_elem(yv[c][r], mv[c][r], 1.0 / mu, Ts[jl * tst + i], gv, v7);
+                sn[c][r] = cadd(Ss[(4 * c + r) * NT + t], gv);
+                yn[c][r] = y;
+                mv[c][r] = mn;
+                xv[c][r] = ax;
+            }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) v7[k] += __shfl_xor(v7[k], o, 64);
+                v7[5] = fmax(v7[5], __shfl_xor(v7[5], o, 64));
+                v7[6] += __shfl_xor(v7[6], o, 64);
+                v7[7] += __shfl_xor(v7[7], o, 64);
+                v7[8] += __shfl_xor(v7[8], o, 64);
+            }
+            if ((lane & 15) == 0)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) red[w][jl][k] = v7[k];
+        }
+        __syncthreads();
+        MSR_STAMP(3);
+        // the control of realisation t (gyk_body's m-space branch, then fused_control in place)
+        if (t < GRB) {
+            int fl = 0;
+            if (mylive) {
+                double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                for (int q = 0; q < 8; ++q) {   // fixed order over the waves
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) v[k] += red[q][t][k];
+                    v[5] = fmax(v[5], red[q][t][5]);
+                    v[6] += red[q][t][6];
+                    v[7] += red[q][t][7];
+                    v[8] += red[q][t][8];
+                }
+                RealState& rs = rsl[t];
+                rs.obj2 = v[0];
+                rs.nAX2 = v[1];
+                rs.nY2 = v[2];
+                rs.nJM2 = v[3];
+                rs.dY2 = v[4];
+                const bool imp = sqrt(v[0]) < rs.opt_obj;
+                rs.fs0 = rs.fs0 + 2.0 * v[7] + v[8];
+                rs.fs3 = v[8];
+                rs.fzit = it;
+                rs.mzit = it;
+                ++cnt;
+                const int ok = fused_control<false>(za, &rs, z_profile(za, j0 + t), it);
+                // opt_Y follows every improvement; opt_S an improvement whose bound held (after a failed
+                // one the Z-step records X itself).  A pending best that this iterate does not beat is
+                // written now (bits 1, 2); the new pending ones are written if the run ends here (64, 128)
+                if (pbY && !imp) fl |= 1;
+                if (pbS && !imp) fl |= 2;
+                pbY = imp;
+                pbS = imp && (ok & 1);
+                if (pbY) fl |= 64;
+                if (pbS) {
+                    fl |= 128;
+                    rs.optsrc = 3;                       // (fused_control's deferral, resolved here)
+                }
+                if (!(ok & 1)) fl |= 8;                  // the bound failed: the Z-step of `it` runs
+                if (ok & 2) fl |= 16;                    // convergence test pending: the next gyf_kernel finishes it
+                fl |= rs.done ? 4 : 32;                  // stopped (convergence mode) / still live
+                mylive = !rs.done;
+                mu_s[t] = rs.mu;
+            }
+            flg_s[t] = fl;
+        }
+        __syncthreads();
+        MSR_STAMP(4);
+        int any = 0;
+#pragma unroll
+        for (int q = 0; q < GRB; ++q) {
+            const int f = flg_s[q];
+            any |= f;
+        }
+        const bool alive = any & 32;
+        const bool stop = (any & 24) || it + 1 >= a.it_end || !alive;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (!lv[r]) continue;
+            const int f = flg_s[(lane >> 4) + 4 * r];
+            const bool wb = stop || (f & 4);   // leave the state where the per-iteration launches read it
+            const int jl = (lane >> 4) + 4 * r;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int i = 16 * (2 * w + c) + (lane & 15);
+                const long long o = (long long)(j0 + jl) * m + i;
+                d2* ssl = &Ss[(4 * c + r) * NT + t];
+                if (f & 1) reinterpret_cast<d2*>(a.optY)[o] = yv[c][r];   // the previous iterate's
+                if (f & 2) reinterpret_cast<d2*>(a.optS)[o] = *ssl;
+                if (wb && (f & 64)) reinterpret_cast<d2*>(a.optY)[o] = yn[c][r];
+                if (wb && (f & 128)) reinterpret_cast<d2*>(a.optS)[o] = sn[c][r];
+                if (wb) {
+                    reinterpret_cast<d2*>(a.Y[it & 1])[o] = yn[c][r];
+                    reinterpret_cast<d2*>(a.Y[(it + 1) & 1])[o] = yv[c][r];
+                    reinterpret_cast<d2*>(a.M)[o] = mv[c][r];
+                    reinterpret_cast<d2*>(a.AX)[o] = xv[c][r];
+                    reinterpret_cast<d2*>(a.S[it & 1])[o] = sn[c][r];
+                    reinterpret_cast<d2*>(a.S[(it + 1) & 1])[o] = *ssl;
+                }
+                *ssl = sn[c][r];
+                yv[c][r] = yn[c][r];
+            }
+            if (f & 4) lv[r] = false;
+        }
+        MSR_STAMP(5);
+        if (stop) {
+#ifdef ACE_MSR_STAMPS
+            if (blockIdx.x == 5 && t == 0)
+                printf("msr it %d..%d: T %llu GT %llu bar %llu Ystep %llu ctl %llu wb %llu (x10ns)\n", a.it0, it,
+                       ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+#endif
+            const int rp = (any & 8) ? it : it + 1;
+            if (t < GRB && cnt) {
+                atomicAdd(a.mspcount, cnt);
+                atomicAdd(a.steps, cnt);
+            }
+            if (t < GRB && live_s[t]) {   // (stopped realisations were written back at their stop)
+                if (mylive) rsl[t].mres = rp;
+                a.rs[j0 + t] = rsl[t];
+            }
+            if (t == 0 && alive) atomicMin(a.resume, rp);
+            if (t == 0 && (any & 24)) atomicAdd(a.steps + ((any & 8) ? 2 : 3), 1);   // (diagnostics)
+            return;
+        }
+    }
 }
 
 // G [m][m] c128 -> f64 MFMA B-operand fragments: ((ks * (mp/16) + ct) * 64 + lane) holds
@@ -1433,6 +1797,33 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
     const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
     hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad, ctl);
+}
+// live realisations of [0, nb) that an m-space run starting at `it` could not take: not in the
+// m-space form, a convergence test pending, or not settled through it - 1 (blocks an earlier run
+// took past it count as ready)
+__global__ __launch_bounds__(256) void msr_ready_kernel(int nb, const RealState* __restrict__ rs, int it, int* notready) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    int bad = 0;
+    if (j < nb && !rs[j].done) {
+        const RealState& r = rs[j];
+        bad = !r.msp || r.dpend || r.mzit < it - 1 || r.zit < it - 1;
+    }
+    bad = __syncthreads_count(bad);
+    if (threadIdx.x == 0 && bad) atomicAdd(notready, bad);
+}
+bool msr_supported(int m) { return m == 256; }
+void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStream_t st) {
+    hipLaunchKernelGGL(msr_ready_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, nb, rs, it, notready);
+}
+void launch_msr(const MsrArgs& a, const ZArgs& za, hipStream_t st) {
+    static const bool attr = [] {
+        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
+        (void)hipGetLastError();
+        return ok;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(msr_kernel, dim3((a.nb + GRB - 1) / GRB), dim3(NT), msr_lds_bytes(), st, a, za);
 }
 // best m-space iterates still in an S ping-pong buffer (optsrc 4 / 5) -> opt_S (optsrc 3)
 __global__ __launch_bounds__(256) void msp_opt_gather_kernel(int m, RealState* rs, const double* S0, const double* S1,

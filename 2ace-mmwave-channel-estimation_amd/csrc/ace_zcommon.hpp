@@ -96,8 +96,9 @@ struct IterIn {
 __device__ __forceinline__ IterIn iter_in(const RealState* st) {
     return IterIn{st->obj2, st->nAX2, st->nY2, st->nJM2, st->dY2, st->opt_obj, st->last_res, st->status};
 }
+// (it: the iteration being controlled, a.it except in msr_kernel, which runs several per launch)
 __device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, const IterIn& in, double mu, double nX2,
-                                               double nZ2, double jn2, double dZ2, double dAtY, double nAtY) {
+                                               double nZ2, double jn2, double dZ2, double dAtY, double nAtY, int it) {
     const int m = a.m, n = a.n;
     const double nX = sqrt(nX2), nZ = sqrt(nZ2);
     const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
@@ -117,7 +118,7 @@ __device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, co
         const double t_prim = a.tol_abs * sqrt((double)(m + n) * r) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2);
         const double t_comb =
             a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
-        st->iters = a.it;
+        st->iters = it;
         if (res_prim < t_prim && !(res_comb < t_comb)) {
             st->dpend = 1;
             st->pd_dZ2 = dZ2;
@@ -146,7 +147,7 @@ __device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, co
     const double t_dual = a.tol_abs * sqrt((double)n * r * 2) + a.tol_rel * sqrt(nAtY2 + nZ * nZ);
     const double t_comb =
         a.tol_abs * sqrt((double)(m + n) * r * 2) + a.tol_rel * sqrt(mx1 * mx1 + mx2 * mx2 + nY * nY + nZ * nZ);
-    st->iters = a.it;
+    st->iters = it;
     const bool conv = (res_prim < t_prim && res_dual < t_dual) || (res_comb < t_comb);
     bool stop = false;
     if (conv) {
@@ -161,6 +162,10 @@ __device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, co
         st->last_res = res_comb;
     }
     return improved;
+}
+__device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, const IterIn& in, double mu, double nX2,
+                                               double nZ2, double jn2, double dZ2, double dAtY, double nAtY) {
+    return iter_control_in(a, st, in, mu, nX2, nZ2, jn2, dZ2, dAtY, nAtY, a.it);
 }
 // Finish a pending convergence test (RealState::dpend) on one wave, for the last iteration
 // (ZArgs::fixup_now; before it, gyk_kernel of the next iteration finishes it on the int8
@@ -217,7 +222,7 @@ __device__ __forceinline__ int iter_control(const ZArgs& a, RealState* st, doubl
 // COPY: the state is copied to registers in one batch of loads and written back (the one-wave
 // Z-step, scalar loads); otherwise the fields are used in place (gyf_kernel's m-space steps).
 template <bool COPY = true>
-__device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
+__device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf, int it) {
     RealState sc;
     if constexpr (COPY) sc = *st;
     RealState& s = COPY ? sc : *st;
@@ -230,20 +235,24 @@ __device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, cons
         const double lb = s.kf[p] * (1.0 - 1e-12) - cum;
         pass &= lb > 0.0 && lb * lb > pf.fl[p] * s0 * (1.0 + 1e-9);
     }
-    pass &= !(a.msp && s.mzit == a.it && a.it == a.msp_fail_it);   // (tests: the fallback path)
+    pass &= !(a.msp && s.mzit == it && it == a.msp_fail_it);   // (tests: the fallback path)
     if (!pass) return 0;
     const bool improved_pre = sqrt(s.obj2) < s.opt_obj;
     const int optsrc = s.optsrc;   // (the fused kernel kept a best iterate in Z')
-    const int ctl = iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY);
+    const int ctl = iter_control_in(a, &s, iter_in(&s), s.mu, s0, s0, 0.0, s3, s.dAtY, s.nAtY, it);
     s.vbound = sqrt(s0) * (1.0 + 0x1p-40);   // N' = 0: max|Z'| <= ||Z'|| (NaN-sticky)
     s.nzero = 1;
     s.avok = 1;
     // deferred opt_X: X = Z' bit for bit, or (m-space) X = Z0 + A^H S' with S' in Sg[it & 1]
-    s.optsrc = improved_pre ? (a.msp && s.mzit == a.it ? 4 + (a.it & 1) : 1 + (a.it & 1)) : optsrc;
+    s.optsrc = improved_pre ? (a.msp && s.mzit == it ? 4 + (it & 1) : 1 + (it & 1)) : optsrc;
     s.kfcum = cum;
-    s.zit = a.it;
+    s.zit = it;
     if constexpr (COPY) *st = sc;
     return 1 | (ctl & 2);
+}
+template <bool COPY = true>
+__device__ __forceinline__ int fused_control(const ZArgs& a, RealState* st, const ZProfile& pf) {
+    return fused_control<COPY>(a, st, pf, a.it);
 }
 
 }  // namespace

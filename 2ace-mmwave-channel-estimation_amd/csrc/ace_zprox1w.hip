@@ -137,7 +137,8 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     asm volatile("" ::"s"(s_done), "s"(s_zit), "s"(s_fzit), "v"(r1));
     const ZProfile pf = z_profile_flag(a, r1);
     if (!INIT && s_done) return;
-    if (!INIT && a.lean && s_zit == a.it) return;   // zlean_kernel completed this iteration
+    // zlean_kernel or the fused control completed this iteration (msr_kernel: this and later ones)
+    if (!INIT && a.lean && s_zit >= a.it) return;
     // The fused apply_AH formed X = Z + W of this iteration in Z' with its sums: the perturbation
     // certificate of zlean_kernel, then the iteration control; if the bound fails, the full
     // Z-step below runs on X read from Z'.
@@ -922,7 +923,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void zs
     if (lane < ZC && b0 + lane < nb) {
         const int b = b0 + lane;
         RealState* st = a.st + b;
-        if (!st->done && !(a.lean && st->zit == a.it)) {
+        if (!st->done && !(a.lean && st->zit >= a.it)) {
             full = 1;
             if (a.xfuse && st->fzit == a.it) full = !fused_control(a, st, z_profile(a, b));
         }

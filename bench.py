@@ -309,7 +309,7 @@ def _barrier(world):
         dist.barrier()
 
 
-def _prof_read(nclass=10):
+def _prof_read(nclass=11):
     """(total ms, launches, algorithmic flops) per kernel class since ace_prof_start."""
     import ctypes as C
     from ace_amd._lib import LIB, check
@@ -442,7 +442,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     _barrier(world)
     prof = not args.no_prof
     if prof:   # HIP event pairs on every PROF_STRIDE-th launch of each kernel class
-        check(LIB.ace_prof_sample(PROF_STRIDE, 0))
+        check(LIB.ace_prof_sample(PROF_STRIDE, 1 << 10))   # every m-space run (msr) launch
         check(LIB.ace_prof_start(args.steps * (args.iters * 8 + 16)))
     torch.cuda.synchronize()
     _barrier(world)
@@ -456,7 +456,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     out = outs[(nstep[0] - 1) & 1]
     msp_steps = C.c_longlong(0)
     if prof:
-        kt, kn, _ = _prof_read()
+        kt, kn, kw = _prof_read()
         check(LIB.ace_prof_msp_steps(C.byref(msp_steps)))
     elapsed = _max_over_ranks(elapsed, dev, world)
     it_ok = bool((out.iters == args.iters).all().item())
@@ -465,7 +465,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         return None
 
     total = sum(counts) * args.steps
-    kernels, roof, roof_gemm = {}, None, None
+    kernels, roof, roof_gemm, roof_msr = {}, None, None, None
     tag = wl.get("tag", "private" if private else ("nuclear" if variant == "A2nuclear" else "unit"))
     msp_frac = 0.0
     if prof:
@@ -498,8 +498,28 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
         ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac, nms=nms)
         timed = [k for k in kernels if k in ITER_CLASSES and unit_resources(k, m, n, **ctx)]
-        # every timed class launches once per iteration: dominant = largest average launch
-        dom = max(timed, key=lambda k: kernels[k]["avg_ms"])
+        # device time per class: the iteration classes are sampled on every PROF_STRIDE-th launch, the
+        # m-space runs (msr, ace_i8gemm.hip::msr_kernel) on every launch; dominant = most device time
+        dev_ms = {k: kernels[k]["total_ms"] * PROF_STRIDE for k in timed}
+        msr_i = KERNEL_CLASSES.index("msr") if "msr" in KERNEL_CLASSES else -1
+        roof_msr = None
+        if msr_i >= 0 and kn[msr_i] and kw[msr_i] > 0:
+            # flops: 8 m^2 per realisation-iteration the runs executed (ace_prof_work, counted on the device)
+            roof_msr = roofline_from("msr_kernel (m-space run)", kernels["msr"]["avg_ms"] * 1e-3,
+                                     {"f64": kw[msr_i] / kn[msr_i]}, note=(
+                "the unit's steady m-space iterations (T, g = G T on the f64 matrix cores in 3M form, the "
+                "Y-step, the certified control) of a 16-realisation block inside one launch, state on chip; "
+                "achieved counts 8 flops per complex MAC of g = G T over the realisation-iterations the run "
+                "executed (device counter)"))
+            roof_msr["iterations_per_launch"] = round(kw[msr_i] / kn[msr_i] / (8.0 * m * m) / per_launch, 1)
+            roof_msr["realisations_per_launch"] = per_launch
+            roof_msr["concurrent_launches"] = nsplit
+            roof_msr["chip_frac"] = round(roof_msr["frac"] * nsplit, 4)
+            tr = _pmc_traffic("msr_kernel", tag)
+            if tr:
+                roof_msr["traffic"], roof_msr["traffic_source"] = tr
+            dev_ms["msr"] = kernels["msr"]["total_ms"]
+        dom = max(dev_ms, key=dev_ms.get)
 
         def roof_of(k):
             res = {r: a * per_launch for r, a in unit_resources(k, m, n, **ctx).items()}
@@ -537,11 +557,12 @@ def unit_bench(args, private, dev, rank, world, workload=None):
                     r["traffic_per_algorithmic"] = round(tr[0] / res["hbm"], 3)
             return r
 
-        roof = roof_of(dom)
+        roof = roof_msr if dom == "msr" else roof_of(dom)
+        roof["device_time_share"] = {k: round(v / sum(dev_ms.values()), 4) for k, v in dev_ms.items()}
         roof["note"] = (f"dominant kernel by device time (HIP event pairs on the launch stream inside the timed "
-                        f"region, on every {PROF_STRIDE}th launch of each kernel class); peaks: MI355X spec (FP64 "
-                        "78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); traffic: PMC FETCH_SIZE+WRITE_SIZE per launch "
-                        "from the profile named in traffic_source (same workload tag)")
+                        f"region, on every {PROF_STRIDE}th launch of each iteration class and every m-space run); "
+                        "peaks: MI355X spec (FP64 78.6 TF, int8 5 POP/s dense, HBM3E 8 TB/s); traffic: PMC "
+                        "FETCH_SIZE+WRITE_SIZE per launch from the profile named in traffic_source (same workload tag)")
         if not pc:
             fk = [k for k in timed if "f64" in unit_resources(k, m, n, **ctx)]
             if fk:
@@ -583,6 +604,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         },
         "roofline": roof,
         "roofline_gemm": roof_gemm,
+        "roofline_msr": roof_msr if prof else None,
         "cpu_baseline": cpu,
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "msp_frac": round(msp_frac, 4),

@@ -288,7 +288,8 @@ int ace_synth_channels(uint64_t seed, int64_t first, int count, int m, int tx, i
 #define ACE_K_APPLY_AH 7 /* X = V + A^H g */
 #define ACE_K_ZSTEP 8    /* ArgMinZ, N update, residuals, stop test */
 #define ACE_K_FINAL 9
-#define ACE_NKCLASS 10
+#define ACE_K_MSR 10     /* m-space run: several steady iterations of the unit in one launch */
+#define ACE_NKCLASS 11
 int ace_prof_start(int max_launches);
 /* From the next ace_prof_start on, record only every stride-th launch of each kernel class
  * (default 1) except the classes whose bit (1 << ACE_K_*) is set in full_mask, which are

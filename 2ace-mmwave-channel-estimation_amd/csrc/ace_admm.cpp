@@ -475,11 +475,14 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 ACE_HIP(hipEventRecord(cev[h], ss[h]));
                 ACE_HIP(hipStreamWaitEvent(st, cev[h], 0));
             }
-            ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 28), 0, 1, st));
+            ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 28), 0, 3, st));
             launch_msr_ready(batch, w.st, it, w.done + 28, st);
-            int nr = 0;
-            ACE_HIP(read_back(&nr, w.done + 28, sizeof(int), st));
-            run_msr = nr == 0;
+            int nr[3] = {0, 0, 0};
+            ACE_HIP(read_back(nr, w.done + 28, sizeof(nr), st));
+            run_msr = nr[0] == 0;
+            if (msr_trace())
+                fprintf(stderr, "msr check it %d: not ready %d (not m-space %d, test pending %d)\n", it, nr[0], nr[1],
+                        nr[2]);
             if (!run_msr) msr_next = it + kn.msr_retry;
         }
         if (run_msr) {

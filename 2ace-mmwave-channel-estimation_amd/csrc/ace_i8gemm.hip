@@ -1803,13 +1803,21 @@ void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, doubl
 // took past it count as ready)
 __global__ __launch_bounds__(256) void msr_ready_kernel(int nb, const RealState* __restrict__ rs, int it, int* notready) {
     const int j = blockIdx.x * 256 + threadIdx.x;
-    int bad = 0;
+    int bad = 0, nm = 0, np = 0;
     if (j < nb && !rs[j].done) {
         const RealState& r = rs[j];
         bad = !r.msp || r.dpend || r.mzit < it - 1 || r.zit < it - 1;
+        nm = !r.msp;
+        np = r.dpend;
     }
     bad = __syncthreads_count(bad);
-    if (threadIdx.x == 0 && bad) atomicAdd(notready, bad);
+    nm = __syncthreads_count(nm);
+    np = __syncthreads_count(np);
+    if (threadIdx.x == 0 && bad) {
+        atomicAdd(notready, bad);
+        atomicAdd(notready + 1, nm);   // (diagnostics: not in the m-space form, test pending)
+        atomicAdd(notready + 2, np);
+    }
 }
 bool msr_supported(int m) { return m == 256; }
 void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStream_t st) {

@@ -33,6 +33,18 @@ __device__ __forceinline__ double dpp_shl1(double x) {  // lane k <- lane k+1 wi
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x101, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+// The same shifts with the row-end lane keeping `old` (it has no source lane and bound_ctrl is off):
+// row_shr:1 leaves lane 0 of each row with old, row_shl:1 lane 15.  One DPP move per dword, no select.
+__device__ __forceinline__ double dpp_shr1_keep(double old, double x) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(x), 0x111, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(x), 0x111, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_shl1_keep(double old, double x) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(x), 0x101, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(x), 0x101, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
 
 __device__ __forceinline__ void mfma_c(d2 a, d2 b, d4v& cr, d4v& ci) {  // (cr, ci) += a * b (complex)
     cr = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b.x, cr, 0, 0, 0);
@@ -55,6 +67,11 @@ __device__ __forceinline__ void mm16(FA fa, FB fb, d4v& cr, d4v& ci, int lane) {
         mfma_c(fa(lane & 15, kk), fb(k0, kk, lane & 15), cr, ci);
     }
 }
+
+// off-diagonal 16x16 slot-pair blocks (ka < kb) for the one-wave sweep: two per lane; the 16 diagonal
+// blocks are updated by the lanes that form their pair's rotation (zstep1w_body)
+static __constant__ unsigned char c_off_a[120] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,1,1,1,1,1,1,1,1,1,1,2,2,2,2,2,2,2,2,2,2,2,2,2,3,3,3,3,3,3,3,3,3,3,3,3,4,4,4,4,4,4,4,4,4,4,4,5,5,5,5,5,5,5,5,5,5,6,6,6,6,6,6,6,6,6,7,7,7,7,7,7,7,7,8,8,8,8,8,8,8,9,9,9,9,9,9,10,10,10,10,10,11,11,11,11,12,12,12,13,13,14};
+static __constant__ unsigned char c_off_b[120] = {1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,2,3,4,5,6,7,8,9,10,11,12,13,14,15,3,4,5,6,7,8,9,10,11,12,13,14,15,4,5,6,7,8,9,10,11,12,13,14,15,5,6,7,8,9,10,11,12,13,14,15,6,7,8,9,10,11,12,13,14,15,7,8,9,10,11,12,13,14,15,8,9,10,11,12,13,14,15,9,10,11,12,13,14,15,10,11,12,13,14,15,11,12,13,14,15,12,13,14,15,13,14,15,14,15,15};
 
 // m-space fallback (RealState::msp): the bound failed for an iterate gyk_kernel settled in m-space,
 // so the full Z-step needs Z and X = Z' in memory.  One wave forms them from the implicit form,
@@ -543,31 +560,35 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         Rb[r][0] = (i == 2 * kl + 1) ? 1.0 : 0.0;
         Rb[r][1] = 0.0;
     }
-    // this lane's H blocks: slots lane, lane+64, lane+128 of the triangular enumeration
-    int ta[3], tb[3];
-    unsigned pk[3][4];   // rd | wr << 11 | (write conj) << 22 | (diag block) << 23
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int e = lane + 64 * q;
-        ta[q] = -1;
-        tb[q] = 0;
-        if (e < 136) {
-            const int A_ = c_tri_a[e], B_ = c_tri_b[e];
-            if (B_ < P) {
-                ta[q] = A_;
-                tb[q] = B_;
-            }
-        }
-        const int sa = ta[q] < 0 ? 0 : ta[q], sb = tb[q];
+    // this lane's H blocks: off-diagonal slots lane, lane + 64 (a < b); the diagonal block of pair kl
+    // (pkd) is updated by the lanes that form that pair's rotation
+    int ta[2], tb[2];
+    unsigned pk[2][4], pkd[4];   // rd | wr << 11 | (write conj) << 22 | (diag block) << 23
+    auto pack = [&](int sa, int sb, unsigned (&o)[4]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 2 * sa + (r >> 1), j = 2 * sb + (r & 1);
             const unsigned rd = i <= j ? up_idx(i, j) : up_idx(j, i);
             const int ii = circ_next(tx, i), jj = circ_next(tx, j);
             const unsigned wr = ii <= jj ? up_idx(ii, jj) : up_idx(jj, ii);
-            pk[q][r] = rd | (wr << 11) | ((ii <= jj ? 0u : 1u) << 22) | ((sa == sb ? 1u : 0u) << 23);
+            o[r] = rd | (wr << 11) | ((ii <= jj ? 0u : 1u) << 22) | ((sa == sb ? 1u : 0u) << 23);
         }
+    };
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int e = lane + 64 * q;
+        ta[q] = -1;
+        tb[q] = 0;
+        if (e < 120) {
+            const int A_ = c_off_a[e], B_ = c_off_b[e];
+            if (B_ < P) {
+                ta[q] = A_;
+                tb[q] = B_;
+            }
+        }
+        pack(ta[q] < 0 ? 0 : ta[q], ta[q] < 0 ? 1 : tb[q], pk[q]);
     }
+    pack(kl < P ? kl : 0, kl < P ? kl : 0, pkd);
     const int rp = up_idx(2 * kl, 2 * kl), rq = up_idx(2 * kl + 1, 2 * kl + 1), rc = up_idx(2 * kl, 2 * kl + 1);
     int cur = 0;
     for (; sweeps < 40; ++sweeps) {
@@ -575,8 +596,9 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         bool need = false;
         {
             const d2* H = T0 + cur * ZPACK;
+            if (kl < P) need = needs_rot(H[rp].x, H[rq].x, H[rc], abs_tol);   // the pair's own entry
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < 2; ++q) {
                 if (ta[q] < 0) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -590,19 +612,13 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
             const d2* H = T0 + cur * ZPACK;
             d2* Hn = T0 + (cur ^ 1) * ZPACK;
             Rot Jl{1.0, 0.0, make_double2(1.0, 0.0), false};
-            if (kl < P) Jl = make_rot(H[rp].x, H[rq].x, H[rc], abs_tol);
+            const d2 hp = H[rp], hq = H[rq], hc = H[rc];
+            if (kl < P) Jl = make_rot(hp.x, hq.x, hc, abs_tol);
             if (lane < 16) RotS[lane] = make_double4(Jl.cs, Jl.sn, Jl.e.x, Jl.e.y);
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                if (ta[q] < 0) continue;
-                const double4 ra = RotS[ta[q]], rb = RotS[tb[q]];
-                const unsigned p0 = pk[q][0], p1 = pk[q][1], p2 = pk[q][2], p3 = pk[q][3];
-                const bool diagblk = (p0 >> 23) & 1u;
-                const d2 h00 = H[p0 & 2047u], h01 = H[p1 & 2047u], h11 = H[p3 & 2047u];
-                d2 h10 = H[p2 & 2047u];
-                if (diagblk) h10.y = -h10.y;
-                // H'[a,b] = Ja^H H[a,b] Jb,  J = [[cs, sn], [-sn e*, cs e*]]
+            // H'[a,b] = Ja^H H[a,b] Jb,  J = [[cs, sn], [-sn e*, cs e*]] (the block update below; the
+            // same expressions for the diagonal block of pair kl, Ja = Jb = Jl, written by row 0)
+            auto blk = [&](double4 ra, double4 rb, d2 h00, d2 h01, d2 h10, d2 h11, d2& n00, d2& n01, d2& n10,
+                           d2& n11) {
                 const d2 ebc = make_double2(rb.z, -rb.w), ea = make_double2(ra.z, ra.w);
                 const d2 t01 = cmul(h01, ebc), t11 = cmul(h11, ebc);
                 const d2 T00 = csub(cscale(h00, rb.x), cscale(t01, rb.y));
@@ -610,17 +626,36 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                 const d2 T10 = csub(cscale(h10, rb.x), cscale(t11, rb.y));
                 const d2 T11 = cadd(cscale(h10, rb.y), cscale(t11, rb.x));
                 const d2 u10 = cmul(ea, T10), u11 = cmul(ea, T11);
-                const d2 n00 = csub(cscale(T00, ra.x), cscale(u10, ra.y));
-                const d2 n01 = csub(cscale(T01, ra.x), cscale(u11, ra.y));
-                const d2 n10 = cadd(cscale(T00, ra.y), cscale(u10, ra.x));
-                const d2 n11 = cadd(cscale(T01, ra.y), cscale(u11, ra.x));
-                auto put = [&](unsigned pw, d2 v) {
-                    Hn[(pw >> 11) & 2047u] = make_double2(v.x, ((pw >> 22) & 1u) ? -v.y : v.y);
-                };
+                n00 = csub(cscale(T00, ra.x), cscale(u10, ra.y));
+                n01 = csub(cscale(T01, ra.x), cscale(u11, ra.y));
+                n10 = cadd(cscale(T00, ra.y), cscale(u10, ra.x));
+                n11 = cadd(cscale(T01, ra.y), cscale(u11, ra.x));
+            };
+            auto put = [&](unsigned pw, d2 v) {
+                Hn[(pw >> 11) & 2047u] = make_double2(v.x, ((pw >> 22) & 1u) ? -v.y : v.y);
+            };
+            if (lane < 16 && kl < P) {
+                const double4 rl = make_double4(Jl.cs, Jl.sn, Jl.e.x, Jl.e.y);
+                d2 n00, n01, n10, n11;
+                blk(rl, rl, hp, hc, make_double2(hc.x, -hc.y), hq, n00, n01, n10, n11);
+                put(pkd[0], n00);
+                put(pkd[1], n01);
+                put(pkd[3], n11);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (ta[q] < 0) continue;
+                const double4 ra = RotS[ta[q]], rb = RotS[tb[q]];
+                const unsigned p0 = pk[q][0], p1 = pk[q][1], p2 = pk[q][2], p3 = pk[q][3];
+                const d2 h00 = H[p0 & 2047u], h01 = H[p1 & 2047u], h11 = H[p3 & 2047u];
+                const d2 h10 = H[p2 & 2047u];
+                d2 n00, n01, n10, n11;
+                blk(ra, rb, h00, h01, h10, h11, n00, n01, n10, n11);
                 put(p0, n00);
                 put(p1, n01);
                 put(p3, n11);
-                if (!diagblk) put(p2, n10);
+                put(p2, n10);
             }
             // R <- R J for this lane's column pair, then the circle-method column permutation
             {
@@ -661,8 +696,23 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
                     }
                 }
                 };
-                if (P == 16) shift(true);
-                else shift(false);
+                if (P == 16) {
+                    // tx = 32: the rows' ends are the circle's ends, so the DPP moves' own row-end
+                    // behaviour supplies new top(0) = top(0) and new bot(15) = top(15) (the same
+                    // permutation as shift(true), without its selects)
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const double s0 = kl == 0 ? Rb[r][0] : Rt[r][0], s1 = kl == 0 ? Rb[r][1] : Rt[r][1];
+                        const double nt0 = dpp_shr1_keep(Rt[r][0], s0), nt1 = dpp_shr1_keep(Rt[r][1], s1);
+                        const double nb0 = dpp_shl1_keep(Rt[r][0], Rb[r][0]), nb1 = dpp_shl1_keep(Rt[r][1], Rb[r][1]);
+                        Rt[r][0] = nt0;
+                        Rt[r][1] = nt1;
+                        Rb[r][0] = nb0;
+                        Rb[r][1] = nb1;
+                    }
+                } else {
+                    shift(false);
+                }
             }
             cur ^= 1;
             __syncthreads();

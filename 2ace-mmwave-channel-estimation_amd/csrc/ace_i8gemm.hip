@@ -1359,12 +1359,16 @@ __global__ __launch_bounds__(NT, 1) void gyf_kernel(int nb, int m, int n, GykArg
 // at it0 returns at once (resume = it0).  Stopped realisations (convergence mode) write their state
 // back at the stop and drop out.
 constexpr int MGSK = 2;   // G T pipeline depth here (registers hold the state; the k order is gyk_body's)
-__host__ __device__ __forceinline__ size_t msr_lds_bytes() { return (size_t)GRB * 257 * 16 + (size_t)8 * NT * 16; }
-__global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
+__host__ __device__ __forceinline__ size_t msr_lds_bytes() { return (size_t)GRB * 257 * 16 + (size_t)4096 * 16; }
+// TPW output tiles of 16 per wave: 2 (8 waves of 256 VGPRs) or 4 (4 waves, one per SIMD, with the
+// whole register file); the per-realisation sums keep the 8-wave partial order (red[8]) either way
+template <int TPW>
+__global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs za) {
+    constexpr int NTW = 64 * 16 / TPW;   // threads
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int mp = 256, tst = mp + 1, nct = mp / 16, nks = mp / 4, nstage = nks / MGSK;
     d2* Ts = reinterpret_cast<d2*>(smem);        // [16][tst]: T
-    d2* Ss = Ts + GRB * tst;                     // [8][NT]: S of the thread's 8 outputs (thread-private)
+    d2* Ss = Ts + GRB * tst;                     // [4 TPW][NTW]: S of the thread's outputs (thread-private)
     __shared__ double red[8][GRB][9];
     __shared__ double mu_s[GRB];
     __shared__ int live_s[GRB], flg_s[GRB];
@@ -1409,14 +1413,14 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) lv[r] = live_s[(lane >> 4) + 4 * r];
     auto off = [&](int r, int c) -> long long {
-        return (long long)(lv[r] ? j0 + (lane >> 4) + 4 * r : j0) * m + 16 * (2 * w + c) + (lane & 15);
+        return (long long)(lv[r] ? j0 + (lane >> 4) + 4 * r : j0) * m + 16 * (TPW * w + c) + (lane & 15);
     };
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int fl = flg_s[(lane >> 4) + 4 * r];
         if (!lv[r] || !fl) continue;
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < TPW; ++c) {
             if (fl & 3) reinterpret_cast<d2*>(a.optY)[off(r, c)] = reinterpret_cast<const d2*>(a.Y[(fl & 3) - 1])[off(r, c)];
             if (fl >> 2) reinterpret_cast<d2*>(a.optS)[off(r, c)] = reinterpret_cast<const d2*>(a.S[(fl >> 2) - 1])[off(r, c)];
         }
@@ -1427,12 +1431,12 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
         if (flg_s[t] >> 2) rsl[t].optsrc = 3;
     }
     // state of iterate it0 - 1
-    d2 yv[2][4], mv[2][4], xv[2][4];
-    double bv[2][4];
+    d2 yv[TPW][4], mv[TPW][4], xv[TPW][4];
+    double bv[TPW][4];
     {
         const int p = (a.it0 - 1) & 1;
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < TPW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const long long o = off(r, c);
@@ -1440,13 +1444,12 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
                 mv[c][r] = reinterpret_cast<const d2*>(a.M)[o];
                 xv[c][r] = reinterpret_cast<const d2*>(a.AX)[o];
                 bv[c][r] = a.B[o];
-                Ss[(4 * c + r) * NT + t] = reinterpret_cast<const d2*>(a.S[p])[o];
+                Ss[(4 * c + r) * NTW + t] = reinterpret_cast<const d2*>(a.S[p])[o];
             }
     }
     __syncthreads();   // (every thread is done with the flush flags)
     if (t < GRB) flg_s[t] = 0;
-    const d2* gp0 = reinterpret_cast<const d2*>(a.Gf) + (long long)(2 * w) * 64 + lane;
-    const d2* gp1 = reinterpret_cast<const d2*>(a.Gf) + (long long)(2 * w + 1) * 64 + lane;
+    const d2* gp = reinterpret_cast<const d2*>(a.Gf) + (long long)(TPW * w) * 64 + lane;   // tile TPW w + c: + 64 c
     const d2* trow = Ts + (lane & 15) * tst + (lane >> 4);
     int cnt = 0;   // m-space steps of realisation t (ace_prof_msp_steps)
     bool mylive = t < GRB && live_s[t] && !(flg_s[t] & 4);
@@ -1466,23 +1469,23 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
             const int jl = (lane >> 4) + 4 * r;
             const double im = lv[r] ? 1.0 / mu_s[jl] : 0.0;
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
+            for (int c = 0; c < TPW; ++c) {
                 d2 v = make_double2(0.0, 0.0);
                 if (lv[r])
                     v = make_double2(fma(-mv[c][r].x, im, yv[c][r].x) - xv[c][r].x,
                                      fma(-mv[c][r].y, im, yv[c][r].y) - xv[c][r].y);
-                Ts[jl * tst + 16 * (2 * w + c) + (lane & 15)] = v;
+                Ts[jl * tst + 16 * (TPW * w + c) + (lane & 15)] = v;
             }
         }
         __syncthreads();
         MSR_STAMP(0);
         // g = G T: gyk_body's 3M product, the same k order
-        d4v p1[2], p2[2], p3[2];
+        d4v p1[TPW], p2[TPW], p3[TPW];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) p1[c] = p2[c] = p3[c] = d4v{0.0, 0.0, 0.0, 0.0};
+        for (int c = 0; c < TPW; ++c) p1[c] = p2[c] = p3[c] = d4v{0.0, 0.0, 0.0, 0.0};
         {
             struct GS {
-                d2 f[MGSK][2];
+                d2 f[MGSK][TPW];
             };
             struct TS {
                 d2 v[MGSK];
@@ -1491,8 +1494,8 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
 #pragma unroll
                 for (int kk = 0; kk < MGSK; ++kk) {
                     const long long ks = min(MGSK * s + kk, nks - 1);
-                    gs.f[kk][0] = gp0[ks * nct * 64];
-                    gs.f[kk][1] = gp1[ks * nct * 64];
+#pragma unroll
+                    for (int c = 0; c < TPW; ++c) gs.f[kk][c] = gp[ks * nct * 64 + 64 * c];
                 }
             };
             auto tload = [&](TS& ts, int s) {
@@ -1506,7 +1509,7 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
                     const d2 v = ts.v[kk];
                     const double ar = v.x, ai = v.y, as = v.x + v.y;
 #pragma unroll
-                    for (int c = 0; c < 2; ++c) {
+                    for (int c = 0; c < TPW; ++c) {
                         const d2 l = gs.f[kk][c];
                         p1[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, l.x, p1[c], 0, 0, 0);
                         p2[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, l.y, p2[c], 0, 0, 0);
@@ -1535,23 +1538,25 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
         MSR_STAMP(2);
         // Y-step and m-space sums.  gyk_body runs c outer, r inner; each sum v7[r][k] still adds its
         // c = 0 term first, so r outer (one r's sums live at a time) rounds identically.
-        d2 yn[2][4], sn[2][4];   // Y' and S' (S of the previous iterate stays in Ss until the control)
+        d2 yn[TPW][4], sn[TPW][4];   // Y' and S' (S of the previous iterate stays in Ss until the control)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int jl = (lane >> 4) + 4 * r;
+#pragma unroll
+          for (int h = 0; h < TPW / 2; ++h) {   // tile pair h: the sums of 8-wave wave TPW w / 2 + h
             double v7[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) v7[k] = 0.0;
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int i = 16 * (2 * w + c) + (lane & 15);
+            for (int c = 2 * h; c < 2 * h + 2; ++c) {
+                const int i = 16 * (TPW * w + c) + (lane & 15);
                 yn[c][r] = sn[c][r] = make_double2(0.0, 0.0);
                 if (!lv[r]) continue;
                 const double mu = mu_s[jl];
                 d2 gv, ax, mn, y;
                 ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mv[c][r], yv[c][r], bv[c][r], gv, ax, mn, y, v7);
                 msp_sums_elem(yv[c][r], mv[c][r], 1.0 / mu, Ts[jl * tst + i], gv, v7);
-                sn[c][r] = cadd(Ss[(4 * c + r) * NT + t], gv);
+                sn[c][r] = cadd(Ss[(4 * c + r) * NTW + t], gv);
                 yn[c][r] = y;
                 mv[c][r] = mn;
                 xv[c][r] = ax;
@@ -1567,7 +1572,8 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
             }
             if ((lane & 15) == 0)
 #pragma unroll
-                for (int k = 0; k < 9; ++k) red[w][jl][k] = v7[k];
+                for (int k = 0; k < 9; ++k) red[TPW / 2 * w + h][jl][k] = v7[k];
+          }
         }
         __syncthreads();
         MSR_STAMP(3);
@@ -1634,10 +1640,10 @@ __global__ __launch_bounds__(NT, 1) void msr_kernel(MsrArgs a, ZArgs za) {
             const bool wb = stop || (f & 4);   // leave the state where the per-iteration launches read it
             const int jl = (lane >> 4) + 4 * r;
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int i = 16 * (2 * w + c) + (lane & 15);
+            for (int c = 0; c < TPW; ++c) {
+                const int i = 16 * (TPW * w + c) + (lane & 15);
                 const long long o = (long long)(j0 + jl) * m + i;
-                d2* ssl = &Ss[(4 * c + r) * NT + t];
+                d2* ssl = &Ss[(4 * c + r) * NTW + t];
                 if (f & 1) reinterpret_cast<d2*>(a.optY)[o] = yv[c][r];   // the previous iterate's
                 if (f & 2) reinterpret_cast<d2*>(a.optS)[o] = *ssl;
                 if (wb && (f & 64)) reinterpret_cast<d2*>(a.optY)[o] = yn[c][r];
@@ -1824,14 +1830,25 @@ void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStr
     hipLaunchKernelGGL(msr_ready_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, nb, rs, it, notready);
 }
 void launch_msr(const MsrArgs& a, const ZArgs& za, hipStream_t st) {
+    // ACE_MSR_WAVES=4: four waves of four output tiles (one per SIMD, 256 VGPRs + 256 AGPRs) instead
+    // of eight of two; measured 44 against 40 us per iteration (the 8-wave G T overlaps its waves)
+    static const int waves = [] {
+        const char* e = getenv("ACE_MSR_WAVES");
+        return e && atoi(e) == 4 ? 4 : 8;
+    }();
     static const bool attr = [] {
-        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
+        bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel<2>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
+        ok = ok && hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel<4>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
         (void)hipGetLastError();
         return ok;
     }();
     (void)attr;
-    hipLaunchKernelGGL(msr_kernel, dim3((a.nb + GRB - 1) / GRB), dim3(NT), msr_lds_bytes(), st, a, za);
+    if (waves == 8)
+        hipLaunchKernelGGL(msr_kernel<2>, dim3((a.nb + GRB - 1) / GRB), dim3(512), msr_lds_bytes(), st, a, za);
+    else
+        hipLaunchKernelGGL(msr_kernel<4>, dim3((a.nb + GRB - 1) / GRB), dim3(256), msr_lds_bytes(), st, a, za);
 }
 // best m-space iterates still in an S ping-pong buffer (optsrc 4 / 5) -> opt_S (optsrc 3)
 __global__ __launch_bounds__(256) void msp_opt_gather_kernel(int m, RealState* rs, const double* S0, const double* S1,

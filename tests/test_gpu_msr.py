@@ -51,6 +51,8 @@ def _same(a, b):
     (1024, False, {"ACE_MSP_FAIL_IT": "100"}),
     (512, True, {"ACE_MSP_ROOM": "1", "ACE_MSR_START": "40", "ACE_MSR_RETRY": "2"}),
     (256, False, {"ACE_MSR_START": "20", "ACE_MSR_RETRY": "1"}),
+    (1024, True, {"ACE_MSR_WAVES": "4"}),
+    (1024, False, {"ACE_MSR_WAVES": "4", "ACE_MSP_FAIL_IT": "120"}),
 ])
 def test_msr_bit_identical(gpu, monkeypatch, batch, fixed, env):
     from ace_amd import synth_problem

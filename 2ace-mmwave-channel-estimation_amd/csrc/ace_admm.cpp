@@ -84,8 +84,9 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //   ACE_MSR=0           no m-space runs (msr_kernel): every iteration as its own launches
 //   ACE_MSR_START=<it>  first iteration at which an m-space run is tried (default 56)
 //   ACE_MSR_RETRY=<k>   after a run stopped early, the next try k iterations after its resume point
+//   ACE_MSR_WAVES=4     the m-space run as four waves of four output tiles (default eight of two)
 struct Knobs {
-    int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8;
+    int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8, msr_waves = 8;
     bool msr = true;
     bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true;
     double msp_room = 32.0;
@@ -116,6 +117,7 @@ static Knobs read_knobs() {
     k.msr_start = (int)num("ACE_MSR_START", 56);
     k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
     if (k.msr_retry < 1) k.msr_retry = 1;
+    k.msr_waves = (int)num("ACE_MSR_WAVES", 8) == 4 ? 4 : 8;
     return k;
 }
 // ACE_MSR_TRACE=1: one stderr line per m-space run (resume point, steps, exit reasons)
@@ -503,7 +505,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 12 + 4 * h), 0, 4, ss[h]));
                 ProfScope ps(ACE_K_MSR, ss[h]);
                 pidx[h] = ps.idx;
-                launch_msr(ma, za, ss[h]);
+                launch_msr(ma, za, kn.msr_waves, ss[h]);
             }
             for (int h = 1; h < nsplit; ++h) {   // (the caller's stream waits for the sub-batches)
                 ACE_HIP(hipEventRecord(cev[h], ss[h]));

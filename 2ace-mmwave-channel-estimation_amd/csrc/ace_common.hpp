@@ -291,7 +291,7 @@ bool msr_supported(int m);
 // notready[0] += live realisations of the batch an m-space run from `it` could not take; [1], [2] of
 // them not in the m-space form, with a convergence test pending (diagnostics)
 void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStream_t st);
-void launch_msr(const MsrArgs& a, const ZArgs& za, hipStream_t st);
+void launch_msr(const MsrArgs& a, const ZArgs& za, int waves, hipStream_t st);   // waves: 8 (default) or 4
 // KY = K Y with K = c^2 K_int (cmax[1] = c^2): two digit planes of K_int (setup: launch_i8k_expand)
 size_t i8k_frag_bytes(int m);
 void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, int* flag, hipStream_t st);

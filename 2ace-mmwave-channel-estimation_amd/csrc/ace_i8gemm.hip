@@ -1829,13 +1829,9 @@ bool msr_supported(int m) { return m == 256; }
 void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStream_t st) {
     hipLaunchKernelGGL(msr_ready_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, nb, rs, it, notready);
 }
-void launch_msr(const MsrArgs& a, const ZArgs& za, hipStream_t st) {
-    // ACE_MSR_WAVES=4: four waves of four output tiles (one per SIMD, 256 VGPRs + 256 AGPRs) instead
-    // of eight of two; measured 44 against 40 us per iteration (the 8-wave G T overlaps its waves)
-    static const int waves = [] {
-        const char* e = getenv("ACE_MSR_WAVES");
-        return e && atoi(e) == 4 ? 4 : 8;
-    }();
+void launch_msr(const MsrArgs& a, const ZArgs& za, int waves, hipStream_t st) {
+    // waves = 4: four waves of four output tiles (one per SIMD, 256 VGPRs + 256 AGPRs) instead of
+    // eight of two; measured 44 against 40 us per iteration (the 8-wave G T overlaps its waves)
     static const bool attr = [] {
         bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel<2>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;

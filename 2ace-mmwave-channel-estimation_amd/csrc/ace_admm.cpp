@@ -85,10 +85,12 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //   ACE_MSR_START=<it>  first iteration at which an m-space run is tried (default 56)
 //   ACE_MSR_RETRY=<k>   after a run stopped early, the next try k iterations after its resume point
 //   ACE_MSR_WAVES=4     the m-space run as four waves of four output tiles (default eight of two)
+//   ACE_ZCERT=0         the four-wave Z-step (r-column stages) always runs its eigensolver (no Ky Fan
+//                       certificate)
 struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8, msr_waves = 8;
     bool msr = true;
-    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true;
+    bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true, zcert = true;
     double msp_room = 32.0;
 };
 static Knobs read_knobs() {
@@ -114,6 +116,7 @@ static Knobs read_knobs() {
     k.nuc_msp = on("ACE_NUC_MSP");
     k.i8r = on("ACE_I8_STAGES");
     k.msr = on("ACE_MSR");
+    k.zcert = on("ACE_ZCERT");
     k.msr_start = (int)num("ACE_MSR_START", 56);
     k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
     if (k.msr_retry < 1) k.msr_retry = 1;
@@ -756,6 +759,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.rho = p.rho;
     za.fixed_iters = p.fixed_iters;
     za.warm = p.eig_warm;
+    za.zcert = kn.zcert ? 1 : 0;
     za.wmode = 0;
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)

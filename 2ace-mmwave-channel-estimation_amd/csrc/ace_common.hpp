@@ -427,6 +427,7 @@ struct ZArgs {
     int matz;              // (launch_i8_msp_optx) the apply_AH launch forms opt_X = Z0 + A^H opt_S
     int msp_fail_it;       // (tests: ACE_MSP_FAIL_IT) the bound of m-space iterates fails at this iteration
     int xzn;               // (apply_AH of the r-column stages) write X = (Z - N/mu) + A^H g instead of W
+    int zcert;             // four-wave A2only Z-step: skip the eigensolver when the Ky Fan certificate holds
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

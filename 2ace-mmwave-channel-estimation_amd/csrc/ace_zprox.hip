@@ -255,6 +255,41 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             }
             __syncthreads();
         }
+        // Ky Fan certificate (the one-wave kernel's): the sum of any r diagonal entries
+        // of Q^H H Q (Q unitary: the warm start, or I) is at most the sum of the r largest
+        // eigenvalues of H, so if the r_p largest diagonal entries clear f_p * trace with margin for
+        // every profile entry, no tail rescaling fires (:475) and Z = E exactly (:482).  The
+        // eigendecomposition is then skipped (Q stays the next warm start).
+        __shared__ int cert_s;
+        if (t < tx) {   // descending order of the diagonal (ties by index)
+            const double dk = L0[t * HS + t].x;
+            int rank = 0;
+            for (int j = 0; j < tx; ++j) {
+                const double dj = L0[j * HS + j].x;
+                rank += (dj > dk) || (dj == dk && j < t);
+            }
+            rs2[rank] = dk;
+        }
+        __syncthreads();
+        if (t == 0) {
+            double tr = 0.0;
+            for (int k = 0; k < tx; ++k) tr += fmax(0.0, rs2[k]);
+            int ok = tr > 0.0;
+            #pragma unroll
+            for (int pi = 0; pi < 4; ++pi) {
+                if (pi >= pf.np) break;
+                double vr = 0.0;
+                for (int k = 0; k < pf.rl[pi]; ++k) vr += rs2[k];
+                ok &= vr * (1.0 - 1e-12) > pf.fl[pi] * tr * (1.0 + 1e-9);
+            }
+            cert_s = a.zcert ? ok : 0;
+        }
+        __syncthreads();
+        const bool cert = cert_s;
+        if (cert) {
+            if (t < TXMAX) scl[t] = 1.0;
+            if (t == 0) flag_any = 0;
+        } else {
         if (jacobi_eig32(L0, L1, tx, wv, jsh) >= JAC_MAX_SWEEPS && t == 0)
             atomicOr(&st->status, (int)ACE_ST_EIG_NOCONV);
         ascending_positions(wv, tx, ascp);           // LAPACK order of eig (:428)
@@ -293,8 +328,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             for (int k = 0; k < tx; ++k) any |= scl[k] < 1.0;
             flag_any = any;
         }
+        }
         __syncthreads();
-        if (a.Q) {
+        if (a.Q && (!cert || !warm)) {   // (a certified cold step stores I: a unitary warm start)
             for (int e = t; e < tx * tx; e += nt) Qg[e] = L1[(e / tx) * HS + (e % tx)];
         }
         if (flag_any) {

@@ -150,6 +150,25 @@ def test_pipeline_int8_stage_applies(gpu, monkeypatch):
     np.testing.assert_allclose(a.quality, f.quality, rtol=0, atol=1e-10)
 
 
+@pytest.mark.parametrize("ant,m", [(32, 256), (16, 64)])
+def test_pipeline_zstep_certificate(gpu, monkeypatch, ant, m):
+    """The r-column Z-step skips its eigensolver when the Ky Fan certificate proves that no tail
+    rescaling fires (Z = E exactly, inferLowRankV4_multi.m:475-484): the same results as the
+    always-eigensolve path (ACE_ZCERT=0) to rounding, identical stage iteration counts and rollback
+    flags (32-ant / m = 256 and the 16 x 16 small-tile path)."""
+    from ace_amd import infer_low_rank_pipeline_host, synth, draw_partitions
+    A, B, _, _ = synth.problem(71, 0, 16, m, ant, ant)
+    tr = draw_partitions(np.random.default_rng(71), m, 3)
+    c = infer_low_rank_pipeline_host(A[0], B, ant, ant, tr, maxiter=120)
+    monkeypatch.setenv("ACE_ZCERT", "0")
+    f = infer_low_rank_pipeline_host(A[0], B, ant, ant, tr, maxiter=120)
+    assert np.array_equal(c.stage_iters, f.stage_iters), (c.stage_iters, f.stage_iters)
+    assert np.array_equal(c.rolled_back, f.rolled_back)
+    for b in range(16):
+        assert O.phase_aligned_rel_err(c.X[b], f.X[b]) <= 1e-8, b
+    np.testing.assert_allclose(c.quality, f.quality, rtol=0, atol=1e-10)
+
+
 def test_pipeline_matlab_signature(gpu):
     """inferLowRankV4_multi(A, B, tx, rx) with explicit partitions == the batch host call."""
     from ace_amd import inferLowRankV4_multi, infer_low_rank_pipeline_host, synth, draw_partitions

@@ -494,14 +494,20 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         # share of the realisation-iterations gyf_kernel settled in m-space form (no apply_AH pass,
         # no Z traffic: ace_prof_msp_steps); the per-launch work below is averaged with it
         msp_frac = msp_steps.value / float(args.steps * bsz * args.iters) if msp_on else 0.0
+        # the m-space runs (msr_kernel) take the steady iterations away from gyf_kernel: its launches see
+        # the m-space share of the realisation-iterations the runs did not execute (ace_prof_work counts
+        # 8 m^2 per realisation-iteration of every run launch)
+        msr_i = KERNEL_CLASSES.index("msr") if "msr" in KERNEL_CLASSES else -1
+        msr_steps = kw[msr_i] / (8.0 * m * m) if (msr_i >= 0 and kn[msr_i]) else 0.0
+        rest = float(args.steps * bsz * args.iters) - msr_steps
+        msp_frac_gyf = min(1.0, max(0.0, (msp_steps.value - msr_steps) / rest)) if (msp_on and rest > 0) else 0.0
         # private phase-code codebooks: apply_G is pgk_kernel (ace_private.hip), HBM-bound on G_b
         pc = private and os.environ.get("ACE_NO_I8") != "1" and m <= 256 and n <= 2048
-        ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac, nms=nms)
+        ctx = dict(variant=variant, pc=pc, gyf=gyf, gyk=gyk, i8=i8, msp_frac=msp_frac_gyf, nms=nms)
         timed = [k for k in kernels if k in ITER_CLASSES and unit_resources(k, m, n, **ctx)]
         # device time per class: the iteration classes are sampled on every PROF_STRIDE-th launch, the
         # m-space runs (msr, ace_i8gemm.hip::msr_kernel) on every launch; dominant = most device time
         dev_ms = {k: kernels[k]["total_ms"] * PROF_STRIDE for k in timed}
-        msr_i = KERNEL_CLASSES.index("msr") if "msr" in KERNEL_CLASSES else -1
         roof_msr = None
         if msr_i >= 0 and kn[msr_i] and kw[msr_i] > 0:
             # flops: 8 m^2 per realisation-iteration the runs executed (ace_prof_work, counted on the device)
@@ -534,7 +540,8 @@ def unit_bench(args, private, dev, rank, world, workload=None):
                 note = ("gyf_kernel runs T and g = G T (f64 3M; achieved counts 8 flops per complex MAC), the "
                         "Y-step, then W = A^H g (int8 digit planes) with the certified Z-step pass (Z in, Z' out) "
                         "in its epilogue, one phase after another in each work-group; a realisation in m-space "
-                        "form (msp_frac of the realisation-iterations) skips the int8 pass and the Z traffic and "
+                        "form (msp_frac of the realisation-iterations its launches ran: those outside the m-space "
+                        "runs) skips the int8 pass and the Z traffic and "
                         "moves S in / S' out instead (bench.msp_bytes); bound = the resource with the largest "
                         "time at peak; serial_frac = (t_f64 + t_int8 + t_hbm at peak) / launch time")
             elif variant == "A2nuclear" and i8:
@@ -543,7 +550,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             r = roofline_from(name, kernels[k]["avg_ms"] * 1e-3, res, bounds={"f64": "valu"} if pc else None,
                               note=note)
             if gyf:
-                r["msp_frac"] = round(msp_frac, 4)
+                r["msp_frac"] = round(msp_frac_gyf, 4)
             r["realisations_per_launch"] = per_launch
             # the nsplit sub-batch launches of a class run at the same time on disjoint CUs (rocprofv3
             # kernel trace, tools/timeline.py): the chip-level rate is nsplit x the per-launch rate

@@ -39,6 +39,7 @@
 namespace ace {
 
 namespace {
+
 // Phase timestamps of work-group 5 (diagnostic build only: -DACE_PHASE_STAMPS)
 #ifdef ACE_PHASE_STAMPS
 #define STAMP_DECL unsigned long long ts_[12] = {}
@@ -1101,15 +1102,12 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-            for (int k = 0; k < 5; ++k) v7[r][k] += __shfl_xor(v7[r][k], o, 64);
-            v7[r][5] = fmax(v7[r][5], __shfl_xor(v7[r][5], o, 64));
-            v7[r][6] += __shfl_xor(v7[r][6], o, 64);
-            if (GLDS && a.msp) {
-                v7[r][7] += __shfl_xor(v7[r][7], o, 64);
-                v7[r][8] += __shfl_xor(v7[r][8], o, 64);
-            }
+        for (int k = 0; k < 5; ++k) v7[r][k] = bsum16(v7[r][k]);
+        v7[r][5] = bmax16(v7[r][5]);
+        v7[r][6] = bsum16(v7[r][6]);
+        if (GLDS && a.msp) {
+            v7[r][7] = bsum16(v7[r][7]);
+            v7[r][8] = bsum16(v7[r][8]);
         }
         if ((lane & 15) == 0)
 #pragma unroll
@@ -1562,14 +1560,11 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 xv[c][r] = ax;
             }
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-                for (int k = 0; k < 5; ++k) v7[k] += __shfl_xor(v7[k], o, 64);
-                v7[5] = fmax(v7[5], __shfl_xor(v7[5], o, 64));
-                v7[6] += __shfl_xor(v7[6], o, 64);
-                v7[7] += __shfl_xor(v7[7], o, 64);
-                v7[8] += __shfl_xor(v7[8], o, 64);
-            }
+            for (int k = 0; k < 5; ++k) v7[k] = bsum16(v7[k]);
+            v7[5] = bmax16(v7[5]);
+            v7[6] = bsum16(v7[6]);
+            v7[7] = bsum16(v7[7]);
+            v7[8] = bsum16(v7[8]);
             if ((lane & 15) == 0)
 #pragma unroll
                 for (int k = 0; k < 9; ++k) red[TPW / 2 * w + h][jl][k] = v7[k];

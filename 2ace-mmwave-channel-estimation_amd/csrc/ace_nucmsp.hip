@@ -158,8 +158,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
                 }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) q[r] += __shfl_xor(q[r], o, 64);
+                q[r] = bsum16(q[r]);
                 if ((lane & 15) == 0) red[w][(lane >> 4) + 4 * r][pass] = q[r];
             }
             __syncthreads();
@@ -245,9 +244,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-            for (int k = 0; k < NSUM; ++k) v[r][k] += __shfl_xor(v[r][k], o, 64);
+        for (int k = 0; k < NSUM; ++k) v[r][k] = bsum16(v[r][k]);
         if ((lane & 15) == 0)
 #pragma unroll
             for (int k = 0; k < NSUM; ++k) red[w][(lane >> 4) + 4 * r][k] = v[r][k];

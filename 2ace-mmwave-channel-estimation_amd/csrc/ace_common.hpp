@@ -120,6 +120,32 @@ __device__ __forceinline__ int dual_finish(const DualCtl& c, RealState* st, doub
 }
 
 // wave64 reduction of a double
+// 16-lane butterfly reductions with DPP partners instead of ds_bpermute (__shfl_xor): step o pairs
+// lane l with quad_perm l^1, quad_perm l^2, row_half_mirror (7 - l within 8) and row_mirror (15 - l).
+// After the steps below o every lane of an o-group holds the same value (x + y == y + x, and max
+// likewise, bit for bit), so each partner holds lane l^o's value: the results equal the xor
+// butterfly's bit for bit, at VALU latency.
+template <int O>
+__device__ __forceinline__ double bfly16(double x) {
+    constexpr int ctrl = O == 1 ? 0xB1 : O == 2 ? 0x4E : O == 4 ? 0x141 : 0x140;
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double bsum16(double v) {
+    v += bfly16<1>(v);
+    v += bfly16<2>(v);
+    v += bfly16<4>(v);
+    v += bfly16<8>(v);
+    return v;
+}
+__device__ __forceinline__ double bmax16(double v) {
+    v = fmax(v, bfly16<1>(v));
+    v = fmax(v, bfly16<2>(v));
+    v = fmax(v, bfly16<4>(v));
+    v = fmax(v, bfly16<8>(v));
+    return v;
+}
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

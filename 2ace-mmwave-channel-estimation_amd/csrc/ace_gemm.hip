@@ -380,10 +380,7 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
                     }
                 }
 #pragma unroll
-                for (int k = 0; k < 5; ++k) {
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) v[k] += __shfl_xor(v[k], o, 64);
-                }
+                for (int k = 0; k < 5; ++k) v[k] = bsum16(v[k]);
                 if ((lane & 15) == 0) {
 #pragma unroll
                     for (int k = 0; k < 5; ++k) red[(jl * CF::WI + wi) * 5 + k] = v[k];

@@ -423,9 +423,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
             double v = 0.0;
 #pragma unroll
             for (int J = 0; J < 2; ++J) v += cr[0][J][r] * cr[0][J][r] + ci[0][J][r] * ci[0][J][r];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-            rn[r] = v;
+            rn[r] = bsum16(v);
         }
         // lane L (of each 16-lane group) takes row L = (L&3) + 4(L>>2)
         const int L16 = lane & 15;

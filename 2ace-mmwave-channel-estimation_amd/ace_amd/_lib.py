@@ -25,6 +25,7 @@ ACE_ST_CONVERGED = 1
 ACE_ST_NO_OPT = 2
 ACE_ST_EIG_NOCONV = 4
 ACE_ST_ROLLBACK = 8
+ACE_ST_RANK_ONE = 128
 
 KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final", "msr"]
 
@@ -50,6 +51,9 @@ class AdmmCfg(C.Structure):
         ("rho", C.c_double),
         ("tol_rel", C.c_double),
         ("tol_abs", C.c_double),
+        ("r", C.c_int),
+        ("reserved", C.c_int),
+        ("rank_one", C.c_void_p),
     ]
 
 

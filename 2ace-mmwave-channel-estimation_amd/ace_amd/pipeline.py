@@ -30,7 +30,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import LIB, check, pipeline_cfg, ACE_ST_ROLLBACK
+from ._lib import LIB, check, pipeline_cfg, ACE_ST_ROLLBACK, ACE_ST_RANK_ONE
 from .solver import VARIANTS
 
 
@@ -45,6 +45,12 @@ class PipelineResult:
     @property
     def rolled_back(self):
         return (self.status & ACE_ST_ROLLBACK) != 0
+
+    @property
+    def rank_one(self):
+        """The refinement's use_rank_one per realisation: the last restart ran the rank-one retry
+        (inferLowRankV4_multi.m:73-77, passed at :92/:100)."""
+        return (self.status & ACE_ST_RANK_ONE) != 0
 
 
 def _cfg(variant, restarts, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm):

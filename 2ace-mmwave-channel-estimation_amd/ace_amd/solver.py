@@ -39,6 +39,7 @@ class BatchResult:
     iters: object      # [batch] int32
     status: object     # [batch] uint32 (ACE_ST_* bits)
     mu: object         # [batch] float64
+    rank_one: object = None   # the per-realisation flags the solve was given (device), if any
 
     @property
     def converged(self):
@@ -46,12 +47,31 @@ class BatchResult:
 
 
 def _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-         eig_warm, f64_applies=False):
+         eig_warm, f64_applies=False, r=1):
     return default_cfg(variant=VARIANTS[variant], scale_by_row=int(bool(scale_by_row)),
                        use_rank_one=int(bool(use_rank_one)), mu0=float(mu0), rho=float(rho),
                        tol_rel=float(tol_rel), tol_abs=float(tol_abs), maxiter=int(maxiter),
                        fixed_iters=int(bool(fixed_iters)), a_shared=int(bool(a_shared)),
-                       eig_warm=int(bool(eig_warm)), f64_applies=int(bool(f64_applies)))
+                       eig_warm=int(bool(eig_warm)), f64_applies=int(bool(f64_applies)), r=int(r))
+
+
+def _flags(use_rank_one, batch):
+    """use_rank_one as (batch-wide bool, per-realisation uint8 array or None)."""
+    shp = getattr(use_rank_one, "shape", None)
+    if shp is None and isinstance(use_rank_one, (list, tuple)):
+        shp = (len(use_rank_one),)
+    if shp is None or len(shp) == 0:
+        return bool(use_rank_one), None
+    return False, use_rank_one
+
+
+def _cols(X0, batch, n):
+    """X0 [batch][n] or [batch][r][n] -> r (columns per realisation, :281 X0 is n x r)."""
+    if X0.ndim == 2 and tuple(X0.shape) == (batch, n):
+        return 1
+    if X0.ndim == 3 and X0.shape[0] == batch and X0.shape[2] == n and 1 <= X0.shape[1] <= 32:
+        return int(X0.shape[1])
+    raise ValueError(f"X0 must be [batch][n] or [batch][r][n] with r <= 32, got {tuple(X0.shape)}")
 
 
 def _dp(a):
@@ -65,41 +85,58 @@ def InferADMM(A, B, X0, scale_by_row, use_rank_one, tx, rx, lambda_=0.0, mu0=1e-
 
     ``U``/``D`` are accepted for signature parity and ignored: the GPU path forms
     its own (I + A A^H)^{-1} (algebraically identical to U = inv(A'A + I)).
-    Only lambda = 0 (the value every reference driver reaches) and r = 1
-    (size(X0, 2) == 1, the refinement stage) run on the GPU.
+    Only lambda = 0 (the value every reference driver reaches) runs on the GPU.  X0 is n x r
+    (r <= 32): r = 1 is the refinement stage (:92/:100), r = 20 the stages of inferLowRankImpl
+    (:258 with scale_by_row, :270 without: X, Y are then the best column, :352-361).
     """
     if lambda_ != 0:
         raise NotImplementedError("lambda != 0 is unreachable from the reference drivers and not implemented")
     A = np.ascontiguousarray(A, dtype=np.complex128)
     m, n = A.shape
     X0 = np.asarray(X0, dtype=np.complex128)
-    if X0.ndim == 2 and X0.shape[1] != 1:
-        raise NotImplementedError("GPU InferADMM implements r = 1 (refinement stage) only")
-    X0 = np.ascontiguousarray(X0.reshape(n))
+    X0 = X0.reshape(n, -1)
+    r = X0.shape[1]
+    if r > 32:
+        raise NotImplementedError("GPU InferADMM implements r <= 32 columns")
+    X0 = np.ascontiguousarray(X0.T)[None]                   # [1][r][n]: column j contiguous
     B = np.ascontiguousarray(np.asarray(B, dtype=np.float64).reshape(m))
-    res = infer_admm_host(A[None], B[None], X0[None], tx, rx, variant=variant, scale_by_row=scale_by_row,
-                          use_rank_one=use_rank_one, mu0=mu0, rho=rho, tol_rel=tol_rel, tol_abs=tol_abs,
-                          maxiter=maxiter, fixed_iters=fixed_iters, eig_warm=eig_warm)
-    return res.X[0].reshape(n, 1), res.Y[0].reshape(m, 1), bool(res.converged[0])
+    res = infer_admm_host(A[None], B[None], X0 if r > 1 else X0[:, 0], tx, rx, variant=variant,
+                          scale_by_row=scale_by_row, use_rank_one=use_rank_one, mu0=mu0, rho=rho, tol_rel=tol_rel,
+                          tol_abs=tol_abs, maxiter=maxiter, fixed_iters=fixed_iters, eig_warm=eig_warm)
+    R = r if scale_by_row else 1
+    return res.X[0].reshape(R, n).T.copy(), res.Y[0].reshape(R, m).T.copy(), bool(res.converged[0])
 
 
 def infer_admm_host(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, use_rank_one=False, mu0=1e-3,
                     rho=1.03, tol_rel=1e-4, tol_abs=1e-8, maxiter=500, fixed_iters=False, eig_warm=True,
                     f64_applies=False):
-    """Batch solve on host numpy arrays: A [1|batch][m][n], B [batch][m], X0 [batch][n].
-    ``f64_applies`` keeps the f64 matrix-core applies for phase-code codebooks too."""
+    """Batch solve on host numpy arrays: A [1|batch][m][n], B [batch][m], X0 [batch][n] or
+    [batch][r][n] (r > 1: shared A).  ``use_rank_one``: one flag for the batch or one per
+    realisation (the refinement of a batch of pipelines, inferLowRankV4_multi.m:92/:100).
+    ``f64_applies`` keeps the f64 matrix-core applies for phase-code codebooks too.
+    X, Y: [batch][n] / [batch][m] at r = 1, else [batch][R][n] / [batch][R][m] with
+    R = r (scale_by_row) or 1 (per-column mode: the best column)."""
     A = np.ascontiguousarray(A, dtype=np.complex128)
     B = np.ascontiguousarray(B, dtype=np.float64)
     X0 = np.ascontiguousarray(X0, dtype=np.complex128)
     batch, m = B.shape
-    n = X0.shape[1]
-    if A.ndim != 3 or A.shape[1:] != (m, n) or A.shape[0] not in (1, batch) or X0.shape[0] != batch:
+    n = X0.shape[-1]
+    r = _cols(X0, batch, n)
+    if A.ndim != 3 or A.shape[1:] != (m, n) or A.shape[0] not in (1, batch):
         raise ValueError(f"shape mismatch: A{A.shape} B{B.shape} X0{X0.shape}")
     a_shared = A.shape[0] == 1
-    cfg = _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-               eig_warm, f64_applies)
-    X = np.empty((batch, n), np.complex128)
-    Y = np.empty((batch, m), np.complex128)
+    uro, flags = _flags(use_rank_one, batch)
+    cfg = _cfg(variant, scale_by_row, uro, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
+               eig_warm, f64_applies, r)
+    if flags is not None:
+        flags = np.ascontiguousarray(np.asarray(flags).reshape(-1) != 0, dtype=np.uint8)
+        if flags.shape != (batch,):
+            raise ValueError(f"use_rank_one must be a scalar or one flag per realisation ({batch})")
+        cfg.rank_one = flags.ctypes.data
+    R = r if scale_by_row else 1
+    shp = (batch,) if X0.ndim == 2 else (batch, R)
+    X = np.empty(shp + (n,), np.complex128)
+    Y = np.empty(shp + (m,), np.complex128)
     it = np.empty(batch, np.int32)
     stt = np.empty(batch, np.uint32)
     mu = np.empty(batch, np.float64)
@@ -131,9 +168,12 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
                      f64_applies=False, out=None, workspace=None, stream=None):
     """Batched InferADMM on device tensors (torch, complex128 / float64, contiguous).
 
-    A: [1|batch][m][n] (1 = shared codebook), B: [batch][m], X0: [batch][n].
-    Returns BatchResult of device tensors; asynchronous on ``stream`` (default:
-    torch's current stream) except for the convergence polls of early-exit mode.
+    A: [1|batch][m][n] (1 = shared codebook), B: [batch][m], X0: [batch][n] or [batch][r][n]
+    (r <= 32, shared A).  ``use_rank_one``: a bool for the whole batch, or one flag per
+    realisation (a device tensor, or a host array uploaded here) -- the refinement of a batch of
+    pipelines passes each realisation's last-restart flag (inferLowRankV4_multi.m:73-77, :92/:100;
+    PipelineResult.rank_one).  Returns BatchResult of device tensors; asynchronous on ``stream``
+    (default: torch's current stream) except for the convergence polls of early-exit mode.
     """
     import torch
     if not (A.is_cuda and B.is_cuda and X0.is_cuda):
@@ -142,16 +182,26 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
         raise TypeError("A, X0 must be complex128 and B float64")
     A, B, X0 = A.contiguous(), B.contiguous(), X0.contiguous()
     batch, m = B.shape
-    n = X0.shape[1]
-    if A.dim() != 3 or tuple(A.shape[1:]) != (m, n) or A.shape[0] not in (1, batch) or X0.shape[0] != batch:
+    n = X0.shape[-1]
+    r = _cols(X0, batch, n)
+    if A.dim() != 3 or tuple(A.shape[1:]) != (m, n) or A.shape[0] not in (1, batch):
         raise ValueError(f"shape mismatch: A{tuple(A.shape)} B{tuple(B.shape)} X0{tuple(X0.shape)}")
     a_shared = A.shape[0] == 1
-    cfg = _cfg(variant, scale_by_row, use_rank_one, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
-               eig_warm, f64_applies)
+    uro, flags = _flags(use_rank_one, batch)
+    cfg = _cfg(variant, scale_by_row, uro, mu0, rho, tol_rel, tol_abs, maxiter, fixed_iters, a_shared,
+               eig_warm, f64_applies, r)
     dev = A.device
+    if flags is not None:
+        flags = torch.as_tensor(flags).reshape(-1).to(device=dev)
+        flags = (flags != 0).to(torch.uint8).contiguous()
+        if flags.numel() != batch:
+            raise ValueError(f"use_rank_one must be a scalar or one flag per realisation ({batch})")
+        cfg.rank_one = flags.data_ptr()
+    R = r if scale_by_row else 1
+    shp = (batch,) if X0.dim() == 2 else (batch, R)
     if out is None:
-        out = BatchResult(torch.empty((batch, n), dtype=torch.complex128, device=dev),
-                          torch.empty((batch, m), dtype=torch.complex128, device=dev),
+        out = BatchResult(torch.empty(shp + (n,), dtype=torch.complex128, device=dev),
+                          torch.empty(shp + (m,), dtype=torch.complex128, device=dev),
                           torch.empty(batch, dtype=torch.int32, device=dev),
                           torch.empty(batch, dtype=torch.int32, device=dev),
                           torch.empty(batch, dtype=torch.float64, device=dev))
@@ -163,6 +213,8 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
                                    out.X.data_ptr(), out.Y.data_ptr(), out.iters.data_ptr(),
                                    out.status.data_ptr(), out.mu.data_ptr(), ws.data_ptr(), ws.numel(),
                                    stream.cuda_stream))
+    if flags is not None:
+        out.rank_one = flags   # (kept alive until the asynchronous solve has read it)
     return out
 
 

@@ -2,6 +2,7 @@
 // ace_admm_solve_batch (InferADMM at r = 1, main/src/my_recovery_algorithms/ADMM_v2/
 // inferLowRankV4_multi.m:281-386, driven by admm_run in ace_admm.cpp), its host-buffer
 // wrapper, synthetic traces, kernel timing, error text and version.
+#include <algorithm>
 #include <cstring>
 
 #include "ace_host.hpp"
@@ -9,6 +10,8 @@
 using namespace ace;
 
 namespace {
+int cols(const ace_admm_cfg* c) { return c->r == 0 ? 1 : c->r; }   // r = 0: the refinement stage, r = 1
+
 int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
     if (!c) return fail(ACE_ERR_ARG, "cfg is NULL");
     if (batch < 1 || m < 1 || n < 1) return fail(ACE_ERR_ARG, "batch/m/n must be >= 1 (got %d/%d/%d)", batch, m, n);
@@ -20,6 +23,9 @@ int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
     if (n > 4096 || m > 4096) return fail(ACE_ERR_UNSUPPORTED, "m, n must be <= 4096 (got %d, %d)", m, n);
     if (c->maxiter < 1) return fail(ACE_ERR_ARG, "maxiter must be >= 1");
     if (!(c->mu0 > 0) || !(c->rho > 0)) return fail(ACE_ERR_ARG, "mu0 and rho must be > 0");
+    const int r = cols(c);
+    if (r < 1 || r > 32) return fail(ACE_ERR_UNSUPPORTED, "r must be in [1, 32] (got %d)", r);
+    if (r > 1 && !c->a_shared) return fail(ACE_ERR_UNSUPPORTED, "r > 1 needs a shared A (a_shared = 1)");
     return ACE_OK;
 }
 }  // namespace
@@ -121,6 +127,8 @@ void ace_admm_cfg_default(ace_admm_cfg* c) {
     c->rho = 1.03;
     c->tol_rel = 1e-4;
     c->tol_abs = 1e-8;
+    c->r = 1;
+    c->rank_one = nullptr;
 }
 
 size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n) {
@@ -129,7 +137,7 @@ size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n)
     LinOps L;
     AdmmState w;
     linops_carve(cv, cfg->a_shared != 0, batch, m, n, &L);
-    admm_state_carve(cv, batch, m, n, 1, &w);
+    admm_state_carve(cv, batch, m, n, std::max(1, cols(cfg)), &w);
     return cv.off + 256;
 }
 
@@ -149,14 +157,14 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     LinOps L;
     AdmmState w;
     linops_carve(cv, cfg->a_shared != 0, batch, m, n, &L);
-    admm_state_carve(cv, batch, m, n, 1, &w);
+    admm_state_carve(cv, batch, m, n, cols(cfg), &w);
     L.A = A;
     L.allow_i8 = cfg->f64_applies == 0;
     ACE_TRY(linops_setup(L, batch, st));
     AdmmParams p{};
     p.variant = cfg->variant;
-    p.r = 1;
-    p.row_mode = 1;
+    p.r = cols(cfg);
+    p.row_mode = cfg->scale_by_row != 0;
     p.maxiter = cfg->maxiter;
     p.fixed_iters = cfg->fixed_iters;
     p.eig_warm = cfg->eig_warm;
@@ -167,7 +175,7 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     p.tx = tx;
     p.rx = rx;
     p.use_rank_one = cfg->use_rank_one;
-    p.rank_one = nullptr;
+    p.rank_one = cfg->rank_one;
     return admm_run(L, p, w, batch, B, X0, Xo, Yo, iters, status, mu_out, st);
 }
 
@@ -177,8 +185,10 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
     g_err.clear();
     int rc = validate(cfg, batch, m, n, tx, rx);
     if (rc) return rc;
+    const int r = cols(cfg), R = cfg->scale_by_row ? r : 1;
     const size_t nA = (size_t)(cfg->a_shared ? 1 : batch) * m * n * 16;
-    const size_t nB = (size_t)batch * m * 8, nX = (size_t)batch * n * 16, nY = (size_t)batch * m * 16;
+    const size_t nB = (size_t)batch * m * 8, nX0 = (size_t)batch * r * n * 16, nX = (size_t)batch * R * n * 16,
+                 nY = (size_t)batch * R * m * 16;
     const size_t ws = ace_admm_workspace_size(cfg, batch, m, n) + 4096;
     std::vector<void*> bufs;
     auto dalloc = [&](size_t bytes, void** p) -> hipError_t {
@@ -190,11 +200,12 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
         for (void* p : bufs) (void)hipFree(p);
         bufs.clear();
     };
-    void *dA, *dB, *dX0, *dX, *dY, *dW, *dI, *dS, *dM;
+    void *dA, *dB, *dX0, *dX, *dY, *dW, *dI, *dS, *dM, *dR = nullptr;
     hipError_t e = hipSuccess;
-    if ((e = dalloc(nA, &dA)) || (e = dalloc(nB, &dB)) || (e = dalloc(nX, &dX0)) || (e = dalloc(nX, &dX)) ||
+    if ((e = dalloc(nA, &dA)) || (e = dalloc(nB, &dB)) || (e = dalloc(nX0, &dX0)) || (e = dalloc(nX, &dX)) ||
         (e = dalloc(nY, &dY)) || (e = dalloc(ws, &dW)) || (e = dalloc(4 * (size_t)batch, &dI)) ||
-        (e = dalloc(4 * (size_t)batch, &dS)) || (e = dalloc(8 * (size_t)batch, &dM))) {
+        (e = dalloc(4 * (size_t)batch, &dS)) || (e = dalloc(8 * (size_t)batch, &dM)) ||
+        (cfg->rank_one && (e = dalloc((size_t)batch, &dR)))) {
         cleanup();
         return fail(ACE_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
     }
@@ -208,8 +219,13 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
     } while (0)
     ACE_HIPC(hipMemcpy(dA, A, nA, hipMemcpyHostToDevice));
     ACE_HIPC(hipMemcpy(dB, B, nB, hipMemcpyHostToDevice));
-    ACE_HIPC(hipMemcpy(dX0, X0, nX, hipMemcpyHostToDevice));
-    rc = ace_admm_solve_batch(cfg, batch, m, n, tx, rx, (const double*)dA, (const double*)dB, (const double*)dX0,
+    ACE_HIPC(hipMemcpy(dX0, X0, nX0, hipMemcpyHostToDevice));
+    ace_admm_cfg dcfg = *cfg;   // the per-realisation flags, if any, as a device array
+    if (cfg->rank_one) {
+        ACE_HIPC(hipMemcpy(dR, cfg->rank_one, (size_t)batch, hipMemcpyHostToDevice));
+        dcfg.rank_one = (const uint8_t*)dR;
+    }
+    rc = ace_admm_solve_batch(&dcfg, batch, m, n, tx, rx, (const double*)dA, (const double*)dB, (const double*)dX0,
                               (double*)dX, (double*)dY, (int32_t*)dI, (uint32_t*)dS, (double*)dM, dW, ws, nullptr);
     if (rc) {
         std::string keep = g_err;

@@ -34,6 +34,8 @@ void launch_finish(int n, int m, int mt, int batch, const double* qlast, const d
 // dst[(idx ? idx[k] : k) * ld + col] = src[k] (or_mask 0) or |= src[k] & or_mask, k < count
 void launch_put_col(int count, const int* src, const int* idx, int* dst, int ld, int col, unsigned or_mask,
                     hipStream_t st);
+// dst[k] |= bit where flag[k] != 0, k < count
+void launch_flag_bits(int count, const unsigned char* flag, int* dst, unsigned bit, hipStream_t st);
 void launch_fill(long long count, double v, double* dst, hipStream_t st);
 
 // ---- SpectralInitialize (:561-574) through the m_t x m_t dual Gram (ace_spectral.hip)

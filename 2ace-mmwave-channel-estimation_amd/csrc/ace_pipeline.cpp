@@ -460,6 +460,8 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         ACE_TRY(rct);
     }
 
+    // the refinement's profile (:92/:100: the last restart's use_rank_one), reported per realisation
+    if (cfg->variant == ACE_VARIANT_A2ONLY) launch_flag_bits(batch, w.rank_one, w.status_dev, ACE_ST_RANK_ONE, st);
     if (cfg->stop_before_refine) {   // X_max and Y_max (on the train rows), rescaled; no rollback test
         launch_fill(batch, -1.0, w.rw[0].q_s, st);
         ACE_HIP(hipMemsetAsync(w.Yr, 0, 16 * (size_t)batch * m, st));

@@ -426,6 +426,11 @@ __global__ __launch_bounds__(256) void put_col_kernel(int count, const int* src,
     dst[o] = or_mask ? (int)((unsigned)dst[o] | ((unsigned)src[k] & or_mask)) : src[k];
 }
 
+__global__ __launch_bounds__(256) void flag_bits_kernel(int count, const unsigned char* flag, int* dst, unsigned bit) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < count && flag[k]) dst[k] = (int)((unsigned)dst[k] | bit);
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(long long count, double v, double* dst) {
     const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < count) dst[k] = v;
@@ -495,6 +500,9 @@ void launch_put_col(int count, const int* src, const int* idx, int* dst, int ld,
     if (count > 0)
         hipLaunchKernelGGL(put_col_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, src, idx, dst, ld, col,
                            or_mask);
+}
+void launch_flag_bits(int count, const unsigned char* flag, int* dst, unsigned bit, hipStream_t st) {
+    if (count > 0) hipLaunchKernelGGL(flag_bits_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, flag, dst, bit);
 }
 void launch_fill(long long count, double v, double* dst, hipStream_t st) {
     if (count > 0) hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, count, v, dst);

@@ -412,6 +412,8 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     A, B, X0, H = synth_problem(args.seed, first, bsz, m, tx, tx, a_shared=not private, device=dev, A=wl.get("A"))
     if wl.get("X0") is not None:
         X0 = wl["X0"]
+    # per-realisation use_rank_one (the refinement's profile, inferLowRankV4_multi.m:73-77, :92/:100)
+    r1 = wl.get("rank_one", False)
     ws = ace_amd.solver.Workspace()
     outs, pend, nstep = [None, None], [None, None], [0]
 
@@ -424,7 +426,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             pend[i].wait()
             pend[i] = None
         outs[i] = infer_admm_batch(A, B, X0, tx, tx, variant=variant, maxiter=args.iters, fixed_iters=True,
-                                   out=outs[i], workspace=ws)
+                                   use_rank_one=r1, out=outs[i], workspace=ws)
         if world > 1:
             pend[i] = gather_to_root_async(outs[i].X, counts)
         nstep[0] += 1
@@ -620,11 +622,13 @@ def unit_bench(args, private, dev, rank, world, workload=None):
 
 
 def refine_input_bench(args, dev, rank, world):
-    """The unit on the reference's own refinement input: X0 = X_max of the 3-restart pipeline
+    """The unit on the reference's own refinement: X0 = X_max of the 3-restart pipeline
     (inferLowRankV4_multi.m:90-92: spectral init, the r = 20 stages, rank-one retries, best of
-    restarts) on the same synthetic batch, instead of the bench's H + 0.5 noise warm start.  The
-    synthetic A has ||A||_F = sqrt(m) and B is unit-norm, so X_max is already in the unit's
-    coordinates (A_norm = B_norm = 1, :27-38)."""
+    restarts) on the same synthetic batch, and each realisation's own use_rank_one -- the last
+    restart's (:73-77), which selects the [1]/[0.95] rank profile (:448-450) of the refinement
+    (:92/:100); ACE_ST_RANK_ONE of the pipeline.  The synthetic A has ||A||_F = sqrt(m) and B is
+    unit-norm, so X_max is already in the unit's coordinates (A_norm = B_norm = 1, :27-38).  Also
+    reports the same X0 with the default profile for every realisation (the round-3 measurement)."""
     import torch
     from ace_amd import synth_problem, infer_low_rank_pipeline_batch, draw_partitions
     tx, m, bsz = args.tx, args.m, args.batch
@@ -635,9 +639,11 @@ def refine_input_bench(args, dev, rank, world):
     torch.cuda.synchronize()
     t_pipe = time.perf_counter() - t0
     X0 = pr.X.contiguous()
+    flags = pr.rank_one.to(torch.uint8).contiguous()
     saved = args.no_cpu_baseline
     args.no_cpu_baseline = True
-    line = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max"})
+    line = unit_bench(args, False, dev, rank, world, {"X0": X0, "rank_one": flags, "x0_note": "pipeline X_max"})
+    line0 = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max, default profile"})
     args.no_cpu_baseline = saved
     if rank != 0:
         return None
@@ -646,9 +652,15 @@ def refine_input_bench(args, dev, rank, world):
             "msp_frac": line["msp_frac"],
             "x0": "X_max of inferLowRankV4_multi's 3 restarts (:90-92) on the same batch (ace_pipeline_solve_batch "
                   "with stop_before_refine)",
+            "rank_one_frac": round(float(flags.float().mean().item()), 4),
+            "profile": "per realisation: the last restart's use_rank_one (:73-77, :92/:100; ACE_ST_RANK_ONE)",
             "pipeline_s": round(t_pipe, 2), "quality_median": float(np.median(q)),
-            "roofline_frac": line["roofline"]["frac"] if line["roofline"] else None,
-            "kernels_ms": line["kernels_ms"], "checks": line["checks"]}
+            "roofline": line["roofline"], "roofline_msr": line["roofline_msr"],
+            "kernels_ms": line["kernels_ms"], "checks": line["checks"],
+            "default_profile": {"value": line0["value"], "ms_per_step": line0["ms_per_step"],
+                                "msp_frac": line0["msp_frac"],
+                                "note": "the same X0 with use_rank_one = 0 for every realisation (not the "
+                                        "reference's refinement for rank_one_frac of them)"}}
 
 
 def config5_workload(args, rank, world, dev):

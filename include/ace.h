@@ -74,11 +74,16 @@ extern "C" {
 #define ACE_ST_NO_OPT 2u      /* objective never finite: returned last iterate (reference would raise) */
 #define ACE_ST_EIG_NOCONV 4u  /* Z-prox Jacobi hit its sweep cap at least once */
 #define ACE_ST_ROLLBACK 8u    /* pipeline: refinement rolled back to X_max (inferLowRankV4_multi.m:94-98) */
+#define ACE_ST_RANK_ONE 128u  /* pipeline: the last restart ran the rank-one retry (:73-77), so the refinement
+                                 (:92/:100) uses the [1]/[0.95] profile -- set with stop_before_refine too, so a
+                                 caller can hand the refinement's flags to ace_admm_cfg::rank_one */
 
 typedef struct ace_admm_cfg {
     int variant;       /* ACE_VARIANT_* */
-    int scale_by_row;  /* 1: row-wise magnitude step (refinement); at r = 1 both modes coincide */
-    int use_rank_one;  /* ArgMinZ rank profile [1] / [0.95] (inferLowRankV4_multi.m:448-450) */
+    int scale_by_row;  /* 1: row-wise magnitude step (:300-308, :344-351); 0: per-column (:352-361).  The two
+                          coincide at r = 1 */
+    int use_rank_one;  /* ArgMinZ rank profile [1] / [0.95] (inferLowRankV4_multi.m:448-450) for every
+                          realisation, unless rank_one is given */
     int maxiter;       /* 500 in the reference (:13) */
     int fixed_iters;   /* 1: throughput mode -- run exactly maxiter iterations (no early exit) */
     int a_shared;      /* 1: one A for the whole batch (shared codebook); 0: private A per realisation */
@@ -89,26 +94,36 @@ typedef struct ace_admm_cfg {
     double rho;        /* 1.03   (:8) */
     double tol_rel;    /* 1e-4   (:10) */
     double tol_abs;    /* 1e-8   (:11) */
+    int r;             /* columns of X0: 1 (0 = 1) is the refinement stage (:92/:100); up to 32 on a shared A
+                          (a_shared = 1): the r-column stages of inferLowRankImpl (:258 row-scaled, :270
+                          per-column) */
+    int reserved;
+    /* Per-realisation use_rank_one [batch] (0/1 bytes, in the same memory space as the solve's other
+     * buffers: device for ace_admm_solve_batch, host for ace_admm_solve_host), or NULL: use_rank_one for
+     * every realisation.  The refinement of a batch of inferLowRankV4_multi calls passes each call's own
+     * last-restart flag (:73-77, :92/:100): ACE_ST_RANK_ONE of ace_pipeline_solve_batch. */
+    const uint8_t* rank_one;
 } ace_admm_cfg;
 
 /* Fill cfg with the reference defaults (inferLowRankV4_multi.m:6-14), variant A2only,
- * refinement stage (scale_by_row = 1), shared A, convergence enabled. */
+ * refinement stage (r = 1, scale_by_row = 1), shared A, convergence enabled. */
 void ace_admm_cfg_default(ace_admm_cfg* cfg);
 
-/* Workspace bytes needed by ace_admm_solve_batch for this problem. */
+/* Workspace bytes needed by ace_admm_solve_batch for this problem (cfg->r columns). */
 size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n);
 
-/* Batched InferADMM at r = 1 on device buffers.
+/* Batched InferADMM on device buffers (r = cfg->r columns; R = scale_by_row ? r : 1 output columns).
  *   A      [a_shared?1:batch][m][n] c128      sensing matrix (codebook rows)
  *   B      [batch][m] f64                     RSS magnitudes
- *   X0     [batch][n] c128                    initial iterate
- *   X, Y   [batch][n] / [batch][m] c128 out   best-objective iterate (opt_X, opt_Y)
+ *   X0     [batch][r][n] c128                 initial iterate (column j of realisation b contiguous)
+ *   X, Y   [batch][R][n] / [batch][R][m] c128 out  best-objective iterate (opt_X, opt_Y; per-column mode
+ *                                             returns the best column, :352-361)
  *   iters  [batch] int32 out (may be NULL)    iterations run
  *   status [batch] uint32 out (may be NULL)   ACE_ST_* bits
  *   mu     [batch] f64 out (may be NULL)      final penalty mu
  * Constraints: n == tx*rx, tx <= 32, rx <= 32 (tx, rx in {4,8,16,32} in the reference),
- * m >= 1.  Returns once all kernels are enqueued; in convergence mode
- * (fixed_iters == 0) the host polls a device flag every few iterations and so
+ * m >= 1, 1 <= r <= 32 (r > 1: shared A only).  Returns once all kernels are enqueued; in
+ * convergence mode (fixed_iters == 0) the host polls a device flag every few iterations and so
  * synchronises `stream` periodically. */
 int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx,
                          const double* A, const double* B, const double* X0,

@@ -302,6 +302,8 @@ class PipelineResult:
     stage_iters: list
     restart_quality: list
     rolled_back: bool
+    use_rank_one: bool = False     # the refinement's profile: the last restart's retry ran (:73-77, :92)
+    X_max: np.ndarray = None       # the refinement's input (:90-92), rescaled like X (:106)
 
 
 def infer_low_rank_pipeline(A, B, tx, rx, train_idx_list, *, variant=VARIANT_A2ONLY, r=20,
@@ -369,7 +371,8 @@ def infer_low_rank_pipeline(A, B, tx, rx, train_idx_list, *, variant=VARIANT_A2O
             rolled_back = True
     Xf = Xf * (B_norm / A_norm)                                  # :106-107
     Yf = Yf * (B_norm / A_norm)
-    return PipelineResult(Xf.ravel(), Yf.ravel(), float(quality), stage_iters, qualities, rolled_back)
+    return PipelineResult(Xf.ravel(), Yf.ravel(), float(quality), stage_iters, qualities, rolled_back,
+                          bool(use_rank_one), (X_max * (B_norm / A_norm)).ravel())
 
 
 # ----------------------------------------------------------------------------

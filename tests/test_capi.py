@@ -38,6 +38,7 @@ def test_cfg_defaults_match_reference():
     c = ace_amd.default_cfg()
     assert (c.maxiter, c.mu0, c.rho, c.tol_rel, c.tol_abs) == (500, 1e-3, 1.03, 1e-4, 1e-8)
     assert c.variant == ace_amd.ACE_VARIANT_A2ONLY and c.scale_by_row == 1 and c.a_shared == 1
+    assert c.r == 1 and not c.rank_one     # the refinement stage, one flag for the batch
     with pytest.raises(TypeError):
         ace_amd.default_cfg(no_such_field=1)
 
@@ -50,6 +51,8 @@ def test_workspace_size():
     # 6 n-vectors (X Z N V optX Q) + 9 m-vectors + K, G, A^H, per-realisation state
     assert 4096 * (6 * 1024 + 9 * 256) * 16 < w < 2 * 4096 * (6 * 1024 + 9 * 256) * 16
     assert lib.ace_admm_workspace_size(C.byref(c), 0, 256, 1024) == 0
+    c20 = ace_amd.default_cfg(r=20)          # the r-column stages carry r columns of state
+    assert lib.ace_admm_workspace_size(C.byref(c20), 64, 256, 1024) > 64 * 20 * 6 * 1024 * 16
     cp = ace_amd.default_cfg(a_shared=0)
     assert lib.ace_admm_workspace_size(C.byref(cp), 8, 256, 1024) > 8 * 2 * 256 * 256 * 16
 
@@ -60,6 +63,8 @@ def test_workspace_size():
     ({"variant": 7}, 4, 4, "unknown variant"),
     ({"maxiter": 0}, 4, 4, "maxiter"),
     ({"mu0": 0.0}, 4, 4, "mu0"),
+    ({"r": 33}, 4, 4, "r must be in"),
+    ({"r": 2, "a_shared": 0}, 4, 4, "shared A"),
 ])
 def test_validation_errors(kw, tx, rx, msg):
     """Validation runs before any HIP call; NULL buffers make a missed check fail safely."""
@@ -85,8 +90,11 @@ def test_host_api_shape_checks():
     import ace_amd
     with pytest.raises(ValueError):
         ace_amd.infer_admm_host(np.zeros((2, 4, 16), complex), np.ones((3, 4)), np.ones((3, 16), complex), 4, 4)
-    with pytest.raises(NotImplementedError):
-        ace_amd.InferADMM(np.zeros((4, 16), complex), np.ones(4), np.ones((16, 2), complex), True, False, 4, 4)
+    with pytest.raises(NotImplementedError):   # r <= 32 columns (the reference's stages use r = 20)
+        ace_amd.InferADMM(np.zeros((4, 16), complex), np.ones(4), np.ones((16, 33), complex), True, False, 4, 4)
+    with pytest.raises(ValueError):            # one use_rank_one flag per realisation
+        ace_amd.infer_admm_host(np.zeros((1, 4, 16), complex), np.ones((3, 4)), np.ones((3, 16), complex), 4, 4,
+                                use_rank_one=np.ones(2, bool))
     with pytest.raises(NotImplementedError):
         ace_amd.InferADMM(np.zeros((4, 16), complex), np.ones(4), np.ones(16, complex), True, False, 4, 4,
                           lambda_=0.1)

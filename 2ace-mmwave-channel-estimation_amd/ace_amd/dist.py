@@ -5,7 +5,9 @@ reference (it ``parfor``s over them: Numerical_Simulation/main_programs/
 Vs_M_par.m:145); nothing is exchanged while solving.  Each rank takes a
 contiguous block of the global batch and the recovered channels are collected
 on rank 0 with a single gather (RCCL over xGMI with the "nccl" backend, or gloo
-on CPU).
+on CPU).  The gather carries the whole per-realisation result of SURVEY.md §8(e) -- X, quality,
+iteration counts and status -- packed into one byte row per realisation (gather_results_async), so
+one collective moves everything.
 """
 from __future__ import annotations
 
@@ -91,3 +93,77 @@ def gather_to_root_async(local, counts, group=None):
     bufs = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
     work = dist.gather(send, gather_list=bufs, dst=0, group=group, async_op=True)
     return PendingGather(work, bufs, counts, cplx)
+
+
+# ---- the §8(e) payload in one collective ---------------------------------------------------------
+def _as_rows(t):
+    """[count, ...] tensor -> [count, nbytes] uint8 view (complex as (re, im) pairs)."""
+    import torch
+    t = t.contiguous()
+    if t.is_complex():
+        t = torch.view_as_real(t)
+    t = t.reshape(t.shape[0], -1).contiguous()
+    return t.view(torch.uint8) if t.dtype != torch.uint8 else t
+
+
+def pack_results(fields):
+    """Pack per-realisation results {name: tensor [count, ...]} into one uint8 tensor [count, row_bytes]
+    (fields in the given order, each row 8-byte aligned) and the layout needed to unpack it."""
+    import torch
+    rows, layout, off = [], [], 0
+    count = None
+    for name, t in fields.items():
+        if t is None:
+            continue
+        if count is None:
+            count = t.shape[0]
+        if t.shape[0] != count:
+            raise ValueError(f"field {name!r} has {t.shape[0]} rows, expected {count}")
+        r = _as_rows(t)
+        layout.append((name, off, r.shape[1], t.dtype, tuple(t.shape[1:])))
+        rows.append(r)
+        off += r.shape[1]
+    pad = (-off) % 8
+    if pad:
+        rows.append(torch.zeros((count, pad), dtype=torch.uint8, device=rows[0].device))
+    return torch.cat(rows, dim=1).contiguous(), layout
+
+
+def unpack_results(buf, layout):
+    """Inverse of pack_results on the gathered [total, row_bytes] buffer: {name: tensor [total, ...]}."""
+    import torch
+    out = {}
+    for name, off, nb, dtype, shape in layout:
+        cols = buf[:, off:off + nb].contiguous()
+        if dtype.is_complex:
+            real = torch.float64 if dtype == torch.complex128 else torch.float32
+            v = torch.view_as_complex(cols.view(real).reshape((buf.shape[0],) + shape + (2,)))
+        else:
+            v = cols.view(dtype).reshape((buf.shape[0],) + shape)
+        out[name] = v
+    return out
+
+
+class PendingResults:
+    """An in-flight gather_results_async: ``wait()`` returns {name: tensor} on rank 0, None elsewhere."""
+
+    def __init__(self, pend, layout):
+        self.pend, self.layout = pend, layout
+
+    def wait(self):
+        buf = self.pend.wait()
+        return None if buf is None else unpack_results(buf, self.layout)
+
+
+def gather_results_async(fields, counts, group=None):
+    """Gather every rank's per-realisation results to rank 0 in ONE collective (X +
+    quality + iteration counts + status): the fields are packed into one byte row per realisation,
+    ragged shards padded to the largest count.  ``fields``: {name: tensor [count, ...]} (None values
+    are skipped); the tensors must stay unchanged until ``wait()``."""
+    buf, layout = pack_results(fields)
+    return PendingResults(gather_to_root_async(buf, counts, group), layout)
+
+
+def gather_results(fields, counts, group=None):
+    """Synchronous gather_results_async."""
+    return gather_results_async(fields, counts, group).wait()

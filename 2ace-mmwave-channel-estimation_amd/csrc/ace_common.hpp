@@ -78,8 +78,6 @@ struct RealState {
     // m-space run (msr_kernel) that left this realisation's block ahead of the per-iteration launches:
     // the first iteration those must run for the block (its resume point)
     int32_t mres, mres_pad_[3];
-    // A2nuclear m-space iteration (ace_nucmsp.hip): Z = na X_init + A^H zeta, N = nbeta X_init +
-    // A^H nu; nx0 = ||X_init||^2; the X_init coefficients of the best / last iterate
     // A2nuclear m-space iteration (ace_nucmsp.hip): E_prev = na X_init + A^H e, Z = naz E_prev,
     // N = nbeta E_prev, nep2 = ||E_prev||^2, nx0 = ||X_init||^2; best / current iterate's X_init coefficient
     double na, nbeta, nx0, nopt_a, ncur_a, naz, nep2, npad2_;

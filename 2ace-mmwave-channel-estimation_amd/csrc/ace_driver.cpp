@@ -284,9 +284,10 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
                              H_amp + (size_t)i * n, H_angle + (size_t)i * n);
         if (rcs[i]) errs[i] = g_err;
     };
-    // ACE_DRIVER_SERIAL=1 runs the sweep points one after another on the calling thread (A/B)
+    // ACE_DRIVER_SERIAL=1 runs the sweep points one after another on the calling thread (A/B); so does a
+    // profiling session (ace_prof_start): the kernel timer's launch slots are not thread-safe
     const char* ser = getenv("ACE_DRIVER_SERIAL");
-    if (n_M == 1 || (ser && ser[0] == '1')) {
+    if (n_M == 1 || g_prof.on || (ser && ser[0] == '1')) {
         for (int i = 0; i < n_M; ++i) point(i);
     } else {
         std::vector<std::thread> th;

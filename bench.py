@@ -399,7 +399,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     import ace_amd
     from ace_amd import infer_admm_batch, synth_problem
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
-    from ace_amd.dist import gather_to_root_async
+    from ace_amd.dist import gather_results_async
     import ctypes as C
 
     wl = workload or {}
@@ -417,9 +417,11 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     ws = ace_amd.solver.Workspace()
     outs, pend, nstep = [None, None], [None, None], [0]
 
-    # The single result gather of recovered channels over RCCL/xGMI (north_star), asynchronous: the
-    # gather of step k overlaps the solve of step k + 1 (outputs double-buffered; a buffer is
-    # reused only after its gather has completed, and the timed region waits for the last one).
+    # The single result gather over RCCL/xGMI (north_star; SURVEY.md §8(e): X, iteration counts and
+    # status per realisation -- the unit solve has no quality -- packed into one byte row each, one
+    # collective), asynchronous: the gather of step k overlaps the solve of step k + 1 (outputs
+    # double-buffered; a buffer is reused only after its gather has completed, and the timed region
+    # waits for the last one).
     def step():
         i = nstep[0] & 1
         if pend[i] is not None:
@@ -428,7 +430,8 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         outs[i] = infer_admm_batch(A, B, X0, tx, tx, variant=variant, maxiter=args.iters, fixed_iters=True,
                                    use_rank_one=r1, out=outs[i], workspace=ws)
         if world > 1:
-            pend[i] = gather_to_root_async(outs[i].X, counts)
+            o = outs[i]
+            pend[i] = gather_results_async({"X": o.X, "iters": o.iters, "status": o.status, "mu": o.mu}, counts)
         nstep[0] += 1
 
     def drain():
@@ -609,7 +612,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             "m": m, "n": n, "iters": args.iters,
             "x0": wl.get("x0_note", "H + 0.5 CN noise (synthetic warm start; refine_input measures the "
                                     "reference's own refinement input)"),
-            "parallelism": f"dp{world} (realisation sharding, RCCL gather of X to rank 0)",
+            "parallelism": f"dp{world} (realisation sharding, one RCCL gather of X, iters, status, mu to rank 0)",
         },
         "roofline": roof,
         "roofline_gemm": roof_gemm,
@@ -697,6 +700,7 @@ def bench_pipeline(args, dev, rank, world):
     import ace_amd
     from ace_amd import infer_low_rank_pipeline_batch, synth_problem, draw_partitions
     from ace_amd._lib import LIB, KERNEL_CLASSES, check
+    from ace_amd.dist import gather_results_async
     tx, m, bsz = args.tx, args.m, args.batch
     restarts = 3 if args.variant == "A2only" else 1
     A, B, _, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
@@ -704,9 +708,14 @@ def bench_pipeline(args, dev, rank, world):
     ws = ace_amd.solver.Workspace()
     res = None
 
+    counts = [bsz] * world
+
     def step():
         nonlocal res
         res = infer_low_rank_pipeline_batch(A, B, tx, tx, tr, variant=args.variant, workspace=ws)
+        if world > 1:   # X, quality, stage iteration counts, status in one collective
+            gather_results_async({"X": res.X, "quality": res.quality, "stage_iters": res.stage_iters,
+                                  "status": res.status}, counts).wait()
 
     for _ in range(args.warmup):
         step()

@@ -163,7 +163,9 @@ typedef struct ace_pipeline_cfg {
 
 /* Reference defaults for `variant`: A2only -> 3 restarts, nuclear -> 1 restart. */
 void ace_pipeline_cfg_default(ace_pipeline_cfg* cfg, int variant);
-/* Workspace bytes for ace_pipeline_solve_batch (0 on invalid arguments). */
+/* Workspace bytes for ace_pipeline_solve_batch (0 on invalid arguments).  Not monotonic in batch: a batch
+ * of at most 16 realisations runs its restarts concurrently on one workspace copy each, so it can need
+ * more than a batch of 17 -- size the workspace for the batch actually passed. */
 size_t ace_pipeline_workspace_size(const ace_pipeline_cfg* cfg, int batch, int m, int n);
 /* Batched pipeline on device buffers (shared codebook A [m][n] c128, B [batch][m] f64).
  * Outputs: X [batch][n], Y [batch][m] (c128; Y's last m - m_t entries are 0 after a
@@ -233,7 +235,11 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
  * NaN -> 0 of :176). */
 #define ACE_DRIVER_A2ONLY 0     /* channel_recovery_ADMM_v2_simulation_A2only.m */
 #define ACE_DRIVER_A2NUCLEAR 1  /* channel_recovery_ADMM_v2_simulation_A2nuclear.m */
-#define ACE_DRIVER_MULTIRES 2   /* channel_recovery_ADMM_v2_simulation_multiresolution.m */
+#define ACE_DRIVER_MULTIRES 2   /* channel_recovery_ADMM_v2_simulation_multiresolution.m.  The reference defines the
+                                   tiers for 16 x 16 only (rows [1984, 3968, 3968], M <= 96 / <= 256 / else,
+                                   ..._multiresolution.m:110-112,137-144); at 32 x 32 the build uses its own analogue
+                                   (4x the rows: 7936/15872/15872, thresholds 384/1024) -- a builder-defined layout
+                                   whose parity with any reference codebook is unpinned */
 #define ACE_DRIVER_PHASELIFT 3  /* channel_recovery_ADMM_v2_simulation_phaselift.m (MyPhaseLift, rng(4096)) */
 int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
                        const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list,

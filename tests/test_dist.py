@@ -151,3 +151,65 @@ def test_async_gather_two_ranks_gloo():
     _, _, _, H = synth.problem(4242, 0, total, 16, 4, 4)
     np.testing.assert_array_equal(a, H)
     np.testing.assert_array_equal(b, 2 * H)
+
+
+def _payload_worker(rank, world, port, total, out_q):
+    """SURVEY.md §8(e)'s payload: X (c128), quality (f64), per-stage iteration counts (int32 [k]) and
+    status (int32) of every realisation, packed into one byte row each and gathered in one collective."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ace_amd import synth
+        from ace_amd.dist import gather_results_async
+        counts = [shard_range(total, world, r)[1] for r in range(world)]
+        first, count = shard_range(total, world, rank)
+        _, _, _, H = synth.problem(4242, first, count, 16, 4, 4)
+        idx = torch.arange(first, first + count)
+        fields = {"X": torch.from_numpy(H), "quality": idx.to(torch.float64) / 7.0,
+                  "iters": torch.stack([idx * 13 + k for k in range(13)], 1).to(torch.int32),
+                  "status": (idx * 37 % 129).to(torch.int32), "mu": None}
+        got = gather_results_async(fields, counts).wait()
+        if rank == 0:
+            out_q.put({k: v.numpy() for k, v in got.items()})
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,world", [(7, 2), (5, 3)])
+def test_result_payload_one_gather(total, world):
+    """Ragged shards (7 over 2 ranks, 5 over 3): X, quality, iteration counts and status arrive on rank 0
+    in realisation order, bit-identical, dtypes and shapes preserved."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_payload_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from ace_amd import synth
+    _, _, _, H = synth.problem(4242, 0, total, 16, 4, 4)
+    idx = np.arange(total)
+    np.testing.assert_array_equal(got["X"], H)
+    np.testing.assert_array_equal(got["quality"], idx / 7.0)
+    np.testing.assert_array_equal(got["iters"], np.stack([idx * 13 + k for k in range(13)], 1).astype(np.int32))
+    np.testing.assert_array_equal(got["status"], (idx * 37 % 129).astype(np.int32))
+    assert got["iters"].dtype == np.int32 and got["X"].dtype == np.complex128 and "mu" not in got
+
+
+def test_pack_roundtrip_single_process():
+    from ace_amd.dist import pack_results, unpack_results
+    X = torch.randn(3, 5, dtype=torch.complex128)
+    q = torch.randn(3, dtype=torch.float64)
+    it = torch.randint(0, 500, (3, 13), dtype=torch.int32)
+    st = torch.randint(0, 255, (3,), dtype=torch.int32)
+    buf, layout = pack_results({"X": X, "q": q, "it": it, "st": st})
+    assert buf.dtype == torch.uint8 and buf.shape == (3, 16 * 5 + 8 + 4 * 13 + 4) and buf.shape[1] % 8 == 0
+    out = unpack_results(buf, layout)
+    assert torch.equal(out["X"], X) and torch.equal(out["q"], q) and torch.equal(out["it"], it)
+    assert torch.equal(out["st"], st)

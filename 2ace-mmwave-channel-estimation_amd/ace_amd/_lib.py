@@ -120,6 +120,8 @@ def _load():
     lib.ace_prof_msp_steps.restype = C.c_int
     lib.ace_prof_work.argtypes = [dp]
     lib.ace_prof_work.restype = C.c_int
+    lib.ace_prof_work_ex.argtypes = [dp, dp, dp]
+    lib.ace_prof_work_ex.restype = C.c_int
     lib.ace_nuclear_prox_batch.argtypes = [C.c_int, C.c_int, C.c_int, vp, C.c_double, vp, vp]
     lib.ace_nuclear_prox_batch.restype = C.c_int
     lib.ace_spectral_init_host.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]

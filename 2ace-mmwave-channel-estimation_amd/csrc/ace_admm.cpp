@@ -798,8 +798,24 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     // algorithmic flops of the f64 GEMM-shaped applies as launched (all batch * r vectors; the
     // unit path's fused int8 kernels are accounted by the bench): ace_prof_work
     const double fl_mn = 8.0 * m * n * nv, fl_mm = 8.0 * m * m * nv;
+    // ... and their algorithmic HBM bytes (c128 = 16 B; every per-vector array read or written once, a
+    // shared operator once per launch) and int8 matrix-core ops (8 digit planes x the 2 x 2 real
+    // expansion; K carries two base-128 planes): ace_prof_work_ex, so that the r-column stages' int8
+    // applies, Y-step and Z-step get a roofline too
+    const double vb = 16.0 * nv;                           // bytes of one c128 entry over the launch's vectors
+    const double op_mn = 2.0 * 8 * (2.0 * m) * (2.0 * n) * nv, op_mm = 2.0 * 8 * 2 * (2.0 * m) * (2.0 * m) * nv;
+    const double shA = L.shared ? 16.0 * m * n : 16.0 * m * n * batch, shM = L.shared ? 16.0 * m * m : 16.0 * m * m * batch;
+    // r-column Z-step: E E^H over the r column blocks (tx x tx x rx r complex MACs) plus the 32 x 32 Hermitian
+    // eig (0.8 Mflop at tx = 32); A2nuclear: the r x r Gram E^H E and Z = E V diag V^H
+    // (3 n r^2 MACs).  Bytes: X, N, Z in; Z, N out; the warm-start eigenvectors in and out
+    const double zs_fl = !fast ? (p.variant == ACE_VARIANT_NUCLEAR
+                                      ? 8.0 * 3 * n * r * r * batch
+                                      : (8.0 * p.tx * p.tx * p.rx * r + 0.8e6 * std::pow(p.tx / 32.0, 3)) * batch)
+                               : 0.0;
+    const double zs_b = !fast ? (80.0 * n * r + 32.0 * p.tx * p.tx) * batch : 0.0;
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
+    double lv = 1.0;   // share of the batch still iterating (convergence mode: from the polls), for ace_prof_work
     for (int it = 1; it <= p.maxiter; ++it) {
         if (pc) {
             ProfScope ps(ACE_K_APPLY_G, st);
@@ -812,18 +828,18 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
-            ProfScope ps(ACE_K_APPLY_A, st, fl_mn);
+            ProfScope ps(ACE_K_APPLY_A, st, lv * (fl_mn));
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
         } else {
             {
-                ProfScope ps(ACE_K_PRE, st);
+                ProfScope ps(ACE_K_PRE, st, 0.0, lv * (vb * (3.0 * m + (i8r ? 0.0 : 3.0 * n))));
                 launch_pre(n * r, m * r, batch, w.Z, w.N, w.Y[q], w.M, i8r ? nullptr : w.V, w.S, w.st, st);
             }
             if (i8r) {   // T = (Y - M/mu) - A (Z - N/mu) per vector, digit planes
-                ProfScope ps(ACE_K_APPLY_A, st);
+                ProfScope ps(ACE_K_APPLY_A, st, 0.0, lv * (vb * (2.0 * n + 3.0 * m)), lv * (op_mn));
                 launch_i8_apply_A(nv, n, m, L.LA8, w.Z, w.N, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, nullptr, st, r);
             } else {
-                ProfScope ps(ACE_K_APPLY_A, st, fl_mn);
+                ProfScope ps(ACE_K_APPLY_A, st, lv * (fl_mn), lv * (vb * (n + 2.0 * m) + shA));
                 applyA(1, w.V, w.T, w.S);   // T = S - A V
             }
         }
@@ -836,25 +852,27 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                              DualCtl{za.tol_abs, za.tol_rel, za.rho, za.fixed_iters, n, 1, w.done}};
             launch_gyk(batch, m, ga, st);
         } else if (fused) {  // g = G T with the Y-step in its epilogue
-            ProfScope ps(ACE_K_APPLY_G, st, fl_mm);
+            ProfScope ps(ACE_K_APPLY_G, st, lv * (fl_mm));
             const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
             launch_zgemm_ystep(m, batch, L.G, w.T, w.g, ys, w.st, st);
         } else {
-            { ProfScope ps(ACE_K_APPLY_G, st, fl_mm); applyMM(L.G, w.T, w.g); }   // g = G T
+            { ProfScope ps(ACE_K_APPLY_G, st, lv * (fl_mm), lv * (vb * 2.0 * m + shM)); applyMM(L.G, w.T, w.g); }   // g = G T
             {
-                ProfScope ps(ACE_K_YSTEP, st);
+                ProfScope ps(ACE_K_YSTEP, st, 0.0, lv * (vb * 6.0 * m + 8.0 * m * batch));   // S, g, M, Y in; M, Y' out
                 if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
                 else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
             }
         }
         if (!gyk && !pc) {   // K Y
-            ProfScope ps(ACE_K_APPLY_K, st, (i8 || i8r) ? 0.0 : fl_mm);
+            ProfScope ps(ACE_K_APPLY_K, st, lv * ((i8 || i8r) ? 0.0 : fl_mm), lv * ((i8 && !i8r) ? 0.0 : vb * 2.0 * m + (i8r ? 0.0 : shM)), lv * (i8r ? op_mm : 0.0));
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
             else if (i8r) launch_i8_apply_K(nv, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st, r);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
         }
         if (!pc) {
-            ProfScope ps(ACE_K_APPLY_AH, st, (wmode || i8r) ? 0.0 : fl_mn);      // X = V + A^H g
+            // X = V + A^H g
+            ProfScope ps(ACE_K_APPLY_AH, st, lv * ((wmode || i8r) ? 0.0 : fl_mn),
+                         lv * (wmode ? 0.0 : i8r ? vb * (m + 3.0 * n) : vb * (m + 2.0 * n) + shA), lv * (i8r ? op_mn : 0.0));
             if (wmode) {
                 za.xfuse = gyk && wmode && p.variant != ACE_VARIANT_NUCLEAR && za.warm && za.Q && kn.lean &&
                            it != p.maxiter && fuse_ok(kn, m);
@@ -897,7 +915,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         za.fixup_now = it == p.maxiter;
         za.compact = za.lean && kn.zcompact > 0 && it > kn.zcompact;
         {
-            ProfScope ps(ACE_K_ZSTEP, st);
+            ProfScope ps(ACE_K_ZSTEP, st, lv * (zs_fl), lv * (zs_b));
             if (za.lean && !za.xfuse) launch_zlean(za, batch, st);
             launch_zstep(p.variant, false, za, batch, st);
         }
@@ -910,6 +928,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             int h_done = 0;
             ACE_HIP(read_back(&h_done, w.done, sizeof(int), st));
             if (h_done >= batch) break;
+            lv = (double)(batch - h_done) / batch;
         }
     }
     ACE_HIP(hipGetLastError());

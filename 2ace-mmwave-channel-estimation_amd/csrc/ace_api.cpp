@@ -51,6 +51,8 @@ int ace_prof_start(int max_launches) {
     for (auto& e : g_prof.ev) ACE_HIP(hipEventCreate(&e));
     g_prof.cls.assign(max_launches, 0);
     g_prof.work.assign(max_launches, 0.0);
+    g_prof.wbytes.assign(max_launches, 0.0);
+    g_prof.wops.assign(max_launches, 0.0);
     g_prof.used = 0;
     for (int& c : g_prof.seen) c = 0;
     if (!g_prof.msp_slots) {
@@ -76,6 +78,16 @@ int ace_prof_work(double* flops) {
     return ACE_OK;
 }
 
+int ace_prof_work_ex(double* flops, double* bytes, double* int8_ops) {
+    g_err.clear();
+    for (int c = 0; c < ACE_NKCLASS; ++c) {
+        if (flops) flops[c] = g_prof.work_tot[c];
+        if (bytes) bytes[c] = g_prof.bytes_tot[c];
+        if (int8_ops) int8_ops[c] = g_prof.ops_tot[c];
+    }
+    return ACE_OK;
+}
+
 int ace_path_counts(int64_t* counts, int reset) {
     g_err.clear();
     for (int k = 0; k < 4; ++k) {
@@ -91,7 +103,7 @@ int ace_prof_stop(double* total_ms, int32_t* launches) {
     for (int c = 0; c < ACE_NKCLASS; ++c) {
         if (total_ms) total_ms[c] = 0.0;
         if (launches) launches[c] = 0;
-        g_prof.work_tot[c] = 0.0;
+        g_prof.work_tot[c] = g_prof.bytes_tot[c] = g_prof.ops_tot[c] = 0.0;
     }
     for (size_t i = 0; i < g_prof.used; ++i) {
         ACE_HIP(hipEventSynchronize(g_prof.ev[2 * i + 1]));
@@ -99,6 +111,8 @@ int ace_prof_stop(double* total_ms, int32_t* launches) {
         ACE_HIP(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
         const int c = g_prof.cls[i];
         g_prof.work_tot[c] += g_prof.work[i];
+        g_prof.bytes_tot[c] += g_prof.wbytes[i];
+        g_prof.ops_tot[c] += g_prof.wops[i];
         if (total_ms) total_ms[c] += ms;
         if (launches) launches[c] += 1;
     }
@@ -106,6 +120,8 @@ int ace_prof_stop(double* total_ms, int32_t* launches) {
     g_prof.ev.clear();
     g_prof.cls.clear();
     g_prof.work.clear();
+    g_prof.wbytes.clear();
+    g_prof.wops.clear();
     g_prof.used = 0;
     ACE_HIP(hipDeviceSynchronize());   // (the m-space counters are copied after the last events)
     g_prof.msp_total = 0;

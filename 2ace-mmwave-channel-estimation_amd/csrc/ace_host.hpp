@@ -48,7 +48,11 @@ struct Prof {
     std::vector<hipEvent_t> ev;   // 2 per record
     std::vector<int> cls;
     std::vector<double> work;     // algorithmic flops of each recorded launch (ProfScope)
+    std::vector<double> wbytes;   // algorithmic HBM bytes of each recorded launch
+    std::vector<double> wops;     // int8 matrix-core ops of each recorded launch
     double work_tot[ACE_NKCLASS] = {};   // per class, over the recorded launches (ace_prof_work)
+    double bytes_tot[ACE_NKCLASS] = {};  // (ace_prof_work_ex)
+    double ops_tot[ACE_NKCLASS] = {};
     size_t used = 0;
     int stride = 1;               // record every stride-th launch of each class (ace_prof_sample) ...
     unsigned full = 0;            // ... except the classes in this mask, recorded on every launch
@@ -115,14 +119,17 @@ inline void poison_workspace(void* ws, size_t bytes, hipStream_t st) {
 struct ProfScope {  // brackets one launch (or a short sequence) of class `c` on stream `st`
     hipStream_t st;
     int idx = -1;
-    // work: the launch's algorithmic flops (8 per complex MAC), 0 where the caller accounts itself
-    ProfScope(int c, hipStream_t s, double work = 0.0) : st(s) {
+    // work: the launch's algorithmic flops (8 per complex MAC), bytes: its algorithmic HBM bytes (each
+    // array read or written once), ops: its int8 matrix-core ops; 0 where the caller accounts itself
+    ProfScope(int c, hipStream_t s, double work = 0.0, double bytes = 0.0, double ops = 0.0) : st(s) {
         const bool pick = ((g_prof.full >> c) & 1u) || (g_prof.seen[c] % g_prof.stride) == 0;
         if (g_prof.on) ++g_prof.seen[c];
         if (g_prof.on && pick && g_prof.used < g_prof.cls.size()) {
             idx = (int)g_prof.used++;
             g_prof.cls[idx] = c;
             g_prof.work[idx] = work;
+            g_prof.wbytes[idx] = bytes;
+            g_prof.wops[idx] = ops;
             (void)hipEventRecord(g_prof.ev[2 * idx], st);
         }
     }

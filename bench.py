@@ -230,16 +230,19 @@ def roofline_from(kernel, avg_s, res, bounds=None, note=None):
     return out
 
 
-def _pmc_traffic(kernel_prefix, tag):
+def _pmc_traffic(kernel_prefix, tag, batch=None):
     """HBM bytes per launch (PMC FETCH_SIZE, gfx950-corrected, + WRITE_SIZE) of the kernel whose name
     starts with `kernel_prefix`, from the newest committed profiles/r<R>_v<V>[_<tag>]_pmc_hbm.json
-    measured on the same workload (tag: unit | private | nuclear | config5; files without a tag are
-    unit-mode passes, *_private_* regime-P passes), or None.  Written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc passes."""
+    measured on the same workload (tag: unit | private | nuclear | config5 | pipeline | phaselift;
+    files without a tag are unit-mode passes), or None.  Written by tools/pmc_summary.py from separate
+    rocprofv3 --pmc passes, with the profiled run's realisations per GPU in "_meta" (every launch of
+    these workloads covers a fixed share of the batch: the split halves, the stage launches over
+    batch x r vectors), so the bytes are rescaled to the line's `batch` -- per realisation, like
+    the algorithmic bytes they are compared with.  Profiles without "_meta" are not used."""
     def parse_name(f):   # r<round>_v<version>[_<tag>]_pmc_hbm.json
         parts = f.name[: -len("_pmc_hbm.json")].split("_")
         try:
-            return (int(parts[0][1:]), int(parts[1][1:])), "_".join(parts[2:]) or "unit"
+            return (int(parts[0][1:]), int("".join(c for c in parts[1][1:] if c.isdigit()))), "_".join(parts[2:]) or "unit"
         except (IndexError, ValueError):
             return None, None
     files = []
@@ -252,9 +255,14 @@ def _pmc_traffic(kernel_prefix, tag):
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
+        meta = d.get("_meta")
+        if not meta or not meta.get("batch"):
+            continue
+        scale = (batch / meta["batch"]) if batch else 1.0
         for k, v in d.items():
-            if k.split(" grid=")[0].strip().startswith(kernel_prefix):
-                return round(v["hbm_bytes"]), f"profiles/{f.name}"
+            if k != "_meta" and k.split(" grid=")[0].strip().startswith(kernel_prefix):
+                return round(v["hbm_bytes"] * scale), f"profiles/{f.name}" + (
+                    f" (profiled at batch {meta['batch']}, x {scale:g})" if scale != 1.0 else "")
     return None
 
 
@@ -267,8 +275,9 @@ PMC_KERNEL = {  # kernel-class -> kernel name prefix in the PMC profiles, per wo
 PMC_KERNEL["nuclear"] = {"apply_G": "nms_kernel<false>"}   # the m-space iteration (ace_nucmsp.hip)
 PMC_KERNEL["config5"] = PMC_KERNEL["nuclear"]
 # pipeline / PhaseLift: the dominant class's largest kernel (one launch per class launch)
-PMC_KERNEL["pipeline"] = {"apply_AH": "zgemm3m_kernel<2, false", "apply_A": "zgemm3m_kernel<1, false",
-                          "apply_G": "zgemm3m_kernel<0, false", "zstep": "zstep_kernel<0, false, false>"}
+PMC_KERNEL["pipeline"] = {"apply_AH": "i8ah_kernel<false, false>", "apply_A": "i8a_kernel",
+                          "apply_K": "i8ah_kernel<true, false>", "apply_G": "zgemm3m_kernel<0, false",
+                          "zstep": "zstep_kernel", "ystep": "ystep_r_kernel", "pre": "pre_kernel"}
 PMC_KERNEL["phaselift"] = {"zstep": "hetrd_kernel"}
 
 
@@ -310,36 +319,46 @@ def _barrier(world):
 
 
 def _prof_read(nclass=11):
-    """(total ms, launches, algorithmic flops) per kernel class since ace_prof_start."""
+    """(total ms, launches, algorithmic flops, HBM bytes, int8 ops) per kernel class since ace_prof_start."""
     import ctypes as C
     from ace_amd._lib import LIB, check
-    kt, kn, kw = (C.c_double * nclass)(), (C.c_int32 * nclass)(), (C.c_double * nclass)()
+    kt, kn = (C.c_double * nclass)(), (C.c_int32 * nclass)()
+    kw, kb, ko = (C.c_double * nclass)(), (C.c_double * nclass)(), (C.c_double * nclass)()
     check(LIB.ace_prof_stop(kt, kn))
-    check(LIB.ace_prof_work(kw))
-    return list(kt), list(kn), list(kw)
+    check(LIB.ace_prof_work_ex(kw, kb, ko))
+    return list(kt), list(kn), list(kw), list(kb), list(ko)
 
 
-def work_roofline(kt, kn, kw, note, tag=None):
-    """Roofline of the dominant kernel class among those whose launches carry an algorithmic flop
-    count (ace_prof_work: the f64 GEMM-shaped applies and prox steps), plus every class's share
-    of the device time.  With `tag`, `traffic` is the PMC HBM bytes per launch of the class's
-    largest kernel (PMC_KERNEL[tag]) from a profile of the same workload."""
+def work_roofline(kt, kn, kw, kb, ko, note, tag=None, batch=None):
+    """Roofline of the dominant kernel class BY DEVICE TIME, from the algorithmic work its launches carry
+    (ace_prof_work_ex: f64 flops of the GEMM-shaped applies and prox steps, HBM bytes of every stage
+    kernel, int8 ops of the digit-plane applies), plus every class's share of the device time.  With
+    `tag`, `traffic` is the PMC HBM bytes per launch of the class's largest kernel (PMC_KERNEL[tag])
+    from a profile of the same workload, rescaled to `batch` realisations."""
     from ace_amd._lib import KERNEL_CLASSES
     tot = sum(kt)
     shares = {KERNEL_CLASSES[i]: round(kt[i] / tot, 4) for i in range(len(kt)) if kn[i]}
-    cand = [i for i in range(len(kt)) if kn[i] and kw[i] > 0]
+    cand = [i for i in range(len(kt)) if kn[i]]
     if not cand:
         return None, shares
     i = max(cand, key=lambda c: kt[c])
     avg_s = kt[i] / kn[i] * 1e-3
-    r = roofline_from(KERNEL_CLASSES[i], avg_s, {"f64": kw[i] / kn[i]}, note=note)
+    res = {k: v / kn[i] for k, v in (("f64", kw[i]), ("hbm", kb[i]), ("int8", ko[i])) if v > 0}
+    if not res:
+        return {"kernel": KERNEL_CLASSES[i], "bound": "latency", "launches": kn[i], "avg_ms": round(avg_s * 1e3, 4),
+                "device_time_share": shares[KERNEL_CLASSES[i]], "traffic": None,
+                "note": "the dominant class carries no algorithmic work count"}, shares
+    r = roofline_from(KERNEL_CLASSES[i], avg_s, res, note=note)
     r["launches"] = kn[i]
+    r["avg_ms"] = round(avg_s * 1e3, 4)
     r["device_time_share"] = shares[KERNEL_CLASSES[i]]
     pmc = PMC_KERNEL.get(tag, {}).get(KERNEL_CLASSES[i]) if tag else None
-    tr = _pmc_traffic(pmc, tag) if pmc else None
+    tr = _pmc_traffic(pmc, tag, batch) if pmc else None
     if tr:
         r["traffic"], r["traffic_source"] = tr
         r["traffic_kernel"] = pmc
+        if res.get("hbm"):
+            r["traffic_per_algorithmic"] = round(tr[0] / res["hbm"], 3)
     return r, shares
 
 
@@ -461,7 +480,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
     out = outs[(nstep[0] - 1) & 1]
     msp_steps = C.c_longlong(0)
     if prof:
-        kt, kn, kw = _prof_read()
+        kt, kn, kw, _, _ = _prof_read()
         check(LIB.ace_prof_msp_steps(C.byref(msp_steps)))
     elapsed = _max_over_ranks(elapsed, dev, world)
     it_ok = bool((out.iters == args.iters).all().item())
@@ -526,7 +545,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             roof_msr["realisations_per_launch"] = per_launch
             roof_msr["concurrent_launches"] = nsplit
             roof_msr["chip_frac"] = round(roof_msr["frac"] * nsplit, 4)
-            tr = _pmc_traffic("msr_kernel", tag)
+            tr = _pmc_traffic("msr_kernel", tag, bsz)
             if tr:
                 roof_msr["traffic"], roof_msr["traffic_source"] = tr
             dev_ms["msr"] = kernels["msr"]["total_ms"]
@@ -562,7 +581,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
             r["concurrent_launches"] = nsplit
             r["chip_frac"] = round(r["frac"] * nsplit, 4)
             pmc = PMC_KERNEL.get(tag, {}).get(k)
-            tr = _pmc_traffic(pmc, tag) if pmc else None
+            tr = _pmc_traffic(pmc, tag, bsz) if pmc else None
             if tr:
                 r["traffic"], r["traffic_source"] = tr
                 if res.get("hbm"):
@@ -732,9 +751,13 @@ def bench_pipeline(args, dev, rank, world):
     elapsed = time.perf_counter() - t0
     roof, shares, kt = None, None, None
     if not args.no_prof:
-        kt, kn, kw = _prof_read()
-        roof, shares = work_roofline(kt, kn, kw, "f64 flops of the GEMM-shaped applies as launched (all batch*r "
-                                     "vectors of the stage, 8 per complex MAC; ace_prof_work)", tag="pipeline")
+        kt, kn, kw, kb, ko = _prof_read()
+        roof, shares = work_roofline(kt, kn, kw, kb, ko, (
+            "algorithmic work of the dominant class by device time (ace_prof_work_ex), over the vectors of the stage "
+            "still iterating (batch*r scaled by the live share at the convergence polls): f64 flops (8 per complex "
+            "MAC), HBM bytes (every per-vector array read or written once), int8 ops of the digit-plane applies; "
+            "the r-column Z-step: E E^H (tx^2 rx r MACs) + the 32x32 eig (0.8 Mflop), X, N, Z in / Z, N out"),
+            tag="pipeline", batch=bsz)
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return
@@ -817,11 +840,11 @@ def bench_phaselift(args, dev, rank, world):
     elapsed = time.perf_counter() - t0
     roof, shares, kt = None, None, None
     if not args.no_prof:
-        kt, kn, kw = _prof_read()
+        kt, kn, kw, kb, ko = _prof_read()
         roof, shares = work_roofline(
-            kt, kn, kw, "algorithmic f64 flops per realisation in the backtracking step (8 per complex MAC) in "
+            kt, kn, kw, kb, ko, "algorithmic f64 flops per realisation in the backtracking step (8 per complex MAC) in "
             "the d = min(m, n) reduced coordinates: prox eig 17.3 d^3 (SURVEY.md §8d's count for a dense Hermitian "
-            "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2", tag="phaselift")
+            "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2", tag="phaselift", batch=bsz)
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
         return

@@ -326,6 +326,11 @@ int ace_prof_msp_steps(long long* steps);
  * f64 path (pipeline stages, PhaseLift) carry their count; classes the caller accounts for
  * itself (the unit path's fused kernels) report 0.  flops: [ACE_NKCLASS]. */
 int ace_prof_work(double* flops);
+/* The same per kernel class, with the launches' algorithmic HBM bytes (every array the step needs read
+ * or written once) and int8 matrix-core ops beside the flops; any pointer may be NULL.  Every class
+ * of the pipeline's r-column stages (the int8 digit-plane applies, the r-column Z-step, the Y-step,
+ * the pre-pass) carries its bytes, so the dominant class by device time has a roofline. */
+int ace_prof_work_ex(double* flops, double* bytes, double* int8_ops);
 
 /* InferADMM solves (unit solves and every pipeline stage) per apply path since the last reset,
  * process-wide: counts[0] shared phase-code codebook on the exact int8 digit-plane applies,

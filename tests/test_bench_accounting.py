@@ -89,14 +89,32 @@ def test_pmc_traffic_is_keyed_by_workload(tmp_path, monkeypatch):
     b = _bench()
     prof = tmp_path / "profiles"
     prof.mkdir()
-    (prof / "r02_v9_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 1.0}}))
-    (prof / "r03_v1_nuclear_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 2.0}}))
-    (prof / "r03_v2_config5_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 3.0}}))
+    meta = {"_meta": {"batch": 4096}}
+    (prof / "r02_v9_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 1.0}, **meta}))
+    (prof / "r03_v1_nuclear_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 2.0}, **meta}))
+    (prof / "r03_v2_config5_pmc_hbm.json").write_text(json.dumps({"gyk_kernel": {"hbm_bytes": 3.0}, **meta}))
     monkeypatch.setattr(b, "ROOT", tmp_path)
     assert b._pmc_traffic("gyk_kernel", "unit") == (1, "profiles/r02_v9_pmc_hbm.json")
     assert b._pmc_traffic("gyk_kernel", "nuclear") == (2, "profiles/r03_v1_nuclear_pmc_hbm.json")
     assert b._pmc_traffic("gyk_kernel", "config5") == (3, "profiles/r03_v2_config5_pmc_hbm.json")
     assert b._pmc_traffic("gyk_kernel", "private") is None
+
+
+def test_pmc_traffic_rescaled_to_the_lines_batch(tmp_path, monkeypatch):
+    """A PMC profile of another batch size is rescaled per realisation (config 5's
+    traffic was divided by four times the realisations the profile's launches carried); a profile
+    without its batch recorded is not used."""
+    import json
+    b = _bench()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r04_v1_config5_pmc_hbm.json").write_text(json.dumps({"nms_kernel<false>": {"hbm_bytes": 800.0},
+                                                                   "_meta": {"batch": 16384}}))
+    (prof / "r04_v2_pipeline_pmc_hbm.json").write_text(json.dumps({"zstep_kernel<0>": {"hbm_bytes": 8.0}}))
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    v, src = b._pmc_traffic("nms_kernel", "config5", 65536)
+    assert v == 3200 and "batch 16384" in src
+    assert b._pmc_traffic("zstep_kernel", "pipeline", 4096) is None
 
 
 def test_nms_bytes():
@@ -116,13 +134,33 @@ def test_work_roofline_attaches_class_kernel_traffic(tmp_path, monkeypatch):
     b = _bench()
     prof = tmp_path / "profiles"
     prof.mkdir()
-    (prof / "r03_v9_phaselift_pmc_hbm.json").write_text(json.dumps({"hetrd_kernel": {"hbm_bytes": 5.0}}))
+    (prof / "r03_v9_phaselift_pmc_hbm.json").write_text(json.dumps({"hetrd_kernel": {"hbm_bytes": 5.0},
+                                                                     "_meta": {"batch": 512}}))
     monkeypatch.setattr(b, "ROOT", tmp_path)
     kt = [0.0] * 10
     kn = [0] * 10
-    kw = [0.0] * 10
+    kw, kb, ko = [0.0] * 10, [0.0] * 10, [0.0] * 10
     kt[8], kn[8], kw[8] = 100.0, 10, 1e12        # zstep class: the prox eig
-    r, shares = b.work_roofline(kt, kn, kw, "note", tag="phaselift")
+    r, shares = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="phaselift", batch=512)
     assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "hetrd_kernel"
-    r, _ = b.work_roofline(kt, kn, kw, "note", tag="pipeline")
+    r, _ = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="pipeline", batch=512)
     assert r["traffic"] is None
+
+
+def test_work_roofline_dominant_by_device_time():
+    """The dominant class is the one with the most device time whatever work it carries (VERDICT r03:
+    the pipeline's r-column Z-step, 37 % of its device time, had no flop count and was never
+    picked); its bound is the resource with the largest time at peak among flops, bytes, int8 ops."""
+    b = _bench()
+    kt, kn = [0.0] * 10, [0] * 10
+    kw, kb, ko = [0.0] * 10, [0.0] * 10, [0.0] * 10
+    kt[4], kn[4], kw[4] = 10.0, 10, 1e12            # apply_G: f64 GEMM, little device time
+    kt[8], kn[8], kw[8], kb[8] = 37.0, 10, 1e11, 8e10   # zstep: HBM-bound by time at peak
+    kt[3], kn[3], kb[3], ko[3] = 20.0, 10, 1e10, 5e13   # apply_A: int8 ops
+    r, shares = b.work_roofline(kt, kn, kw, kb, ko, "note")
+    assert r["kernel"] == "zstep" and r["resource"] == "hbm" and r["bound"] == "hbm"
+    assert abs(r["frac"] - 8e9 / 3.7e-3 / 8e12) < 1e-4 and "f64" in r["other_resources"]
+    assert shares["zstep"] == round(37 / 67, 4)
+    kt[8], kb[8], kw[8] = 37.0, 0.0, 0.0            # no work count: reported, marked latency
+    r, _ = b.work_roofline(kt, kn, kw, kb, ko, "note")
+    assert r["kernel"] == "zstep" and r["bound"] == "latency"

@@ -46,6 +46,10 @@ LIB.ace_recover_driver.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER
                                    C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
                                    C.POINTER(C.c_int32), C.POINTER(C.c_double), C.POINTER(C.c_double)]
 LIB.ace_recover_driver.restype = C.c_int
+LIB.ace_recover_driver_ex.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.c_int,
+                                      C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+LIB.ace_recover_driver_ex.restype = C.c_int
 LIB.ace_driver_m_sweep.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int32)]
 LIB.ace_driver_m_sweep.restype = C.c_int
 LIB.ace_driver_randperm.argtypes = [C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int32)]
@@ -70,8 +74,9 @@ def randperm(seed, stream, P, k):
     return out
 
 
-def recover(driver, tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id, M_list=None):
-    """ace_recover_driver on numpy inputs; returns (H_amp, H_angle) of shape (n_M, 1, n)."""
+def recover(driver, tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id, M_list=None, maxiter=0):
+    """ace_recover_driver on numpy inputs; returns (H_amp, H_angle) of shape (n_M, 1, n).  ``maxiter`` > 0
+    caps every solve's iterations (ace_recover_driver_ex; parity runs on a stable horizon)."""
     tx, rx = int(tx_ant_num), int(rx_ant_num)
     amp = np.ascontiguousarray(np.asarray(cb_amp, dtype=np.float64))
     ang = np.ascontiguousarray(np.asarray(cb_angle, dtype=np.float64))
@@ -90,9 +95,9 @@ def recover(driver, tx_ant_num, rx_ant_num, cb_amp, cb_angle, rss_final, seed_id
     H_amp = np.zeros((nM, n), np.float64)
     H_ang = np.zeros((nM, n), np.float64)
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
-    rc = LIB.ace_recover_driver(int(driver), tx, rx, P, dp(amp), dp(ang), dp(rss), int(seed_id), int(nM),
-                                None if Ms is None else Ms.ctypes.data_as(C.POINTER(C.c_int32)),
-                                dp(H_amp), dp(H_ang))
+    rc = LIB.ace_recover_driver_ex(int(driver), tx, rx, P, dp(amp), dp(ang), dp(rss), int(seed_id), int(nM),
+                                   None if Ms is None else Ms.ctypes.data_as(C.POINTER(C.c_int32)), int(maxiter),
+                                   dp(H_amp), dp(H_ang))
     if rc < 0:
         msg = LIB.ace_last_error().decode()
         if rc == ACE_ERR_ARG and "unknown driver" not in msg:

@@ -122,12 +122,14 @@ struct DevBufs {
 
 // One sweep point i (M rows): rows, cb_train / rss_train, the solve, H row (:137-178).
 int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
-                const double* rss_dbm, uint64_t seed, int i, int M, int dev, double* H_amp, double* H_angle) {
+                const double* rss_dbm, uint64_t seed, int i, int M, int dev, int maxiter, double* H_amp,
+                double* H_angle) {
     g_err.clear();
     ACE_HIP(hipSetDevice(dev));
     const int n = tx * rx;
     ace_pipeline_cfg cfg;
     ace_pipeline_cfg_default(&cfg, driver == ACE_DRIVER_A2NUCLEAR ? ACE_VARIANT_NUCLEAR : ACE_VARIANT_A2ONLY);
+    if (maxiter > 0) cfg.maxiter = maxiter;
     // ---- :137 M_idx = randperm(length(rss_final), M) (multiresolution: within its tier)
     std::vector<int32_t> idx(M);
     int avail = P, off = 0;
@@ -167,6 +169,7 @@ int sweep_point(int driver, int tx, int rx, int P, const double* cb_amp, const d
         // ---- Recover_Channel.m:32-35: MyPhaseLift((meas/2e5).^2*1e10, beams)/sqrt(1e10)*2e5
         ace_phaselift_cfg pcfg;
         ace_phaselift_cfg_default(&pcfg);
+        if (maxiter > 0) pcfg.maxIts = maxiter;
         for (int r = 0; r < M; ++r) B[r] = (B[r] / 2e5) * (B[r] / 2e5) * 1e10;
         const size_t ws = ace_phaselift_workspace_size(&pcfg, 1, M, n);
         if (!ws) return fail(ACE_ERR_UNSUPPORTED, "phaselift: unsupported size M = %d, n = %d", M, n);
@@ -231,6 +234,13 @@ int ace_driver_randperm(uint64_t seed, uint64_t stream, int P, int k, int32_t* o
 int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
                        const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list, double* H_amp,
                        double* H_angle) {
+    return ace_recover_driver_ex(driver, tx, rx, P, cb_amp, cb_angle, rss_dbm, seed_id, n_M, M_list, 0, H_amp,
+                                 H_angle);
+}
+
+int ace_recover_driver_ex(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
+                          const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list, int maxiter,
+                          double* H_amp, double* H_angle) {
     g_err.clear();
     if (driver != ACE_DRIVER_A2ONLY && driver != ACE_DRIVER_A2NUCLEAR && driver != ACE_DRIVER_MULTIRES &&
         driver != ACE_DRIVER_PHASELIFT)
@@ -280,7 +290,7 @@ int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, 
     std::vector<int> rcs(n_M, ACE_OK);
     std::vector<std::string> errs(n_M);
     auto point = [&](int i) {
-        rcs[i] = sweep_point(driver, tx, rx, P, cb_amp, cb_angle, rss_dbm, seed, i, Ms[i], dev,
+        rcs[i] = sweep_point(driver, tx, rx, P, cb_amp, cb_angle, rss_dbm, seed, i, Ms[i], dev, maxiter,
                              H_amp + (size_t)i * n, H_angle + (size_t)i * n);
         if (rcs[i]) errs[i] = g_err;
     };

@@ -244,6 +244,13 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
 int ace_recover_driver(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
                        const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list,
                        double* H_amp, double* H_angle);
+/* The same with the iteration cap of every solve in the call: maxiter > 0 replaces the reference's 500 ADMM
+ * iterations per pipeline stage (inferLowRankV4_multi.m:13) or 4000 TFOCS iterations (MyPhaseLift.m:82);
+ * 0 keeps them.  For parity runs on the horizon where the reference algorithm is stable against its own
+ * rounding (the A2nuclear refinement). */
+int ace_recover_driver_ex(int driver, int tx, int rx, int P, const double* cb_amp, const double* cb_angle,
+                          const double* rss_dbm, int seed_id, int n_M, const int32_t* M_list, int maxiter,
+                          double* H_amp, double* H_angle);
 /* The reference M sweep for (tx, rx) into M_out[8]; returns 8 or a negative error code
  * (..._A2only.m:106-118, error :117). */
 int ace_driver_m_sweep(int tx, int rx, int32_t* M_out);

@@ -119,11 +119,48 @@ def test_driver_multiresolution_tiers(gpu):
         assert O.phase_aligned_rel_err(H[i], Xc) <= 1e-12
 
 
-def test_driver_nuclear_runs(gpu):
+NUCLEAR_SEEDS = [1024, 2048, 4096, 8192]   # ..._A2nuclear.m:103 (the build picks seeds((seed_id - 1) % 4 + 1))
+
+
+def _compose_nuclear(amp, ang, rss, tx, seed, points, maxiter=500):
+    """channel_recovery_ADMM_v2_simulation_A2nuclear's steps by hand (ADMM_v2_nuclear.m:30-32 ->
+    inferLowRank_Nuclear: one restart, one partition)."""
+    from ace_amd import engine, infer_low_rank_pipeline_host
+    out = []
+    for i, M in points:
+        idx = engine.randperm(seed, 0x100 + 2 * i, amp.shape[0], M)
+        A = _cb(amp, ang)[idx]
+        B = np.array([math.sqrt(math.pow(10.0, x / 10.0) / 1000.0) * RSS_FCT for x in rss[idx]])
+        tr = engine.randperm(seed, 0x101 + 2 * i, M, math.floor(0.95 * M))[None]
+        res = infer_low_rank_pipeline_host(A, B[None], tx, tx, tr, variant="A2nuclear", maxiter=maxiter)
+        out.append((res.X[0] / RSS_FCT, A, B, tr))
+    return out
+
+
+def test_driver_nuclear_matches_composition_and_oracle(gpu):
+    """channel_recovery_ADMM_v2_simulation_A2nuclear (:104 rows, :158 ADMM_v2_nuclear): equal to the hand
+    composition through the pipeline host API at the reference's 500 iterations (two sweep points, run
+    concurrently by the driver), and to the oracle's nuclear pipeline where the oracle is stable against
+    its own rounding: 25 iterations per stage (a 1e-15 relative change of B moves the oracle's X by
+    2e-11 at M = 121 and 3e-9 at M = 225 there, 7e-5 / 0.93 at 60: the nuclear refinement is
+    rounding-chaotic)."""
     from ace_amd import engine
-    amp, ang, rss = _trace(400, 16)
-    Ha, Hp = engine.recover(engine.DRIVER_A2NUCLEAR, 16, 16, amp, ang, rss, 3, M_list=[121])
-    assert Ha.shape == (1, 1, 256) and np.all(np.isfinite(Ha)) and np.all(np.isfinite(Hp))
+    tx = 16
+    amp, ang, rss = _trace(400, tx)
+    Ms = [121, 225]
+    seed = NUCLEAR_SEEDS[(3 - 1) % 4]
+    Ha, Hp = engine.recover(engine.DRIVER_A2NUCLEAR, tx, tx, amp, ang, rss, 3, M_list=Ms)
+    assert Ha.shape == (2, 1, 256) and np.all(np.isfinite(Ha)) and np.all(Ha.max(axis=-1) > 0)
+    H = np.squeeze(Ha * np.exp(1j * Hp))
+    for i, (Xc, _, _, _) in enumerate(_compose_nuclear(amp, ang, rss, tx, seed, list(enumerate(Ms)))):
+        assert O.phase_aligned_rel_err(H[i], Xc) <= 1e-12, i
+    Ha, Hp = engine.recover(engine.DRIVER_A2NUCLEAR, tx, tx, amp, ang, rss, 3, M_list=Ms, maxiter=25)
+    H = np.squeeze(Ha * np.exp(1j * Hp))
+    for i, (Xc, A, B, tr) in enumerate(_compose_nuclear(amp, ang, rss, tx, seed, list(enumerate(Ms)), maxiter=25)):
+        assert O.phase_aligned_rel_err(H[i], Xc) <= 1e-12, i
+        ref = O.infer_low_rank_pipeline(A, B, tx, tx, list(tr), variant=O.VARIANT_NUCLEAR, maxiter=25)
+        e = O.phase_aligned_rel_err(H[i], ref.X / RSS_FCT)
+        assert e <= 1e-6, (Ms[i], e)
 
 
 def test_driver_phaselift(gpu):

@@ -27,6 +27,9 @@ ACE_ST_EIG_NOCONV = 4
 ACE_ST_ROLLBACK = 8
 ACE_ST_RANK_ONE = 128
 
+ACE_TRAIN_SHARED = 0
+ACE_TRAIN_PER_REALISATION = 1
+
 KERNEL_CLASSES = ["setup", "init", "pre", "apply_A", "apply_G", "ystep", "apply_K", "apply_AH", "zstep", "final", "msr"]
 
 
@@ -66,7 +69,8 @@ class PipelineCfg(C.Structure):
         ("maxiter", C.c_int),
         ("eig_warm", C.c_int),
         ("stop_before_refine", C.c_int),
-        ("reserved", C.c_int * 2),
+        ("train_layout", C.c_int),
+        ("train_seed", C.c_int),
         ("mu0", C.c_double),
         ("rho", C.c_double),
         ("cc_frac", C.c_double),

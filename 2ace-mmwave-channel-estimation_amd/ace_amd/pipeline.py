@@ -7,19 +7,20 @@ Reference (main/src/my_recovery_algorithms/ADMM_v2/):
   inferLowRankV4 (Numerical_Simulation/src/my_recovery_algorithms/ADMM_v2/inferLowRankV4.m):
   the one-restart form of inferLowRankV4_multi.
 
-MATLAB's ``randsample(m, floor(m*cc_frac))`` (:48) is replaced by explicit train
-partitions: ``train_idx`` ([restarts][m_t] shared by a batch, or [batch][restarts][m_t])
-or, when omitted, a numpy Generator drawing a random permutation prefix per restart
-(the same distribution as randsample without replacement; MATLAB's stream itself is
-not reproducible outside MATLAB).
+MATLAB's ``randsample(m, floor(m*cc_frac))`` (:48), drawn inside every call, is replaced by
+explicit train partitions: ``train_idx`` [restarts][m_t] shared by a batch, or
+[batch][restarts][m_t] -- each realisation its own, as a Monte-Carlo batch of calls draws them
+(ACE_TRAIN_PER_REALISATION: one GPU batch, the stages on the full A in m-space) -- or, when
+omitted, random permutation prefixes (the same distribution as randsample without replacement;
+MATLAB's stream itself is not reproducible outside MATLAB).
 
 Entry points:
   * ``inferLowRankV4_multi`` / ``inferLowRankV4`` / ``inferLowRank_Nuclear`` -- one
     realisation, MATLAB argument order, numpy in / out ((n,1), (m,1), quality).
-  * ``infer_low_rank_pipeline_host`` -- a batch on host arrays; realisations whose
-    partitions coincide are solved in one GPU batch (ace_pipeline_solve_host).
-  * ``infer_low_rank_pipeline_batch`` -- device tensors already in HBM, one shared
-    partition set (ace_pipeline_solve_batch); the throughput path.
+  * ``infer_low_rank_pipeline_host`` -- a batch on host arrays, shared or per-realisation
+    partitions, one GPU batch (ace_pipeline_solve_host).
+  * ``infer_low_rank_pipeline_batch`` -- device tensors already in HBM, shared or
+    per-realisation partitions (ace_pipeline_solve_batch); the throughput path.
 There is no CPU fallback: every call goes through libace.so.
 """
 from __future__ import annotations
@@ -30,7 +31,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import LIB, check, pipeline_cfg, ACE_ST_ROLLBACK, ACE_ST_RANK_ONE
+from ._lib import (LIB, check, pipeline_cfg, ACE_ST_ROLLBACK, ACE_ST_RANK_ONE, ACE_TRAIN_SHARED,
+                   ACE_TRAIN_PER_REALISATION)
 from .solver import VARIANTS
 
 
@@ -62,10 +64,24 @@ def _cfg(variant, restarts, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig
     return pipeline_cfg(v, **kw)
 
 
-def draw_partitions(rng, m, restarts, cc_frac=0.95):
-    """randsample(m, floor(m*cc_frac)) per restart (inferLowRankV4_multi.m:48), 0-based."""
+def draw_partitions(rng, m, restarts, cc_frac=0.95, batch=None):
+    """randsample(m, floor(m*cc_frac)) per restart (inferLowRankV4_multi.m:48), 0-based:
+    [restarts][m_t], or [batch][restarts][m_t] (one draw per call) when ``batch`` is given."""
     mt = math.floor(m * cc_frac)
+    if batch is not None:
+        return np.stack([np.stack([rng.permutation(m)[:mt] for _ in range(restarts)])
+                         for _ in range(batch)]).astype(np.int32)
     return np.stack([rng.permutation(m)[:mt] for _ in range(restarts)]).astype(np.int32)
+
+
+def _layout(tr, batch):
+    """(contiguous int32 train_idx, ACE_TRAIN_*) of a [restarts][m_t] or [batch][restarts][m_t] array."""
+    tr = np.ascontiguousarray(np.asarray(tr, dtype=np.int32))
+    if tr.ndim == 2:
+        return tr, ACE_TRAIN_SHARED
+    if tr.ndim == 3 and tr.shape[0] == batch:
+        return tr, ACE_TRAIN_PER_REALISATION
+    raise ValueError(f"train_idx must be [restarts][m_t] or [batch][restarts][m_t], got {tr.shape}")
 
 
 def infer_low_rank_pipeline_host(A, B, tx, rx, train_idx, *, variant="A2only", restarts=None, r=20, mu0=1e-3,
@@ -81,40 +97,23 @@ def infer_low_rank_pipeline_host(A, B, tx, rx, train_idx, *, variant="A2only", r
     if A.ndim != 2 or A.shape[0] != m:
         raise ValueError(f"shape mismatch: A{A.shape} B{B.shape}")
     n = A.shape[1]
-    tr = np.asarray(train_idx, dtype=np.int32)
-    if tr.ndim == 2:
-        tr = np.broadcast_to(tr, (batch,) + tr.shape)
-    if tr.ndim != 3 or tr.shape[0] != batch:
-        raise ValueError(f"train_idx must be [restarts][m_t] or [batch][restarts][m_t], got {tr.shape}")
-    nres = tr.shape[1] if restarts is None else int(restarts)
+    tr, layout = _layout(train_idx, batch)
+    nres = tr.shape[-2] if restarts is None else int(restarts)
     cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
-    if tr.shape[1] != cfg.restarts:
-        raise ValueError(f"train_idx holds {tr.shape[1]} partitions, cfg.restarts = {cfg.restarts}")
+    if tr.shape[-2] != cfg.restarts:
+        raise ValueError(f"train_idx holds {tr.shape[-2]} partitions, cfg.restarts = {cfg.restarts}")
+    cfg.train_layout = layout
     ld = 4 * cfg.restarts + 1
     X = np.empty((batch, n), np.complex128)
     Y = np.empty((batch, m), np.complex128)
     q = np.empty(batch, np.float64)
     its = np.empty((batch, ld), np.int32)
     stt = np.empty(batch, np.uint32)
-    groups = {}
-    for b in range(batch):
-        groups.setdefault(tr[b].tobytes(), []).append(b)
-    for key, members in groups.items():
-        idx = np.asarray(members)
-        part = np.ascontiguousarray(tr[idx[0]])
-        Bg = np.ascontiguousarray(B[idx])
-        g = len(idx)
-        Xg = np.empty((g, n), np.complex128)
-        Yg = np.empty((g, m), np.complex128)
-        qg = np.empty(g, np.float64)
-        ig = np.empty((g, ld), np.int32)
-        sg = np.empty(g, np.uint32)
-        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
-        check(LIB.ace_pipeline_solve_host(
-            C.byref(cfg), g, m, n, tx, rx, dp(A.view(np.float64)), dp(Bg),
-            part.ctypes.data_as(C.POINTER(C.c_int32)), dp(Xg.view(np.float64)), dp(Yg.view(np.float64)),
-            dp(qg), ig.ctypes.data_as(C.POINTER(C.c_int32)), sg.ctypes.data_as(C.POINTER(C.c_uint32))))
-        X[idx], Y[idx], q[idx], its[idx], stt[idx] = Xg, Yg, qg, ig, sg
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    check(LIB.ace_pipeline_solve_host(
+        C.byref(cfg), batch, m, n, tx, rx, dp(A.view(np.float64)), dp(B),
+        tr.ctypes.data_as(C.POINTER(C.c_int32)), dp(X.view(np.float64)), dp(Y.view(np.float64)),
+        dp(q), its.ctypes.data_as(C.POINTER(C.c_int32)), stt.ctypes.data_as(C.POINTER(C.c_uint32))))
     return PipelineResult(X, Y, q, its, stt)
 
 
@@ -160,9 +159,9 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
                                   eig_warm=True, stop_before_refine=False, workspace=None,
                                   stream=None) -> PipelineResult:
     """Batched pipeline on device tensors: A [m][n] complex128 (shared codebook),
-    B [batch][m] float64, train_idx [restarts][m_t] (host, shared by the batch).
-    ``stop_before_refine`` returns X_max, the refinement's input (inferLowRankV4_multi.m:90-92),
-    instead of running the refinement stage."""
+    B [batch][m] float64, train_idx (host) [restarts][m_t] shared by the batch or
+    [batch][restarts][m_t] per realisation.  ``stop_before_refine`` returns X_max, the refinement's
+    input (inferLowRankV4_multi.m:90-92), instead of running the refinement stage."""
     import torch
     from .solver import _DEFAULT_WS
     if not (A.is_cuda and B.is_cuda):
@@ -174,10 +173,11 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
     A, B = A.contiguous(), B.contiguous()
     batch, m = B.shape
     n = A.shape[1]
-    tr = np.ascontiguousarray(np.asarray(train_idx, dtype=np.int32))
-    nres = tr.shape[0] if restarts is None else int(restarts)
+    tr, layout = _layout(train_idx, batch)
+    nres = tr.shape[-2] if restarts is None else int(restarts)
     cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
     cfg.stop_before_refine = int(bool(stop_before_refine))
+    cfg.train_layout = layout
     ld = 4 * cfg.restarts + 1
     dev = A.device
     out = PipelineResult(torch.empty((batch, n), dtype=torch.complex128, device=dev),

@@ -706,6 +706,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const int m = L.m, n = L.n, r = p.r;
     const Knobs kn = read_knobs();
     if (!L.shared && r != 1) return fail(ACE_ERR_UNSUPPORTED, "private sensing matrices support r = 1 only");
+    if (p.part && (r == 1 || !L.shared || p.part->m != m))
+        return fail(ACE_ERR_UNSUPPORTED, "per-realisation partitions run the r-column stages on a shared A");
     const int row_mode = (r == 1) ? 1 : p.row_mode;   // the two modes coincide at r = 1
     const int nv = batch * r;                         // vectors per apply
     const long long mm = (long long)m * m, mn = (long long)m * n;
@@ -760,6 +762,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.fixed_iters = p.fixed_iters;
     za.warm = p.eig_warm;
     za.zcert = kn.zcert ? 1 : 0;
+    za.mthr = p.part ? p.part->mt : 0;   // thresholds on the realisation's m_t train rows (:364-370)
     za.wmode = 0;
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)
@@ -780,7 +783,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
         ProfScope ps(ACE_K_INIT, st);
         if (pc) launch_pc_apply_a(batch, m, n, L.pcodes + pc_codesA_off(batch, m, n), L.pcb, X0, w.T, st);
         else applyA(0, X0, w.T, nullptr);                        // AX = A*X0
-        launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st);
+        launch_init_r(row_mode, n, m, r, batch, X0, w.T, B, w.X, w.Y[0], w.M, w.N, w.st, p.mu0, st, p.part);
         if (!nms) {
             za.it = 0;
             launch_zstep(p.variant, true, za, batch, st);           // Z = ArgMinZ(X, N=0, mu=1)
@@ -856,11 +859,15 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
             launch_zgemm_ystep(m, batch, L.G, w.T, w.g, ys, w.st, st);
         } else {
-            { ProfScope ps(ACE_K_APPLY_G, st, lv * (fl_mm), lv * (vb * 2.0 * m + shM)); applyMM(L.G, w.T, w.g); }   // g = G T
+            {   // g = G T; per-realisation partitions: then (I + K_t)^{-1} T_t by the Schur identity (launch_part_gfix)
+                ProfScope ps(ACE_K_APPLY_G, st, lv * (fl_mm), lv * (vb * 2.0 * m + shM) * (p.part ? 2.0 : 1.0));
+                applyMM(L.G, w.T, w.g);
+                if (p.part) launch_part_gfix(batch, r, *p.part, L.G, w.g, w.st, st);
+            }
             {
                 ProfScope ps(ACE_K_YSTEP, st, 0.0, lv * (vb * 6.0 * m + 8.0 * m * batch));   // S, g, M, Y in; M, Y' out
                 if (fast) launch_ystep(m, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
-                else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st);
+                else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st, p.part);
             }
         }
         if (!gyk && !pc) {   // K Y

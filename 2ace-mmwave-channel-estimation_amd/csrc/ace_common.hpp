@@ -452,6 +452,8 @@ struct ZArgs {
     int msp_fail_it;       // (tests: ACE_MSP_FAIL_IT) the bound of m-space iterates fails at this iteration
     int xzn;               // (apply_AH of the r-column stages) write X = (Z - N/mu) + A^H g instead of W
     int zcert;             // four-wave A2only Z-step: skip the eigensolver when the Ky Fan certificate holds
+    int mthr;              // rows of the convergence thresholds (:364-370) when they differ from the state's m:
+                           // per-realisation train partitions keep m-space state, the reference's A_t has m_t rows
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {
@@ -508,13 +510,39 @@ void launch_ystep(int m, int batch, const double* S, const double* g, double* M,
 // r-column stage kernels (ace_stage.hip).  State is [b][r][n] / [b][r][m].
 // init: InferADMM :296-310 given P0 = A X0 (row mode: one scale, normalize_rows by row
 // norms; column mode: per-column scale and entrywise normalisation).
+// Per-realisation train / test partitions of the r-column stages (MATLAB's randsample inside every
+// inferLowRankV4_multi call, :48-53).  The stage state stays in m-space: every shared-A product runs on
+// the full (normalised) A, the test rows of Y and M are held at zero, and g = (I + K_t)^{-1} T_t comes
+// from the full G = (I + K)^{-1} by the Schur identity (I + K_tt)^{-1} = G_tt - G_te G_ee^{-1} G_et
+// (launch_part_gfix); only the m_te x m_te block G_ee^{-1} is per realisation.
+struct PartRows {
+    const int* rows;             // [nb][m]: train rows in sampled order, then the test rows ascending
+    const unsigned char* mask;   // [nb][ldmask]: 1 on train rows
+    const double* geinv;         // [nb][mte][mte] c128: G_ee^{-1}
+    int m, mt, ldmask;
+};
+constexpr int PART_MAXTE = 96;   // test rows per realisation the LDS inverse takes (m <= 1920 at cc_frac 0.95)
 void launch_init_r(int row_mode, int n, int m, int r, int batch, const double* X0, const double* P0,
                    const double* B, double* X, double* Y, double* M, double* N, RealState* rs, double mu0,
-                   hipStream_t st);
+                   hipStream_t st, const PartRows* pr = nullptr);
 // ystep at r columns (ArgMinY :511-533 row / column mode, M update, reductions, and
 // in column mode the per-column objective with its first argmin, :352-361).
 void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, const double* g, double* M,
-                    const double* B, const double* Yold, double* Ynew, RealState* rs, hipStream_t st);
+                    const double* B, const double* Yold, double* Ynew, RealState* rs, hipStream_t st,
+                    const PartRows* pr = nullptr);
+// G_ee^{-1} per realisation from the full G (m x m, row-major c128); status |= ACE_ST_EIG_NOCONV on a
+// non-positive pivot (G_ee is a principal block of an HPD matrix: cannot happen in exact arithmetic)
+void launch_part_geinv(int nb, const PartRows& pr, const double* G, double* geinv, int* status, hipStream_t st);
+// g[b][j] (m-space, = G T~ on entry) <- (I + K_t)^{-1} T_t on the train rows, 0 on the test rows
+void launch_part_gfix(int nb, int r, const PartRows& pr, const double* G, double* g, const RealState* rs,
+                      hipStream_t st);
+// dst[b][j][rows[k]] = src[b][j][k] (k < mt), 0 on the test rows: compact (sampled order) -> m-space
+void launch_part_expand(int nb, int r, const PartRows& pr, const double* src, double* dst, hipStream_t st);
+// dst[b][j][k] = src[b][j][rows[k]], k < mt: m-space -> compact
+void launch_part_compact(int nb, int r, const PartRows& pr, const double* src, double* dst, hipStream_t st);
+// quality (:68) with A the full normalised A and B the full normalised B, on each realisation's test rows
+void launch_part_quality(int n, int nb, const PartRows& pr, const double* A, const double* X, const double* B,
+                         double* q, hipStream_t st);
 // opt_X / opt_Y (nc columns) or, if the objective never was finite, the current iterate.
 void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
                        const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters,

@@ -215,6 +215,9 @@ struct AdmmParams {
     int tx, rx;
     int use_rank_one;                  // batch-wide flag (ignored where rank_one is given)
     const unsigned char* rank_one;     // per-realisation use_rank_one (device, may be null)
+    // per-realisation train partitions (r > 1 stages only): L is the full A's operators, the state is in
+    // m-space with each realisation's test rows held at zero (PartRows, ace_common.hpp); null: none
+    const PartRows* part;
 };
 // Per-iteration state of a batch of `batch` realisations with r columns each.
 struct AdmmState {

@@ -34,6 +34,9 @@ void launch_finish(int n, int m, int mt, int batch, const double* qlast, const d
 // dst[(idx ? idx[k] : k) * ld + col] = src[k] (or_mask 0) or |= src[k] & or_mask, k < count
 void launch_put_col(int count, const int* src, const int* idx, int* dst, int ld, int col, unsigned or_mask,
                     hipStream_t st);
+// launch_move_rows for rows of `len` bytes (partition tables)
+void launch_move_bytes(int count, long long len, const void* src, void* dst, const int* idx, bool scatter,
+                       hipStream_t st);
 // dst[k] |= bit where flag[k] != 0, k < count
 void launch_flag_bits(int count, const unsigned char* flag, int* dst, unsigned bit, hipStream_t st);
 void launch_fill(long long count, double v, double* dst, hipStream_t st);
@@ -51,10 +54,11 @@ void launch_fill(long long count, double v, double* dst, hipStream_t st);
 // writes X = V(:, 1:r) diag(sqrt(max(0, s))) directly ([batch][r][n]).
 bool spectral_primal(int mt, int n);
 size_t spectral_scratch_bytes(int mt, int n, int batch, int r);
+// pr (per-realisation partitions): K, AH and Bt are the full m-row ones, the rows per realisation in pr
 int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
-                           double* scratch, double* X, int* status, hipStream_t st);
+                           double* scratch, double* X, int* status, hipStream_t st, const PartRows* pr = nullptr);
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
-                    int* status, hipStream_t st);
+                    int* status, hipStream_t st, const PartRows* pr = nullptr);
 
 // ---- batched Hermitian eigenpairs (ace_spectral.hip) for PhaseLift's prox_trace
 // (TFOCS/prox_trace.m:88-147) and MyPhaseLift's final eig (MyPhaseLift.m:106-107).

@@ -32,6 +32,8 @@ constexpr unsigned kStageBits = ACE_ST_NO_OPT | ACE_ST_EIG_NOCONV;
 
 struct PipeDims {
     int batch, m, n, tx, rx, r, mt, mte, restarts;
+    bool part;     // per-realisation partitions: m-space stage state on the full A (PartRows)
+    int ldmask;    // row stride of the train-row masks
 };
 
 // The pieces one restart (:42-77) works on.  Restarts are independent until the best of them is
@@ -43,11 +45,16 @@ struct RestartWs {
     LinOps Lt;
     double *W, *spec, *Xs, *Xs_s;
     double *X1, *Y1;                 // stage-1 output (r columns), reused by both stages' chains
-    double *X2, *Y2, *X2_s, *Y2_s;   // impl outputs (best column)
+    double *X2, *Y2, *X2_s, *Y2_s;   // impl outputs (best column); Y2 on the train rows in sampled order
     double *q, *q_s;
     int *iters, *stat, *idx_rows, *idx_sub, *status_dev;
     unsigned char* rank_one;
-    AdmmState sr;                    // r-column state (m_t rows)
+    AdmmState sr;                    // r-column state (m_t rows; m rows with per-realisation partitions)
+    // per-realisation partitions (PipeDims::part): the restart's PartRows tables, their retry-subset
+    // copies, the subset's B rows, the spectral W in m-space and the stages' m-space Y outputs
+    int *rows, *rows_s;
+    unsigned char *mask, *mask_s;
+    double *geinv, *geinv_s, *Bn_s, *Wm, *Y2m, *Y2m_s;
 };
 
 constexpr int kConcurrentBatch = 16;   // restarts run concurrently up to this batch size
@@ -72,19 +79,38 @@ struct PipeWs {
 
 void restart_carve(Carver& cv, const PipeDims& d, RestartWs* w) {
     const size_t cz = 16, B = (size_t)d.batch;
-    w->Bt = cv.take(8 * B * d.mt);
-    w->Bte = cv.take(8 * B * std::max(d.mte, 1));
-    w->Bt_s = cv.take(8 * B * d.mt);
-    w->Bte_s = cv.take(8 * B * std::max(d.mte, 1));
-    w->At = cv.take(cz * d.mt * d.n);
-    w->Ate = cv.take(cz * std::max(d.mte, 1) * d.n);
-    linops_carve(cv, true, d.batch, d.mt, d.n, &w->Lt);
+    const int md = d.part ? d.m : d.mt;   // rows of the stage state
+    *w = RestartWs{};
+    if (!d.part) {
+        w->Bt = cv.take(8 * B * d.mt);
+        w->Bte = cv.take(8 * B * std::max(d.mte, 1));
+        w->Bt_s = cv.take(8 * B * d.mt);
+        w->Bte_s = cv.take(8 * B * std::max(d.mte, 1));
+        w->At = cv.take(cz * d.mt * d.n);
+        w->Ate = cv.take(cz * std::max(d.mte, 1) * d.n);
+        linops_carve(cv, true, d.batch, d.mt, d.n, &w->Lt);
+        w->spec = cv.take(spectral_scratch_bytes(d.mt, d.n, d.batch, d.r));
+    } else {
+        const size_t te2 = (size_t)std::max(d.mte, 1) * std::max(d.mte, 1);
+        w->rows = cv.take<int>(4 * B * d.m);
+        w->rows_s = cv.take<int>(4 * B * d.m);
+        w->mask = cv.take<unsigned char>(B * d.ldmask);
+        w->mask_s = cv.take<unsigned char>(B * d.ldmask);
+        w->geinv = cv.take(cz * B * te2);
+        w->geinv_s = cv.take(cz * B * te2);
+        w->Bn_s = cv.take(8 * B * d.m);
+        w->Wm = cv.take(cz * B * d.r * d.m);
+        w->Y2m = cv.take(cz * B * d.m);
+        w->Y2m_s = cv.take(cz * B * d.m);
+        // the primal form reads the full A^H and B (m rows): size for both forms
+        w->spec = cv.take(std::max(spectral_scratch_bytes(d.mt, d.n, d.batch, d.r),
+                                   spectral_scratch_bytes(d.m, d.n, d.batch, d.r)));
+    }
     w->W = cv.take(cz * B * d.r * d.mt);
-    w->spec = cv.take(spectral_scratch_bytes(d.mt, d.n, d.batch, d.r));
     w->Xs = cv.take(cz * B * d.r * d.n);
     w->Xs_s = cv.take(cz * B * d.r * d.n);
     w->X1 = cv.take(cz * B * d.r * d.n);
-    w->Y1 = cv.take(cz * B * d.r * d.mt);
+    w->Y1 = cv.take(cz * B * d.r * md);
     w->X2 = cv.take(cz * B * d.n);
     w->Y2 = cv.take(cz * B * d.mt);
     w->X2_s = cv.take(cz * B * d.n);
@@ -97,7 +123,7 @@ void restart_carve(Carver& cv, const PipeDims& d, RestartWs* w) {
     w->idx_sub = cv.take<int>(4 * B);
     w->status_dev = cv.take<int>(4 * B);
     w->rank_one = cv.take<unsigned char>(B);
-    admm_state_carve(cv, d.batch, d.mt, d.n, d.r, &w->sr);
+    admm_state_carve(cv, d.batch, md, d.n, d.r, &w->sr);
 }
 
 void pipe_carve(Carver& cv, const PipeDims& d, PipeWs* w) {
@@ -142,7 +168,7 @@ int validate_dims(const ace_pipeline_cfg* c, int batch, int m, int n, PipeDims* 
     if (std::min(mt, n) > 1600)
         return fail(ACE_ERR_UNSUPPORTED, "min(train rows %d, n %d) > 1600 (spectral tridiagonalisation LDS limit)", mt, n);
     if (n > 4096) return fail(ACE_ERR_UNSUPPORTED, "n must be <= 4096 (got %d)", n);
-    *d = PipeDims{batch, m, n, 0, 0, r, mt, m - mt, c->restarts};
+    *d = PipeDims{batch, m, n, 0, 0, r, mt, m - mt, c->restarts, false, (m + 7) & ~7};
     return ACE_OK;
 }
 
@@ -159,18 +185,20 @@ int validate(const ace_pipeline_cfg* c, int batch, int m, int n, int tx, int rx,
 // inferLowRankImpl (:111-271) for `nb` realisations: Xs [nb][r][n], Bt [nb][mt] ->
 // X2 [nb][n], Y2 [nb][mt] (best column of the per-column stage); iteration counts of the
 // two stages into stage_dev columns col, col + 1 (rows idx[k] or k).
-int run_impl(const PipeDims& d, RestartWs& w, int* stage_dev, const AdmmParams& base, int nb, const double* Xs,
-             const double* Bt, double* X2, double* Y2, const int* idx, int col, hipStream_t st) {
+int run_impl(const PipeDims& d, RestartWs& w, const LinOps& L, const PartRows* pr, int* stage_dev,
+             const AdmmParams& base, int nb, const double* Xs, const double* Bt, double* X2, double* Y2, const int* idx,
+             int col, hipStream_t st) {
     const int ld = 4 * d.restarts + 1;
     AdmmParams p = base;
     p.r = d.r;
     p.row_mode = 1;                                               // :258 scale_by_row = true
-    ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, Xs, w.X1, w.Y1, w.iters, (uint32_t*)w.stat, nullptr, st));
+    p.part = pr;
+    ACE_TRY(admm_run(L, p, w.sr, nb, Bt, Xs, w.X1, w.Y1, w.iters, (uint32_t*)w.stat, nullptr, st));
     launch_put_col(nb, w.iters, idx, stage_dev, ld, col, 0, st);
     launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
     launch_gram_rotate(d.n, d.r, nb, w.X1, nullptr, st);         // :263-264
     p.row_mode = 0;                                               // :270 scale_by_row = false
-    ACE_TRY(admm_run(w.Lt, p, w.sr, nb, Bt, w.X1, X2, Y2, w.iters, (uint32_t*)w.stat, nullptr, st));
+    ACE_TRY(admm_run(L, p, w.sr, nb, Bt, w.X1, X2, Y2, w.iters, (uint32_t*)w.stat, nullptr, st));
     launch_put_col(nb, w.iters, idx, stage_dev, ld, col + 1, 0, st);
     launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
     ACE_HIP(hipGetLastError());
@@ -209,7 +237,7 @@ int run_restart(int i, const PipeDims& d, const double* A, const double* anorm, 
     AdmmParams p = base;
     p.use_rank_one = 0;
     p.rank_one = nullptr;
-    ACE_TRY(run_impl(d, w, stage_dev, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
+    ACE_TRY(run_impl(d, w, w.Lt, nullptr, stage_dev, p, batch, w.Xs, w.Bt, w.X2, w.Y2, nullptr, 4 * i, st));
     launch_quality(n, d.mte, batch, w.Ate, w.X2, w.Bte, w.q, st);
     // ---- :73-77 rank-one retry on the realisations with quality < 0.6
     std::vector<double> hq(batch);
@@ -228,13 +256,142 @@ int run_restart(int i, const PipeDims& d, const double* A, const double* anorm, 
         launch_move_rows(nf, d.mt, w.Bt, w.Bt_s, w.idx_sub, false, st);
         launch_move_rows(nf, std::max(d.mte, 1), w.Bte, w.Bte_s, w.idx_sub, false, st);
         p.use_rank_one = 1;
-        ACE_TRY(run_impl(d, w, stage_dev, p, nf, w.Xs_s, w.Bt_s, w.X2_s, w.Y2_s, w.idx_sub, 4 * i + 2, st));
+        ACE_TRY(run_impl(d, w, w.Lt, nullptr, stage_dev, p, nf, w.Xs_s, w.Bt_s, w.X2_s, w.Y2_s, w.idx_sub, 4 * i + 2, st));
         launch_quality(n, d.mte, nf, w.Ate, w.X2_s, w.Bte_s, w.q_s, st);
         launch_move_rows(nf, 2LL * n, w.X2_s, w.X2, w.idx_sub, true, st);
         launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
         launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
     }
     ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+// One restart with per-realisation partitions (PipeDims::part): the same steps on the full normalised A
+// (Lf: K, G = (I + K)^{-1}, A^H and its int8 images, built once for the call), each realisation's rows
+// in PartRows.  prow [batch][m] (train rows in sampled order, then the test rows ascending) and pmask
+// [batch][ldmask] are the host tables of this restart.
+int run_restart_part(int i, const PipeDims& d, const LinOps& Lf, const double* An, const double* Bn,
+                     const std::vector<int>& prow, const std::vector<unsigned char>& pmask, const AdmmParams& base,
+                     RestartWs& w, int* stage_dev, hipStream_t st) {
+    const int batch = d.batch, n = d.n, m = d.m;
+    ACE_HIP(hipMemsetAsync(w.status_dev, 0, 4 * (size_t)batch, st));
+    ACE_HIP(upload(w.rows, prow.data(), 4 * (size_t)batch * m, st));
+    ACE_HIP(upload(w.mask, pmask.data(), (size_t)batch * d.ldmask, st));
+    const PartRows pr{w.rows, w.mask, w.geinv, m, d.mt, d.ldmask};
+    launch_part_geinv(batch, pr, Lf.G, w.geinv, w.status_dev, st);   // (I + K_t)^{-1} via G_ee^{-1}
+    // ---- :58 SpectralInitialize on each realisation's train rows
+    {
+        ProfScope ps(ACE_K_SETUP, st);
+        if (spectral_primal(d.mt, n)) {
+            if (launch_spectral_primal(d.mt, n, d.r, batch, Lf.K, Lf.AH, Bn, w.spec, w.Xs, w.status_dev, st, &pr))
+                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: n = %d too large", n);
+        } else {
+            if (launch_spectral(d.mt, d.r, batch, Lf.K, Bn, w.spec, w.W, w.status_dev, st, &pr))
+                return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m_t = %d too large", d.mt);
+            launch_part_expand(batch, d.r, pr, w.W, w.Wm, st);      // X = A_t^H W = A^H W~
+            launch_zgemm(0, false, n, m, batch * d.r, Lf.AH, m, 0, w.Wm, m, 0, w.Xs, nullptr, n, 0, 1, st);
+        }
+    }
+    ACE_HIP(hipGetLastError());
+    // ---- :65-68 impl (use_rank_one = false) and test quality
+    AdmmParams p = base;
+    p.use_rank_one = 0;
+    p.rank_one = nullptr;
+    ACE_TRY(run_impl(d, w, Lf, &pr, stage_dev, p, batch, w.Xs, Bn, w.X2, w.Y2m, nullptr, 4 * i, st));
+    launch_part_compact(batch, 1, pr, w.Y2m, w.Y2, st);
+    launch_part_quality(n, batch, pr, An, w.X2, Bn, w.q, st);
+    // ---- :73-77 rank-one retry on the realisations with quality < 0.6
+    std::vector<double> hq(batch);
+    std::vector<unsigned char> ro(batch);
+    std::vector<int> fails;
+    ACE_HIP(read_back(hq.data(), w.q, 8 * (size_t)batch, st));
+    for (int b = 0; b < batch; ++b) {
+        ro[b] = hq[b] < 0.6;
+        if (ro[b]) fails.push_back(b);
+    }
+    ACE_HIP(upload(w.rank_one, ro.data(), batch, st));
+    const int nf = (int)fails.size();
+    if (nf > 0) {
+        const long long te2 = (long long)std::max(d.mte, 1) * std::max(d.mte, 1);
+        ACE_HIP(upload(w.idx_sub, fails.data(), 4 * (size_t)nf, st));
+        launch_move_rows(nf, 2LL * d.r * n, w.Xs, w.Xs_s, w.idx_sub, false, st);
+        launch_move_rows(nf, m, Bn, w.Bn_s, w.idx_sub, false, st);
+        launch_move_rows(nf, 2 * te2, w.geinv, w.geinv_s, w.idx_sub, false, st);
+        launch_move_bytes(nf, 4LL * m, w.rows, w.rows_s, w.idx_sub, false, st);
+        launch_move_bytes(nf, d.ldmask, w.mask, w.mask_s, w.idx_sub, false, st);
+        const PartRows prs{w.rows_s, w.mask_s, w.geinv_s, m, d.mt, d.ldmask};
+        p.use_rank_one = 1;
+        ACE_TRY(run_impl(d, w, Lf, &prs, stage_dev, p, nf, w.Xs_s, w.Bn_s, w.X2_s, w.Y2m_s, w.idx_sub, 4 * i + 2, st));
+        launch_part_compact(nf, 1, prs, w.Y2m_s, w.Y2_s, st);
+        launch_part_quality(n, nf, prs, An, w.X2_s, w.Bn_s, w.q_s, st);
+        launch_move_rows(nf, 2LL * n, w.X2_s, w.X2, w.idx_sub, true, st);
+        launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
+        launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
+    }
+    ACE_HIP(hipGetLastError());
+    return ACE_OK;
+}
+
+// The restarts' partitions from the caller's train_idx (or the build's RNG) in the layout the solve
+// runs: shared [restarts][m_t] rows + test complements, or per-realisation PartRows tables.
+struct Partitions {
+    bool part = false;
+    std::vector<std::vector<int>> rows;               // shared: [restarts] -> train then test rows
+    std::vector<std::vector<int>> prow;               // part: [restarts] -> [batch][m]
+    std::vector<std::vector<unsigned char>> pmask;    // part: [restarts] -> [batch][ldmask]
+};
+
+int check_partition(const int32_t* tr, int m, int mt, std::vector<int>& out, std::vector<char>& seen, int b, int i) {
+    std::fill(seen.begin(), seen.end(), 0);
+    out.clear();
+    for (int k = 0; k < mt; ++k) {
+        const int v = tr[k];
+        if (v < 0 || v >= m || seen[v])
+            return fail(ACE_ERR_ARG, "train_idx[%d][%d][%d] = %d: out of range or repeated", b, i, k, v);
+        seen[v] = 1;
+        out.push_back(v);
+    }
+    for (int v = 0; v < m; ++v)
+        if (!seen[v]) out.push_back(v);
+    return ACE_OK;
+}
+
+int build_partitions(const ace_pipeline_cfg* cfg, const PipeDims& d0, const int32_t* train_idx, Partitions* P) {
+    const int B = d0.batch, R = d0.restarts, m = d0.m, mt = d0.mt;
+    const bool each = train_idx == nullptr || cfg->train_layout == ACE_TRAIN_PER_REALISATION;
+    std::vector<int32_t> drawn;
+    if (!train_idx) {   // randsample per call (:48) from the build's counter RNG
+        drawn.resize((size_t)B * R * mt);
+        for (int b = 0; b < B; ++b)
+            for (int i = 0; i < R; ++i)
+                (void)ace_driver_randperm((uint64_t)(uint32_t)cfg->train_seed, (uint64_t)b * R + i, m, mt,
+                                          drawn.data() + ((size_t)b * R + i) * mt);
+        train_idx = drawn.data();
+    }
+    bool same = true;   // per-realisation partitions that coincide everywhere take the shared path
+    if (each)
+        for (int b = 1; b < B && same; ++b)
+            same = std::equal(train_idx, train_idx + (size_t)R * mt, train_idx + (size_t)b * R * mt);
+    P->part = each && !same;
+    std::vector<char> seen(m);
+    std::vector<int> rw;
+    if (!P->part) {
+        P->rows.assign(R, {});
+        for (int i = 0; i < R; ++i) ACE_TRY(check_partition(train_idx + (size_t)i * mt, m, mt, P->rows[i], seen, 0, i));
+        return ACE_OK;
+    }
+    if (m - mt > PART_MAXTE)
+        return fail(ACE_ERR_UNSUPPORTED, "per-realisation partitions need m - m_t <= %d test rows (got %d)", PART_MAXTE,
+                    m - mt);
+    const int ldm = d0.ldmask;
+    P->prow.assign(R, std::vector<int>((size_t)B * m));
+    P->pmask.assign(R, std::vector<unsigned char>((size_t)B * ldm, 0));
+    for (int b = 0; b < B; ++b)
+        for (int i = 0; i < R; ++i) {
+            ACE_TRY(check_partition(train_idx + ((size_t)b * R + i) * mt, m, mt, rw, seen, b, i));
+            std::copy(rw.begin(), rw.end(), P->prow[i].begin() + (size_t)b * m);
+            for (int k = 0; k < mt; ++k) P->pmask[i][(size_t)b * ldm + rw[k]] = 1;
+        }
     return ACE_OK;
 }
 
@@ -321,7 +478,14 @@ size_t ace_pipeline_workspace_size(const ace_pipeline_cfg* cfg, int batch, int m
     Carver cv{nullptr};
     PipeWs w;
     pipe_carve(cv, d, &w);
-    return cv.off + 256;
+    size_t need = cv.off + 256;
+    if (cfg->train_layout == ACE_TRAIN_PER_REALISATION) {   // either form, as the partitions decide
+        Carver cp{nullptr};
+        d.part = true;
+        pipe_carve(cp, d, &w);
+        need = std::max(need, cp.off + 256);
+    }
+    return need;
 }
 
 int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
@@ -331,21 +495,13 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     g_err.clear();
     PipeDims d;
     ACE_TRY(validate(cfg, batch, m, n, tx, rx, &d));
-    if (!A || !B || !train_idx || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
+    if (!A || !B || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
+    if (cfg->train_layout != ACE_TRAIN_SHARED && cfg->train_layout != ACE_TRAIN_PER_REALISATION)
+        return fail(ACE_ERR_ARG, "unknown train_layout %d", cfg->train_layout);
     // partitions (host): train rows in sampled order, test rows = sorted complement (:48-49)
-    std::vector<std::vector<int>> tr(d.restarts), te(d.restarts);
-    for (int i = 0; i < d.restarts; ++i) {
-        std::vector<char> seen(m, 0);
-        for (int k = 0; k < d.mt; ++k) {
-            const int v = train_idx[(size_t)i * d.mt + k];
-            if (v < 0 || v >= m || seen[v])
-                return fail(ACE_ERR_ARG, "train_idx[%d][%d] = %d: out of range or repeated", i, k, v);
-            seen[v] = 1;
-            tr[i].push_back(v);
-        }
-        for (int v = 0; v < m; ++v)
-            if (!seen[v]) te[i].push_back(v);
-    }
+    Partitions P;
+    ACE_TRY(build_partitions(cfg, d, train_idx, &P));
+    d.part = P.part;
     hipStream_t st = (hipStream_t)stream;
     Carver sz{nullptr};
     PipeWs w;
@@ -379,11 +535,15 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     launch_fill(batch, -1.0, w.qmax, st);                                 // max_quality = -1 (:40)
     ACE_HIP(hipMemsetAsync(w.stage_dev, 0, 4 * (size_t)batch * ld, st));
     ACE_HIP(hipMemsetAsync(w.status_dev, 0, 4 * (size_t)batch, st));
-    std::vector<std::vector<int>> rows(d.restarts);
-    for (int i = 0; i < d.restarts; ++i) {
-        rows[i] = tr[i];
-        rows[i].insert(rows[i].end(), te[i].begin(), te[i].end());
+    const std::vector<std::vector<int>>& rows = P.rows;
+    if (d.part) {   // the full A's operators serve every restart's stages and the refinement
+        w.Lf.A = w.An;
+        ACE_TRY(linops_setup(w.Lf, batch, st));
     }
+    auto restart = [&](int i, RestartWs& rw, hipStream_t s) -> int {
+        return d.part ? run_restart_part(i, d, w.Lf, w.An, w.Bn, P.prow[i], P.pmask[i], base, rw, w.stage_dev, s)
+                      : run_restart(i, d, A, w.anorm, w.Bn, rows[i], base, rw, w.stage_dev, s);
+    };
     // ---- :79-83 best of restarts (A2only; the nuclear pipeline keeps the last X), in restart order
     auto take_restart = [&](int i, RestartWs& rw) -> int {
         if (cfg->variant == ACE_VARIANT_A2ONLY) {
@@ -400,7 +560,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     };
     if (w.nrw == 1 || g_prof.on) {   // one after another (the kernel timer is not thread-safe)
         for (int i = 0; i < d.restarts; ++i) {
-            ACE_TRY(run_restart(i, d, A, w.anorm, w.Bn, rows[i], base, w.rw[0], w.stage_dev, st));
+            ACE_TRY(restart(i, w.rw[0], st));
             ACE_TRY(take_restart(i, w.rw[0]));
         }
     } else {                         // concurrently, one host thread and stream each
@@ -434,7 +594,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
             th.emplace_back([&, i]() {
                 hipError_t ei = hipSetDevice(dev);
                 if (ei == hipSuccess) ei = hipStreamWaitEvent(ss[i], ev0, 0);
-                rc[i] = ei == hipSuccess ? run_restart(i, d, A, w.anorm, w.Bn, rows[i], base, w.rw[i], w.stage_dev, ss[i])
+                rc[i] = ei == hipSuccess ? restart(i, w.rw[i], ss[i])
                                          : fail(ACE_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(ei));
                 if (rc[i] == ACE_OK && (ei = hipEventRecord(done[i], ss[i])) != hipSuccess)
                     rc[i] = fail(ACE_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(ei));
@@ -476,8 +636,10 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         return ACE_OK;
     }
     // ---- :89-101 refinement on the full A, r = 1, the last restart's use_rank_one
-    w.Lf.A = w.An;
-    ACE_TRY(linops_setup(w.Lf, batch, st));
+    if (!d.part) {
+        w.Lf.A = w.An;
+        ACE_TRY(linops_setup(w.Lf, batch, st));
+    }
     AdmmParams p = base;
     p.r = 1;
     p.row_mode = 1;

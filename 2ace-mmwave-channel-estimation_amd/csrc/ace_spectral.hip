@@ -73,8 +73,10 @@ constexpr int HT_RB = HT_THREADS / HT_COLS;  // row quarters
 // the next reflector comes from, takes the pending update on the fly; column k + 1 is never read
 // again.  Every element gets the same update expression and every product the same summation
 // order as in the two-sweep form.
+// rows (PartRows, per-realisation partitions): realisation b's train rows rows[b][0..mt) of the full
+// m x m K (leading dimension ldk = m) and of its full B row (ldb = m); null: K is K_t itself (ldk = ldb = mt)
 __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
-                                                           SpecLayout lay, const int* active) {
+                                                           SpecLayout lay, const int* active, const int* rows, int ldk) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
     extern __shared__ double smem[];
@@ -93,10 +95,13 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
     const int col = t % HT_COLS, rb = t / HT_COLS;
 
     if (Kp) {
+        const int* rw = rows ? rows + (long long)b * ldk : nullptr;
+        const int ld = rows ? ldk : mt;
+        auto ri = [&](int i) { return rw ? rw[i] : i; };
         // D = diag(B_i / ||a_i||), ||a_i||^2 = K_ii  (SpectralInitialize :563-567; zero rows stay zero)
         for (int i = t; i < mt; i += HT_THREADS) {
-            const double kii = K[(long long)i * mt + i].x;
-            const double d = kii > 0.0 ? Bt[(long long)b * mt + i] / sqrt(kii) : 0.0;
+            const double kii = K[(long long)ri(i) * ld + ri(i)].x;
+            const double d = kii > 0.0 ? Bt[(long long)b * ld + ri(i)] / sqrt(kii) : 0.0;
             dvs[i] = d;
             base[lay.dv + i] = d;
         }
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
         // C = D (K + K^H)/2 D, exactly Hermitian (real diagonal)
         for (long long e = t; e < (long long)mt * mt; e += HT_THREADS) {
             const int i = (int)(e / mt), j = (int)(e % mt);
-            const d2 kij = K[e], kji = K[(long long)j * mt + i];
+            const d2 kij = K[(long long)ri(i) * ld + ri(j)], kji = K[(long long)ri(j) * ld + ri(i)];
             const double s = dvs[i] * dvs[j];
             C[e] = i == j ? make_double2(s * kij.x, 0.0)
                           : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
@@ -580,14 +585,17 @@ namespace {
 // ---- primal form for m_t > n: the n x n Gram As^H As itself (a smaller eigenproblem)
 // Ast[b][i][k] = w_b[k] A_t^H[i][k], w_b[k] = B_t[b][k]^2 / ||a_k||^2 (0 for a zero row), so that
 // one batched GEMM C_b = conj(Ast_b) applied to the rows of A_t^H gives As^H As row by row.
+// mask (PartRows): mt is then the full m, A_t^H the full A^H and B_t the full B row; the weight of a test
+// row is zero, so the GEMM below sums the realisation's own train rows (in ascending row order)
 __global__ __launch_bounds__(256) void spec_weight_kernel(int mt, int n, int nb, const double* Kp, const double* AHp,
-                                                          const double* Bt, double* Astp) {
+                                                          const double* Bt, double* Astp, const unsigned char* mask,
+                                                          int ldmask) {
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x, per = (long long)n * mt;
     if (e >= per * nb) return;
     const int b = (int)(e / per), k = (int)(e % mt);
     const double kkk = reinterpret_cast<const d2*>(Kp)[(long long)k * mt + k].x;
     const double bk = Bt[(long long)b * mt + k];
-    const double wk = kkk > 0.0 ? bk * bk / kkk : 0.0;
+    const double wk = (kkk > 0.0 && !(mask && !mask[(long long)b * ldmask + k])) ? bk * bk / kkk : 0.0;
     const d2 a = reinterpret_cast<const d2*>(AHp)[e % per];
     reinterpret_cast<d2*>(Astp)[e] = make_double2(wk * a.x, wk * a.y);
 }
@@ -634,7 +642,8 @@ size_t spectral_scratch_bytes(int mt, int n, int batch, int r) {
 }
 
 int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
-                           double* scratch, double* X, int* status, hipStream_t st) {
+                           double* scratch, double* X, int* status, hipStream_t st, const PartRows* pr) {
+    if (pr) mt = pr->m;   // the full A^H, B and K; test rows weighted zero
     const SpecLayout lay(n, r);
     const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 16;
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
@@ -644,13 +653,14 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
         const int nb = batch - b0 < chunk ? batch - b0 : chunk;
         const long long elems = (long long)nb * n * mt;
         hipLaunchKernelGGL(spec_weight_kernel, dim3((unsigned)((elems + 255) / 256)), dim3(256), 0, st, mt, n, nb, K, AH,
-                           Bt + (long long)b0 * mt, Ast);
+                           Bt + (long long)b0 * mt, Ast, pr ? pr->mask + (long long)b0 * pr->ldmask : nullptr,
+                           pr ? pr->ldmask : 0);
         // C_b[v][i] = sum_k w_k A_t[k][i] conj(A_t[k][v]) = (As^H As)[v][i]
         launch_zgemm(0, true, n, mt, n, Ast, mt, (long long)n * mt, AH, mt, 0, scratch + lay.C, nullptr, n,
                      lay.stride / 2, nb, st);
         hipLaunchKernelGGL(spec_herm_kernel, dim3((n + 15) / 16, nb, (n + 15) / 16), dim3(256), 0, st, n, scratch, lay);
         hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
-                           nullptr);
+                           nullptr, nullptr, 0);
         hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, n, nullptr, scratch, lay, status, b0, nullptr);
         const int cv = backxf_chunk(n);
         double* Xb = X + 2LL * b0 * r * n;
@@ -662,14 +672,15 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
 }
 
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
-                    int* status, hipStream_t st) {
+                    int* status, hipStream_t st, const PartRows* pr) {
     const SpecLayout lay(mt, r);
     const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 16;
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
+    const int ldb = pr ? pr->m : mt;   // per-realisation partitions: the full K and B, rows per realisation
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
-        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * mt, scratch, lay,
-                           nullptr);
+        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
+                           lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
         hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr);
         const int cv = backxf_chunk(mt);
         hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * mt * 16, st, mt, r, scratch, lay,
@@ -806,7 +817,8 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     const SpecLayout lay(d, kmax);
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 16;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active);
+    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
+                       nullptr, 0);
     hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
     if (!wy_path(d, kmax)) {
         const int cv = backxf_chunk(d);

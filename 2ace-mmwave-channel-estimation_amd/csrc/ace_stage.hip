@@ -24,8 +24,11 @@ constexpr int RMAX = 32;  // max columns per realisation (r = min(20, m, n) in t
 template <bool ROW>
 __global__ __launch_bounds__(256) void init_r_kernel(int n, int m, int r, const double* X0p, const double* P0p,
                                                      const double* Bp, double* Xp, double* Yp, double* Mp,
-                                                     double* Np, RealState* st, double mu0) {
+                                                     double* Np, RealState* st, double mu0, const unsigned char* maskp,
+                                                     int ldmask) {
     const int b = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    // per-realisation train rows in m-space (PartRows): test rows take no part and stay Y = M = 0
+    const unsigned char* mask = maskp ? maskp + (long long)b * ldmask : nullptr;
     __shared__ double red[16 * (1 + RMAX)];
     __shared__ double scale[RMAX];
     const long long rn = (long long)r * n, rm = (long long)r * m;
@@ -36,6 +39,7 @@ __global__ __launch_bounds__(256) void init_r_kernel(int n, int m, int r, const 
 #pragma unroll
     for (int j = 0; j <= RMAX; ++j) v[j] = 0.0;
     for (int i = t; i < m; i += nt) {
+        if (mask && !mask[i]) continue;
         v[0] += B[i] * B[i];
 #pragma unroll
         for (int j = 0; j < RMAX; ++j)
@@ -70,6 +74,10 @@ __global__ __launch_bounds__(256) void init_r_kernel(int n, int m, int r, const 
     const double isr = 1.0 / sqrt((double)r);
     for (int i = t; i < m; i += nt) {
         const double bi = B[i];
+        if (mask && !mask[i]) {
+            for (int j = 0; j < r; ++j) Y[j * m + i] = M[j * m + i] = make_double2(0.0, 0.0);
+            continue;
+        }
         if (ROW) {
             double d2s = 0.0;
             for (int j = 0; j < r; ++j) d2s += cabs2(cscale(P0[j * m + i], scale[j]));
@@ -103,9 +111,10 @@ __global__ __launch_bounds__(256) void init_r_kernel(int n, int m, int r, const 
 template <bool ROW>
 __global__ __launch_bounds__(256) void ystep_r_kernel(int m, int r, const double* Sp, const double* gp, double* Mp,
                                                       const double* Bp, const double* Yold, double* Ynew,
-                                                      RealState* st) {
+                                                      RealState* st, const unsigned char* maskp, int ldmask) {
     constexpr int NV = ROW ? 5 : 5 + RMAX;
     const int b = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    const unsigned char* mask = maskp ? maskp + (long long)b * ldmask : nullptr;   // (as init_r_kernel)
     __shared__ double red[16 * NV];
     if (st[b].done) return;
     const double mu = st[b].mu, imu = 1.0 / mu;
@@ -131,6 +140,10 @@ __global__ __launch_bounds__(256) void ystep_r_kernel(int m, int r, const double
     };
     for (int i = t; i < m; i += nt) {
         const double bi = B[i];
+        if (mask && !mask[i]) {
+            for (int j = 0; j < r; ++j) Yn[j * m + i] = make_double2(0.0, 0.0);
+            continue;
+        }
         if constexpr (ROW) {
             double d2s = 0.0, ax2 = 0.0;
             for (int j = 0; j < r; ++j) {
@@ -426,6 +439,14 @@ __global__ __launch_bounds__(256) void put_col_kernel(int count, const int* src,
     dst[o] = or_mask ? (int)((unsigned)dst[o] | ((unsigned)src[k] & or_mask)) : src[k];
 }
 
+// the same for byte rows (partition tables)
+__global__ __launch_bounds__(256) void move_bytes_kernel(long long len, const unsigned char* src, unsigned char* dst,
+                                                         const int* idx, int scatter) {
+    const int k = blockIdx.x;
+    const long long so = (long long)(scatter ? k : idx[k]) * len, dof = (long long)(scatter ? idx[k] : k) * len;
+    for (long long e = threadIdx.x; e < len; e += blockDim.x) dst[dof + e] = src[so + e];
+}
+
 __global__ __launch_bounds__(256) void flag_bits_kernel(int count, const unsigned char* flag, int* dst, unsigned bit) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < count && flag[k]) dst[k] = (int)((unsigned)dst[k] | bit);
@@ -435,21 +456,174 @@ __global__ __launch_bounds__(256) void fill_kernel(long long count, double v, do
     const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < count) dst[k] = v;
 }
+
+// ---------------------------------------------------------------- per-realisation partitions (PartRows)
+// G_ee^{-1}: gather the test-row block of G, invert it in LDS (Gauss-Jordan without pivoting: G_ee is a
+// principal block of the HPD G = (I + K)^{-1}, eigenvalues in [1 / (1 + ||K||), 1])
+__global__ __launch_bounds__(256) void part_geinv_kernel(PartRows pr, const double* Gp, double* geinvp, int* status) {
+    const int b = blockIdx.x, t = threadIdx.x, m = pr.m, mt = pr.mt, te = m - mt;
+    extern __shared__ d2 Hs[];   // te x te
+    __shared__ int te_rows[PART_MAXTE];
+    __shared__ int bad;
+    const d2* G = reinterpret_cast<const d2*>(Gp);
+    const int* rows = pr.rows + (long long)b * m;
+    if (t < te) te_rows[t] = rows[mt + t];
+    if (t == 0) bad = 0;
+    __syncthreads();
+    for (int e = t; e < te * te; e += 256) Hs[e] = G[(long long)te_rows[e / te] * m + te_rows[e % te]];
+    __syncthreads();
+    for (int k = 0; k < te; ++k) {   // in-place Gauss-Jordan inverse
+        const d2 p = Hs[k * te + k];
+        const double pr2 = cabs2(p);
+        if (t == 0 && !(pr2 > 0.0)) bad = 1;
+        const d2 pinv = make_double2(p.x / pr2, -p.y / pr2);
+        __syncthreads();
+        for (int e = t; e < te * te; e += 256) {   // H_ij -= H_ik H_kk^{-1} H_kj off the pivot row and column
+            const int i = e / te, j = e % te;
+            if (i == k || j == k) continue;
+            Hs[e] = csub(Hs[e], cmul(cmul(Hs[i * te + k], pinv), Hs[k * te + j]));
+        }
+        __syncthreads();
+        for (int e = t; e < te; e += 256) {        // then the pivot row (x H_kk^{-1}) and column (x -H_kk^{-1})
+            if (e != k) {
+                Hs[k * te + e] = cmul(pinv, Hs[k * te + e]);
+                const d2 c = cmul(Hs[e * te + k], pinv);
+                Hs[e * te + k] = make_double2(-c.x, -c.y);
+            }
+        }
+        __syncthreads();
+        if (t == 0) Hs[k * te + k] = pinv;
+        __syncthreads();
+    }
+    d2* out = reinterpret_cast<d2*>(geinvp) + (long long)b * te * te;
+    for (int e = t; e < te * te; e += 256) out[e] = Hs[e];
+    if (t == 0 && bad && status) atomicOr(&status[b], (int)ACE_ST_EIG_NOCONV);
+}
+
+// g_t = u_t - G_te (G_ee^{-1} u_e), g_e = 0, with u = G T~ (whatever T~ holds on the test rows: its
+// contributions cancel exactly in the Schur form)
+__global__ __launch_bounds__(256) void part_gfix_kernel(int r, PartRows pr, const double* Gp, double* gp,
+                                                        const RealState* rs) {
+    const int b = blockIdx.x, t = threadIdx.x, m = pr.m, mt = pr.mt, te = m - mt;
+    if (rs && rs[b].done) return;
+    __shared__ d2 Ge[PART_MAXTE * PART_MAXTE / 4];   // G_ee^{-1} (te <= 48) or streamed from global
+    __shared__ int te_rows[PART_MAXTE];
+    __shared__ d2 ue[PART_MAXTE], de[PART_MAXTE];
+    const d2* G = reinterpret_cast<const d2*>(Gp);
+    const int* rows = pr.rows + (long long)b * m;
+    const unsigned char* mask = pr.mask + (long long)b * pr.ldmask;
+    const d2* gi = reinterpret_cast<const d2*>(pr.geinv) + (long long)b * te * te;
+    const bool lds = te * te <= PART_MAXTE * PART_MAXTE / 4;
+    if (t < te) te_rows[t] = rows[mt + t];
+    if (lds)
+        for (int e = t; e < te * te; e += 256) Ge[e] = gi[e];
+    __syncthreads();
+    for (int j = 0; j < r; ++j) {
+        d2* g = reinterpret_cast<d2*>(gp) + ((long long)b * r + j) * m;
+        if (t < te) ue[t] = g[te_rows[t]];
+        __syncthreads();
+        if (t < te) {   // d = G_ee^{-1} u_e
+            double re = 0.0, im = 0.0;
+            for (int f = 0; f < te; ++f) {
+                const d2 p = cmul(lds ? Ge[t * te + f] : gi[t * te + f], ue[f]);
+                re += p.x;
+                im += p.y;
+            }
+            de[t] = make_double2(re, im);
+        }
+        __syncthreads();
+        for (int i = t; i < m; i += 256) {
+            if (!mask[i]) {
+                g[i] = make_double2(0.0, 0.0);
+                continue;
+            }
+            double re = 0.0, im = 0.0;
+            for (int e = 0; e < te; ++e) {
+                const d2 p = cmul(G[(long long)i * m + te_rows[e]], de[e]);
+                re += p.x;
+                im += p.y;
+            }
+            g[i] = csub(g[i], make_double2(re, im));
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void part_expand_kernel(int r, PartRows pr, const double* srcp, double* dstp) {
+    const int b = blockIdx.y, j = blockIdx.x, m = pr.m, mt = pr.mt;
+    const int* rows = pr.rows + (long long)b * m;
+    const d2* src = reinterpret_cast<const d2*>(srcp) + ((long long)b * r + j) * mt;
+    d2* dst = reinterpret_cast<d2*>(dstp) + ((long long)b * r + j) * m;
+    for (int k = threadIdx.x; k < m; k += 256) dst[rows[k]] = k < mt ? src[k] : make_double2(0.0, 0.0);
+}
+
+__global__ __launch_bounds__(256) void part_compact_kernel(int r, PartRows pr, const double* srcp, double* dstp) {
+    const int b = blockIdx.y, j = blockIdx.x, m = pr.m, mt = pr.mt;
+    const int* rows = pr.rows + (long long)b * m;
+    const d2* src = reinterpret_cast<const d2*>(srcp) + ((long long)b * r + j) * m;
+    d2* dst = reinterpret_cast<d2*>(dstp) + ((long long)b * r + j) * mt;
+    for (int k = threadIdx.x; k < mt; k += 256) dst[k] = src[rows[k]];
+}
+
+// quality_kernel on each realisation's own test rows (ascending, as setdiff returns them, :49)
+__global__ __launch_bounds__(256) void part_quality_kernel(int n, PartRows pr, const double* Ap, const double* Xp,
+                                                           const double* Bp, double* q) {
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6, m = pr.m, mt = pr.mt;
+    __shared__ double red[16 * 2];
+    __shared__ double part[4];
+    const d2* X = reinterpret_cast<const d2*>(Xp) + (long long)b * n;
+    const d2* A = reinterpret_cast<const d2*>(Ap);
+    const int* rows = pr.rows + (long long)b * m;
+    double v[2] = {0.0, 0.0};
+    for (int i = mt; i < m; ++i) {
+        const int row = rows[i];
+        double re = 0.0, im = 0.0;
+        for (int k = t; k < n; k += 256) {
+            const d2 p = cmul(A[(long long)row * n + k], X[k]);
+            re += p.x;
+            im += p.y;
+        }
+        re = wave_sum(re);
+        im = wave_sum(im);
+        __syncthreads();
+        if (lane == 0) { part[w] = re; red[w] = im; }
+        __syncthreads();
+        if (t == 0) {
+            double sr = 0.0, si = 0.0;
+            for (int k = 0; k < 4; ++k) { sr += part[k]; si += red[k]; }
+            const double bi = Bp[(long long)b * m + row];
+            const double d = sqrt(sr * sr + si * si) - bi;
+            v[0] += d * d;
+            v[1] += bi * bi;
+        }
+    }
+    if (t == 0) q[b] = 1.0 - sqrt(v[0]) / sqrt(v[1]);
+}
 }  // namespace
 
 void launch_init_r(int row_mode, int n, int m, int r, int batch, const double* X0, const double* P0, const double* B,
-                   double* X, double* Y, double* M, double* N, RealState* rs, double mu0, hipStream_t st) {
+                   double* X, double* Y, double* M, double* N, RealState* rs, double mu0, hipStream_t st,
+                   const PartRows* pr) {
+    const unsigned char* mk = pr ? pr->mask : nullptr;
+    const int ld = pr ? pr->ldmask : 0;
     if (row_mode)
-        hipLaunchKernelGGL(init_r_kernel<true>, dim3(batch), dim3(256), 0, st, n, m, r, X0, P0, B, X, Y, M, N, rs, mu0);
+        hipLaunchKernelGGL(init_r_kernel<true>, dim3(batch), dim3(256), 0, st, n, m, r, X0, P0, B, X, Y, M, N, rs, mu0,
+                           mk, ld);
     else
-        hipLaunchKernelGGL(init_r_kernel<false>, dim3(batch), dim3(256), 0, st, n, m, r, X0, P0, B, X, Y, M, N, rs, mu0);
+        hipLaunchKernelGGL(init_r_kernel<false>, dim3(batch), dim3(256), 0, st, n, m, r, X0, P0, B, X, Y, M, N, rs,
+                           mu0, mk, ld);
 }
 void launch_ystep_r(int row_mode, int m, int r, int batch, const double* S, const double* g, double* M,
-                    const double* B, const double* Yold, double* Ynew, RealState* rs, hipStream_t st) {
+                    const double* B, const double* Yold, double* Ynew, RealState* rs, hipStream_t st,
+                    const PartRows* pr) {
+    const unsigned char* mk = pr ? pr->mask : nullptr;
+    const int ld = pr ? pr->ldmask : 0;
     if (row_mode)
-        hipLaunchKernelGGL(ystep_r_kernel<true>, dim3(batch), dim3(256), 0, st, m, r, S, g, M, B, Yold, Ynew, rs);
+        hipLaunchKernelGGL(ystep_r_kernel<true>, dim3(batch), dim3(256), 0, st, m, r, S, g, M, B, Yold, Ynew, rs, mk,
+                           ld);
     else
-        hipLaunchKernelGGL(ystep_r_kernel<false>, dim3(batch), dim3(256), 0, st, m, r, S, g, M, B, Yold, Ynew, rs);
+        hipLaunchKernelGGL(ystep_r_kernel<false>, dim3(batch), dim3(256), 0, st, m, r, S, g, M, B, Yold, Ynew, rs, mk,
+                           ld);
 }
 void launch_finalize_r(int n, int m, int r, int nc, int batch, const double* optX, const double* optY,
                        const double* Xc, const double* Yc, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
@@ -501,8 +675,33 @@ void launch_put_col(int count, const int* src, const int* idx, int* dst, int ld,
         hipLaunchKernelGGL(put_col_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, src, idx, dst, ld, col,
                            or_mask);
 }
+void launch_move_bytes(int count, long long len, const void* src, void* dst, const int* idx, bool scatter,
+                       hipStream_t st) {
+    if (count > 0)
+        hipLaunchKernelGGL(move_bytes_kernel, dim3(count), dim3(256), 0, st, len, (const unsigned char*)src,
+                           (unsigned char*)dst, idx, scatter ? 1 : 0);
+}
 void launch_flag_bits(int count, const unsigned char* flag, int* dst, unsigned bit, hipStream_t st) {
     if (count > 0) hipLaunchKernelGGL(flag_bits_kernel, dim3((count + 255) / 256), dim3(256), 0, st, count, flag, dst, bit);
+}
+void launch_part_geinv(int nb, const PartRows& pr, const double* G, double* geinv, int* status, hipStream_t st) {
+    const int te = pr.m - pr.mt;
+    if (nb > 0 && te > 0)
+        hipLaunchKernelGGL(part_geinv_kernel, dim3(nb), dim3(256), (size_t)te * te * 16, st, pr, G, geinv, status);
+}
+void launch_part_gfix(int nb, int r, const PartRows& pr, const double* G, double* g, const RealState* rs,
+                      hipStream_t st) {
+    if (nb > 0) hipLaunchKernelGGL(part_gfix_kernel, dim3(nb), dim3(256), 0, st, r, pr, G, g, rs);
+}
+void launch_part_expand(int nb, int r, const PartRows& pr, const double* src, double* dst, hipStream_t st) {
+    if (nb > 0) hipLaunchKernelGGL(part_expand_kernel, dim3(r, nb), dim3(256), 0, st, r, pr, src, dst);
+}
+void launch_part_compact(int nb, int r, const PartRows& pr, const double* src, double* dst, hipStream_t st) {
+    if (nb > 0) hipLaunchKernelGGL(part_compact_kernel, dim3(r, nb), dim3(256), 0, st, r, pr, src, dst);
+}
+void launch_part_quality(int n, int nb, const PartRows& pr, const double* A, const double* X, const double* B,
+                         double* q, hipStream_t st) {
+    if (nb > 0) hipLaunchKernelGGL(part_quality_kernel, dim3(nb), dim3(256), 0, st, n, pr, A, X, B, q);
 }
 void launch_fill(long long count, double v, double* dst, hipStream_t st) {
     if (count > 0) hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, count, v, dst);

@@ -101,7 +101,7 @@ __device__ __forceinline__ IterIn iter_in(const RealState* st) {
 // (it: the iteration being controlled, a.it except in msr_kernel, which runs several per launch)
 __device__ __forceinline__ int iter_control_in(const ZArgs& a, RealState* st, const IterIn& in, double mu, double nX2,
                                                double nZ2, double jn2, double dZ2, double dAtY, double nAtY, int it) {
-    const int m = a.m, n = a.n;
+    const int m = a.mthr ? a.mthr : a.m, n = a.n;
     const double nX = sqrt(nX2), nZ = sqrt(nZ2);
     const double dAtY2 = fmax(0.0, dAtY), nAtY2 = fmax(0.0, nAtY);
     const double obj = sqrt(in.obj2);

@@ -655,7 +655,7 @@ def refine_input_bench(args, dev, rank, world):
     from ace_amd import synth_problem, infer_low_rank_pipeline_batch, draw_partitions
     tx, m, bsz = args.tx, args.m, args.batch
     A, B, _, _ = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
-    tr = draw_partitions(np.random.default_rng(args.seed), m, 3)
+    tr = draw_partitions(np.random.default_rng(args.seed + rank), m, 3, batch=bsz)   # per call (:48)
     t0 = time.perf_counter()
     pr = infer_low_rank_pipeline_batch(A, B, tx, tx, tr, stop_before_refine=True)
     torch.cuda.synchronize()
@@ -723,7 +723,9 @@ def bench_pipeline(args, dev, rank, world):
     tx, m, bsz = args.tx, args.m, args.batch
     restarts = 3 if args.variant == "A2only" else 1
     A, B, _, H = synth_problem(args.seed, rank * bsz, bsz, m, tx, tx, device=dev)
-    tr = draw_partitions(np.random.default_rng(args.seed), m, restarts)
+    # every realisation its own partitions: randsample inside each inferLowRankV4_multi call (:48), as a
+    # Monte-Carlo batch of calls draws them (ACE_TRAIN_PER_REALISATION)
+    tr = draw_partitions(np.random.default_rng(args.seed + rank), m, restarts, batch=bsz)
     ws = ace_amd.solver.Workspace()
     res = None
 
@@ -773,7 +775,8 @@ def bench_pipeline(args, dev, rank, world):
         "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (30 dB SNR, L=3 paths)",
         "config": {"workload": f"{args.variant} pipeline, tx=rx={tx}, m={m}, {restarts} restarts, r=20",
-                   "batch_per_gpu": bsz, "partitions": "one per restart, shared by the batch"},
+                   "batch_per_gpu": bsz,
+                   "partitions": "per realisation and restart (train_idx [batch][restarts][m_t], randsample per call)"},
         "stage_iters_mean": np.round(its.mean(axis=0), 2).tolist(),
         "stage_iters_max": its.max(axis=0).tolist(),
         "median_rel_err_vs_true_H": float(np.median(nmse)),
@@ -789,14 +792,14 @@ def bench_pipeline(args, dev, rank, world):
     print(json.dumps(line), flush=True)
 
 
-def cpu_baseline_pipeline(args, A, B, tr):
+def cpu_baseline_pipeline(args, A, B, tr):   # tr: [batch][restarts][m_t]
     """The numpy oracle pipeline (oracle/ace_oracle.py::infer_low_rank_pipeline, the reference's
     algorithm line by line; BLAS threads as the host provides) on a bounded sample of the batch."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import ace_oracle as O
     k, t0 = 0, time.perf_counter()
     while k < min(len(B), args.cpu_recoveries or 8) and (k == 0 or time.perf_counter() - t0 < 20.0):
-        O.infer_low_rank_pipeline(A, B[k], args.tx, args.tx, list(tr),
+        O.infer_low_rank_pipeline(A, B[k], args.tx, args.tx, list(tr[k]),
                                   variant=O.VARIANT_A2ONLY if args.variant == "A2only" else O.VARIANT_NUCLEAR)
         k += 1
     dt = time.perf_counter() - t0

@@ -137,10 +137,18 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
                         double* X, double* Y, int32_t* iters, uint32_t* status, double* mu);
 
 /* ---- full recovery pipeline (inferLowRankV4_multi / inferLowRankV4 / inferLowRank_Nuclear) ----
- * MATLAB's randsample (:48) is replaced by caller-supplied train partitions: train_idx is a
- * HOST array [restarts][m_t] of 0-based row indices, m_t = floor(m * cc_frac), shared by the
- * whole batch (one codebook, one partition per restart: every GEMM of the stages then runs
- * on one shared A_t); test rows are the sorted complement (setdiff, :49).
+ * MATLAB's randsample (:48), drawn inside every call, is replaced by train partitions: train_idx is a
+ * HOST array of 0-based row indices, m_t = floor(m * cc_frac) per restart, in one of two layouts
+ * (ace_pipeline_cfg::train_layout):
+ *   ACE_TRAIN_SHARED          [restarts][m_t], one partition per restart for the whole batch;
+ *   ACE_TRAIN_PER_REALISATION [batch][restarts][m_t], each realisation its own (a Monte-Carlo batch
+ *                             of calls, each drawing its own randsample).
+ * train_idx = NULL draws per-realisation partitions with the build's counter RNG from
+ * ace_pipeline_cfg::train_seed (randperm prefixes, stream b * restarts + restart).  Test rows are the
+ * sorted complement (setdiff, :49).  Per-realisation partitions keep the stage state in m-space on the
+ * full A (test rows held at zero) and apply (I + K_t)^{-1} through the full (I + K)^{-1} and a
+ * per-realisation m_te x m_te block (the Schur identity; m - m_t <= 96); realisations whose partitions
+ * coincide for every restart take the shared-A_t path.
  * Per realisation, stage_iters holds 4*restarts + 1 counts: for each restart the two
  * inferLowRankImpl stages (:258, :270), then the two stages of the rank-one retry (:73-77;
  * 0 when not run), then the refinement (:92/:100) -- the order of the oracle's stage_iters. */
@@ -153,7 +161,8 @@ typedef struct ace_pipeline_cfg {
     int stop_before_refine; /* 0 (reference); 1: return X_max, the refinement's input (:90-92), rescaled
                           (:106-107), with Y_max on the train rows and no refinement stage (its
                           stage_iters column is 0) -- for measuring the unit on the reference's input */
-    int reserved[2];
+    int train_layout;  /* ACE_TRAIN_SHARED (default) or ACE_TRAIN_PER_REALISATION (see above) */
+    int train_seed;    /* seed of the build's draws when train_idx is NULL */
     double mu0;        /* 1e-3 */
     double rho;        /* 1.03 */
     double cc_frac;    /* 0.95 (:10) */
@@ -161,6 +170,8 @@ typedef struct ace_pipeline_cfg {
     double tol_abs;    /* 1e-8 */
 } ace_pipeline_cfg;
 
+#define ACE_TRAIN_SHARED 0
+#define ACE_TRAIN_PER_REALISATION 1
 /* Reference defaults for `variant`: A2only -> 3 restarts, nuclear -> 1 restart. */
 void ace_pipeline_cfg_default(ace_pipeline_cfg* cfg, int variant);
 /* Workspace bytes for ace_pipeline_solve_batch (0 on invalid arguments).  Not monotonic in batch: a batch

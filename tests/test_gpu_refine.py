@@ -8,8 +8,9 @@ m = 256, batch >= 1024 -- the split sub-batches, the fused gyf kernel and the m-
 check a sample against the C oracle (oracle/ace_oracle.c, the reference's U-form algorithm):
 X within 1e-5 after global-phase alignment (Evaluation_H.m:81-82), iteration counts equal.  They
 also run the whole pipeline at batch 256 (the int8 r-column stages) against the numpy oracle's
-outputs for a sample (tests/golden/pipeline_32ant_m256_b256.npz, make_pipeline_scale_golden.py),
-and InferADMM at r = 20 (the stages :258 / :270) through the public solver API.
+outputs for a sample (tests/golden/pipeline_32ant_m256_b256.npz, make_pipeline_scale_golden.py) with
+one partition set for the batch and with every realisation's own partitions, and InferADMM at
+r = 20 (the stages :258 / :270) through the public solver API.
 """
 import hashlib
 import math
@@ -178,3 +179,63 @@ def test_infer_admm_matlab_signature_r20(gpu):
     o1 = O.infer_admm(A[0], B[0], X0, False, False, 16, 16, maxiter=120)
     assert X1.shape == (256, 1) and Y1.shape == (64, 1)
     assert np.linalg.norm(X1 - o1.X) / np.linalg.norm(o1.X) <= TOL
+
+
+def test_pipeline_batch256_per_realisation_partitions_golden(gpu):
+    """SURVEY.md §8(b)'s train_idx [batch][restarts][m_t]: 256 realisations, each with its own three
+    partitions (randsample inside every call, inferLowRankV4_multi.m:48), in ONE batch: the stages run
+    on the full A in m-space with (I + K_t)^{-1} from the full G by the Schur identity
+    (launch_part_gfix).  Against the numpy oracle run per realisation on its own partitions (sample of
+    8): stage iteration counts, quality, rollback and the refinement's profile equal, X within 1e-5."""
+    import torch
+    from ace_amd import infer_low_rank_pipeline_batch
+    g = np.load(GOLD / "pipeline_32ant_m256_b256.npz")
+    A, B, _, each = _gold_inputs(g)
+    s = g["sample"]
+    pr = infer_low_rank_pipeline_batch(torch.from_numpy(A).cuda(), torch.from_numpy(B).cuda(), 32, 32, each)
+    its = pr.stage_iters.cpu().numpy()[s]
+    assert np.array_equal(its, g["each_stage_iters"]), (its, g["each_stage_iters"])
+    np.testing.assert_allclose(pr.quality.cpu().numpy()[s], g["each_quality"], rtol=0, atol=1e-9)
+    assert np.array_equal(pr.rank_one.cpu().numpy()[s], g["each_rank_one"])
+    assert np.array_equal(pr.rolled_back.cpu().numpy()[s], g["each_rolled_back"])
+    X = pr.X.cpu().numpy()[s]
+    e = np.array([O.phase_aligned_rel_err(X[k], g["each_X"][k]) for k in range(len(s))])
+    assert e.max() <= TOL, e
+
+
+def test_per_realisation_partitions_match_one_by_one(gpu):
+    """Per-realisation partitions in one batch (m-space stages, Schur-form G_t) against each realisation
+    solved alone on its own partition (the shared-A_t path with K_t, G_t formed directly): 16-ant,
+    m = 64 (f64 applies) and 32-ant, m = 256, batch 16 (int8 digit-plane applies, 320 vectors): equal
+    stage iteration counts and rollback flags, X within 1e-8 (different summation orders only)."""
+    from ace_amd import infer_low_rank_pipeline_host, synth, draw_partitions
+    for ant, m, batch, maxiter in ((16, 64, 5, 500), (32, 256, 16, 150)):
+        A, B, _, _ = synth.problem(4151 + ant, 0, batch, m, ant, ant)
+        tr = draw_partitions(np.random.default_rng(4151 + ant), m, 3, batch=batch)
+        full = infer_low_rank_pipeline_host(A[0], B, ant, ant, tr, maxiter=maxiter)
+        for b in range(batch):
+            one = infer_low_rank_pipeline_host(A[0], B[b:b + 1], ant, ant, tr[b], maxiter=maxiter)
+            assert np.array_equal(one.stage_iters[0], full.stage_iters[b]), (ant, b, one.stage_iters, full.stage_iters[b])
+            assert one.rolled_back[0] == full.rolled_back[b] and one.rank_one[0] == full.rank_one[b]
+            assert O.phase_aligned_rel_err(full.X[b], one.X[0]) <= 1e-8, (ant, b)
+            assert abs(one.quality[0] - full.quality[b]) <= 1e-10
+
+
+def test_partitions_drawn_by_the_build(gpu):
+    """train_idx = NULL: per-realisation partitions from the build's counter RNG (train_seed; stream
+    b * restarts + restart), the same as passing those draws explicitly."""
+    import ctypes as C
+    from ace_amd import infer_low_rank_pipeline_host, synth, engine
+    from ace_amd._lib import LIB, check, pipeline_cfg, ACE_TRAIN_PER_REALISATION
+    A, B, _, _ = synth.problem(4157, 0, 3, 64, 16, 16)
+    tr = np.stack([np.stack([engine.randperm(77, b * 3 + i, 64, 60) for i in range(3)]) for b in range(3)])
+    ref = infer_low_rank_pipeline_host(A[0], B, 16, 16, tr)
+    cfg = pipeline_cfg(0, train_layout=ACE_TRAIN_PER_REALISATION, train_seed=77)
+    X = np.empty((3, 256), np.complex128)
+    Y = np.empty((3, 64), np.complex128)
+    its = np.empty((3, 13), np.int32)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    check(LIB.ace_pipeline_solve_host(C.byref(cfg), 3, 64, 256, 16, 16, dp(A[0].view(np.float64)),
+                                      dp(np.ascontiguousarray(B)), None, dp(X.view(np.float64)), dp(Y.view(np.float64)),
+                                      None, its.ctypes.data_as(C.POINTER(C.c_int32)), None))
+    assert np.array_equal(X, ref.X) and np.array_equal(its, ref.stage_iters)

@@ -25,6 +25,7 @@ Modes (each its own line; only ``unit`` is the headline metric):
   phaselift  configs[3]: MyPhaseLift/TFOCS, 200 iterations, batch 512
   beamformer downstream svd_beamformer codebooks/s
   driver     latency of one drop-in driver call (main.py:427) on the reference probe codebook
+  refine     the unit line's refine_input object alone (X_max and the per-realisation rank-one flags)
 """
 from __future__ import annotations
 
@@ -72,7 +73,7 @@ def parse():
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
     ap.add_argument("--mode", default="unit",
-                    choices=["unit", "config5", "pipeline", "phaselift", "beamformer", "driver"])
+                    choices=["unit", "config5", "pipeline", "phaselift", "beamformer", "driver", "refine"])
     a = ap.parse_args()
     if not a.tx:
         a.tx = 16 if a.mode in ("beamformer", "driver") else 32
@@ -1077,6 +1078,12 @@ def main():
     if args.mode in ("pipeline", "phaselift", "beamformer", "driver"):
         {"pipeline": bench_pipeline, "phaselift": bench_phaselift, "beamformer": bench_beamformer,
          "driver": bench_driver}[args.mode](args, dev, rank, world)
+    elif args.mode == "refine":   # the unit on the reference's own refinement alone (refine_input of the unit line)
+        ri = refine_input_bench(args, dev, rank, world)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC + " -- reference refinement input", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                              "dtype": "f64", **ri}), flush=True)
     elif args.mode == "config5":
         line = unit_bench(args, False, dev, rank, world, config5_workload(args, rank, world, dev))
         if rank == 0:

@@ -810,12 +810,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const double shA = L.shared ? 16.0 * m * n : 16.0 * m * n * batch, shM = L.shared ? 16.0 * m * m : 16.0 * m * m * batch;
     // r-column Z-step: E E^H over the r column blocks (tx x tx x rx r complex MACs) plus the 32 x 32 Hermitian
     // eig (0.8 Mflop at tx = 32); A2nuclear: the r x r Gram E^H E and Z = E V diag V^H
-    // (3 n r^2 MACs).  Bytes: X, N, Z in; Z, N out; the warm-start eigenvectors in and out
+    // (3 n r^2 MACs).  Bytes: X, N, Z in; Z, N out; the warm-start eigenvectors in and out; the dual terms'
+    // Y, Y_old, K Y, K Y_old in (m r each)
     const double zs_fl = !fast ? (p.variant == ACE_VARIANT_NUCLEAR
                                       ? 8.0 * 3 * n * r * r * batch
                                       : (8.0 * p.tx * p.tx * p.rx * r + 0.8e6 * std::pow(p.tx / 32.0, 3)) * batch)
                                : 0.0;
-    const double zs_b = !fast ? (80.0 * n * r + 32.0 * p.tx * p.tx) * batch : 0.0;
+    const double zs_b = !fast ? (80.0 * n * r + 64.0 * m * r + 32.0 * p.tx * p.tx) * batch : 0.0;
     // wmode: Z, N ping-pong between (Z, N) and (Z2, N2); the Z-step writes the other pair
     double *Zc = w.Z, *Nc = w.N, *Zo = w.Z2, *No = w.N2;
     double lv = 1.0;   // share of the batch still iterating (convergence mode: from the polls), for ace_prof_work

@@ -1428,8 +1428,9 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
         if (flg_s[t] & 3) rsl[t].optysrc = 0;
         if (flg_s[t] >> 2) rsl[t].optsrc = 3;
     }
-    // state of iterate it0 - 1
-    d2 yv[TPW][4], mv[TPW][4], xv[TPW][4];
+    // state of iterate it0 - 1.  AX lives in the T tile between iterations: the thread's slot (jl, i) holds
+    // AX from its Y-step until its T formation reads it and writes T there (registers: 32 VGPRs fewer)
+    d2 yv[TPW][4], mv[TPW][4];
     double bv[TPW][4];
     {
         const int p = (a.it0 - 1) & 1;
@@ -1440,7 +1441,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 const long long o = off(r, c);
                 yv[c][r] = reinterpret_cast<const d2*>(a.Y[p])[o];
                 mv[c][r] = reinterpret_cast<const d2*>(a.M)[o];
-                xv[c][r] = reinterpret_cast<const d2*>(a.AX)[o];
+                Ts[((lane >> 4) + 4 * r) * tst + 16 * (TPW * w + c) + (lane & 15)] = reinterpret_cast<const d2*>(a.AX)[o];
                 bv[c][r] = a.B[o];
                 Ss[(4 * c + r) * NTW + t] = reinterpret_cast<const d2*>(a.S[p])[o];
             }
@@ -1468,11 +1469,13 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
             const double im = lv[r] ? 1.0 / mu_s[jl] : 0.0;
 #pragma unroll
             for (int c = 0; c < TPW; ++c) {
+                d2* slot = &Ts[jl * tst + 16 * (TPW * w + c) + (lane & 15)];
                 d2 v = make_double2(0.0, 0.0);
-                if (lv[r])
-                    v = make_double2(fma(-mv[c][r].x, im, yv[c][r].x) - xv[c][r].x,
-                                     fma(-mv[c][r].y, im, yv[c][r].y) - xv[c][r].y);
-                Ts[jl * tst + 16 * (TPW * w + c) + (lane & 15)] = v;
+                if (lv[r]) {
+                    const d2 xv = *slot;   // AX of the previous Y-step
+                    v = make_double2(fma(-mv[c][r].x, im, yv[c][r].x) - xv.x, fma(-mv[c][r].y, im, yv[c][r].y) - xv.y);
+                }
+                *slot = v;
             }
         }
         __syncthreads();
@@ -1533,6 +1536,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
             }
         }
         MSR_STAMP(1);
+        __syncthreads();   // every wave has read T: the Y-step writes AX into its slots
         MSR_STAMP(2);
         // Y-step and m-space sums.  gyk_body runs c outer, r inner; each sum v7[r][k] still adds its
         // c = 0 term first, so r outer (one r's sums live at a time) rounds identically.
@@ -1557,7 +1561,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 sn[c][r] = cadd(Ss[(4 * c + r) * NTW + t], gv);
                 yn[c][r] = y;
                 mv[c][r] = mn;
-                xv[c][r] = ax;
+                Ts[jl * tst + i] = ax;
             }
 #pragma unroll
             for (int k = 0; k < 5; ++k) v7[k] = bsum16(v7[k]);
@@ -1647,7 +1651,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                     reinterpret_cast<d2*>(a.Y[it & 1])[o] = yn[c][r];
                     reinterpret_cast<d2*>(a.Y[(it + 1) & 1])[o] = yv[c][r];
                     reinterpret_cast<d2*>(a.M)[o] = mv[c][r];
-                    reinterpret_cast<d2*>(a.AX)[o] = xv[c][r];
+                    reinterpret_cast<d2*>(a.AX)[o] = Ts[jl * tst + i];
                     reinterpret_cast<d2*>(a.S[it & 1])[o] = sn[c][r];
                     reinterpret_cast<d2*>(a.S[(it + 1) & 1])[o] = *ssl;
                 }

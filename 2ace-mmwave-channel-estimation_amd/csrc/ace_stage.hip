@@ -538,8 +538,9 @@ __global__ __launch_bounds__(256) void part_gfix_kernel(int r, PartRows pr, cons
                 continue;
             }
             double re = 0.0, im = 0.0;
-            for (int e = 0; e < te; ++e) {
-                const d2 p = cmul(G[(long long)i * m + te_rows[e]], de[e]);
+            for (int e = 0; e < te; ++e) {   // G[i][te_e] = conj(G[te_e][i]): row reads, coalesced over i
+                const d2 gr = G[(long long)te_rows[e] * m + i];
+                const d2 p = cmul(make_double2(gr.x, -gr.y), de[e]);
                 re += p.x;
                 im += p.y;
             }

@@ -275,6 +275,7 @@ PMC_KERNEL = {  # kernel-class -> kernel name prefix in the PMC profiles, per wo
 }
 PMC_KERNEL["nuclear"] = {"apply_G": "nms_kernel<false>"}   # the m-space iteration (ace_nucmsp.hip)
 PMC_KERNEL["config5"] = PMC_KERNEL["nuclear"]
+PMC_KERNEL["refine"] = PMC_KERNEL["unit"]   # the unit on the pipeline's X_max (bench.py --mode refine)
 # pipeline / PhaseLift: the dominant class's largest kernel (one launch per class launch)
 PMC_KERNEL["pipeline"] = {"apply_AH": "i8ah_kernel<false, false>", "apply_A": "i8a_kernel",
                           "apply_K": "i8ah_kernel<true, false>", "apply_G": "zgemm3m_kernel<0, false",
@@ -665,8 +666,10 @@ def refine_input_bench(args, dev, rank, world):
     flags = pr.rank_one.to(torch.uint8).contiguous()
     saved = args.no_cpu_baseline
     args.no_cpu_baseline = True
-    line = unit_bench(args, False, dev, rank, world, {"X0": X0, "rank_one": flags, "x0_note": "pipeline X_max"})
-    line0 = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max, default profile"})
+    line = unit_bench(args, False, dev, rank, world, {"X0": X0, "rank_one": flags, "x0_note": "pipeline X_max",
+                                                      "tag": "refine"})
+    line0 = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max, default profile",
+                                                       "tag": "refine"})
     args.no_cpu_baseline = saved
     if rank != 0:
         return None

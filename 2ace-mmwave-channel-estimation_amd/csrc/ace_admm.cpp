@@ -91,6 +91,7 @@ struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8, msr_waves = 8;
     bool msr = true;
     bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true, zcert = true;
+    bool r1lz = true;   // rank-one profile: top eigenpair by Lanczos in the one-wave Z-step (ACE_R1_LANCZOS=0: Jacobi)
     double msp_room = 32.0;
 };
 static Knobs read_knobs() {
@@ -117,6 +118,7 @@ static Knobs read_knobs() {
     k.i8r = on("ACE_I8_STAGES");
     k.msr = on("ACE_MSR");
     k.zcert = on("ACE_ZCERT");
+    k.r1lz = on("ACE_R1_LANCZOS");
     k.msr_start = (int)num("ACE_MSR_START", 56);
     k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
     if (k.msr_retry < 1) k.msr_retry = 1;
@@ -763,6 +765,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.warm = p.eig_warm;
     za.zcert = kn.zcert ? 1 : 0;
     za.mthr = p.part ? p.part->mt : 0;   // thresholds on the realisation's m_t train rows (:364-370)
+    za.r1lz = kn.r1lz ? 1 : 0;
     za.wmode = 0;
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)

@@ -452,6 +452,8 @@ struct ZArgs {
     int msp_fail_it;       // (tests: ACE_MSP_FAIL_IT) the bound of m-space iterates fails at this iteration
     int xzn;               // (apply_AH of the r-column stages) write X = (Z - N/mu) + A^H g instead of W
     int zcert;             // four-wave A2only Z-step: skip the eigensolver when the Ky Fan certificate holds
+    int r1lz;              // one-wave Z-step: rank-one profile realisations take the top eigenpair by Lanczos
+                           // (r1_top, ace_zprox1w.hip) instead of the full Jacobi eigensolver
     int mthr;              // rows of the convergence thresholds (:364-370) when they differ from the state's m:
                            // per-realisation train partitions keep m-space state, the reference's A_t has m_t rows
 };

@@ -135,6 +135,194 @@ __device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
     __syncthreads();
 }
 
+// ---- rank-one profile: the top eigenpair only --------------------------------------------------
+// With the profile [1] / [0.95] (use_rank_one, inferLowRankV4_multi.m:448-450) the tail rescaling
+// (:469-480) multiplies every eigenvalue but the largest by one factor c = min(1, vr / (v - vr) (1/f - 1)),
+// vr = lambda_1, v = the eigenvalue sum, so Z = U diag(sqrt(scale)) U^H E (:482-484) needs only
+// (lambda_1, u_1): Z = sqrt(c) E + (1 - sqrt(c)) u_1 u_1^H E.  r1_top finds them with Lanczos (full
+// reorthogonalisation) on the packed H = F F^H of the warm frame, started at the unit vector of H's
+// largest diagonal entry (column 0 of the warm start Q_prev holds the previous u_1: nearly converged),
+// and certifies the result: the Ritz residual beta_k |s_k| <= 2^-48 theta, and theta the LARGEST
+// eigenvalue (theta > v - theta, or sigma I - H positive definite for sigma just above theta: a
+// Cholesky).  Anything else returns false and the caller runs the full Jacobi eigensolver.
+constexpr int LZ_MAX = 16;   // Lanczos steps before giving up (the Jacobi path then runs)
+
+__device__ __forceinline__ d2 conj_d2(d2 v) { return make_double2(v.x, -v.y); }
+__device__ __forceinline__ double half_sum(double v) {   // sum over lanes 0..31 (both halves hold it)
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// largest eigenvalue and its eigenvector of the symmetric tridiagonal T (diag al[0..k), off be[1..k):
+// be[j] couples j - 1 and j), all in LDS: 64-lane multisection on Sturm counts, then on lane 0 the twisted
+// factorisation (LAPACK dlar1v) for the vector s[0..k) (normalised, in LDS; dp, dm: LDS scratch)
+__device__ __forceinline__ double tri_top(const double* al, const double* be, int k, int lane, double* s, double* dp,
+                                       double* dm) {
+    double lo = al[0], hi = al[0];
+    for (int j = 0; j < k; ++j) {
+        const double r = (j > 0 ? fabs(be[j]) : 0.0) + (j + 1 < k ? fabs(be[j + 1]) : 0.0);
+        lo = fmin(lo, al[j] - r);
+        hi = fmax(hi, al[j] + r);
+    }
+    const double scale = fmax(fabs(lo), fabs(hi));
+    const double tiny = 1e-300 + 1e-30 * scale * 2.2e-16;
+    for (int round = 0; round < 12 && hi - lo > 2.2e-16 * scale; ++round) {
+        const double x = lo + (hi - lo) * (double)(lane + 1) / 65.0;
+        int neg = 0;   // Sturm count: eigenvalues < x
+        double d = al[0] - x;
+        if (d == 0.0) d = -tiny;
+        neg += d < 0.0;
+        for (int j = 1; j < k; ++j) {
+            d = (al[j] - x) - be[j] * be[j] / d;
+            if (d == 0.0) d = -tiny;
+            neg += d < 0.0;
+        }
+        const int above = k - neg;
+        // the top eigenvalue lies in (x_i, x_{i+1}] with count(x_i) >= 1 > count(x_{i+1}) = 0
+        double nlo = above >= 1 ? x : lo, nhi = above == 0 ? x : hi;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            nlo = fmax(nlo, __shfl_xor(nlo, o, 64));
+            nhi = fmin(nhi, __shfl_xor(nhi, o, 64));
+        }
+        lo = nlo;
+        hi = nhi;
+    }
+    const double th = 0.5 * (lo + hi);
+    if (lane == 0) {   // twisted factorisation at th
+        for (int j = 0; j < k; ++j) {
+            const double d = (al[j] - th) - (j > 0 ? be[j] * be[j] / dp[j - 1] : 0.0);
+            dp[j] = d == 0.0 ? tiny : d;
+        }
+        for (int j = k - 1; j >= 0; --j) {
+            const double d = (al[j] - th) - (j + 1 < k ? be[j + 1] * be[j + 1] / dm[j + 1] : 0.0);
+            dm[j] = d == 0.0 ? tiny : d;
+        }
+        int r = 0;
+        double gbest = INFINITY;
+        for (int j = 0; j < k; ++j) {
+            const double g = fabs(dp[j] + dm[j] - (al[j] - th));
+            if (g < gbest) { gbest = g; r = j; }
+        }
+        s[r] = 1.0;
+        double nrm = 1.0;
+        for (int j = r - 1; j >= 0; --j) { s[j] = -be[j + 1] * s[j + 1] / dp[j]; nrm += s[j] * s[j]; }
+        for (int j = r + 1; j < k; ++j) { s[j] = -be[j] * s[j - 1] / dm[j]; nrm += s[j] * s[j]; }
+        const double inv = 1.0 / sqrt(nrm);
+        for (int j = 0; j < k; ++j) s[j] *= inv;
+    }
+    __syncthreads();
+    return th;
+}
+
+// H: packed upper Hermitian (up_idx), zero beyond tx; Vb: LDS scratch of ZPACK complex (the Lanczos basis,
+// LZ_MAX x 32, then the Cholesky copy); tri: LDS scratch of 5 LZ_MAX + 2 doubles.  On success y (component
+// lane & 31 of the unit top eigenvector) and theta.
+__device__ __forceinline__ bool r1_top(const d2* H, d2* Vb, double* tri, int tx, int lane, double tr, d2& y, double& theta) {
+    const int i = lane & 31, h = lane >> 5;
+    double* al = tri;                     // alpha_0 ..
+    double* be = tri + LZ_MAX;            // beta_1 .. at be[1 ..]
+    double* sv = tri + 2 * LZ_MAX + 1;    // Ritz vector of T
+    double* dp = sv + LZ_MAX;
+    double* dm = dp + LZ_MAX;
+    if (!(tr > 0.0)) return false;
+    // start: the unit vector of the largest diagonal entry (first index on ties)
+    double dg = i < tx ? H[up_idx(i, i)].x : -1.0;
+    int i0 = i;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        const double od = __shfl_xor(dg, o, 64);
+        const int oi = __shfl_xor(i0, o, 64);
+        if (od > dg || (od == dg && oi < i0)) { dg = od; i0 = oi; }
+    }
+    d2 q = make_double2(i == i0 ? 1.0 : 0.0, 0.0), qprev = make_double2(0.0, 0.0);
+    double bk = 0.0;   // beta_k
+    bool conv = false;
+    int k = 0;
+    for (; k < LZ_MAX && k < tx; ++k) {
+        if (h == 0) Vb[k * 32 + i] = q;
+        __syncthreads();
+        // w = H q_k: row i, columns 16h .. 16h + 15, then the two halves combined
+        double wr = 0.0, wi = 0.0;
+        for (int c = 16 * h; c < 16 * h + 16; ++c) {
+            const d2 hv = i <= c ? H[up_idx(i, c)] : conj_d2(H[up_idx(c, i)]), v = Vb[k * 32 + c];
+            wr += hv.x * v.x - hv.y * v.y;
+            wi += hv.x * v.y + hv.y * v.x;
+        }
+        wr += __shfl_xor(wr, 32, 64);
+        wi += __shfl_xor(wi, 32, 64);
+        const double alpha = half_sum(q.x * wr + q.y * wi);   // Re q^H w
+        wr -= alpha * q.x + bk * qprev.x;
+        wi -= alpha * q.y + bk * qprev.y;
+        for (int pass = 0; pass < 2; ++pass)                  // full reorthogonalisation, twice
+            for (int j = 0; j <= k; ++j) {
+                const d2 v = Vb[j * 32 + i];
+                const double cr = half_sum(v.x * wr + v.y * wi), ci = half_sum(v.x * wi - v.y * wr);
+                wr -= cr * v.x - ci * v.y;
+                wi -= cr * v.y + ci * v.x;
+            }
+        const double bn = sqrt(half_sum(wr * wr + wi * wi));
+        if (lane == 0) {
+            al[k] = alpha;
+            be[k + 1] = bn;
+        }
+        __syncthreads();
+        const int kk = k + 1;
+        const bool inv = !(bn > 1e-300 * tr);   // an invariant subspace: the Ritz values are exact
+        if (kk % 4 == 0 || kk == tx || kk == LZ_MAX || inv) {
+            theta = tri_top(al, be, kk, lane, sv, dp, dm);
+            if (inv || kk == tx || bn * fabs(sv[kk - 1]) <= 0x1p-48 * theta) {
+                conv = theta > 0.0;
+                k = kk;
+                break;
+            }
+        }
+        qprev = q;
+        q = make_double2(wr / bn, wi / bn);
+        bk = bn;
+    }
+    if (!conv) return false;
+    // Ritz vector y = V s
+    double yr = 0.0, yi = 0.0;
+    for (int j = 0; j < k; ++j) {
+        const d2 v = Vb[j * 32 + i];
+        yr += sv[j] * v.x;
+        yi += sv[j] * v.y;
+    }
+    const double yn = 1.0 / sqrt(half_sum(yr * yr + yi * yi));
+    y = make_double2(yr * yn, yi * yn);
+    // theta is the largest eigenvalue: every other is <= tr - theta < theta, or sigma I - H > 0
+    if (theta > 0.5 * tr * (1.0 + 1e-12)) return true;
+    const double sigma = theta * (1.0 + 1e-11);
+    __syncthreads();
+    d2* C = Vb;   // packed copy of sigma I - H
+    for (int e = lane; e < ZPACK; e += 64) {
+        const d2 v = H[e];
+        C[e] = make_double2(-v.x, -v.y);
+    }
+    __syncthreads();
+    if (lane < 32) C[up_idx(lane, lane)].x += sigma;
+    __syncthreads();
+    int bad = 0;
+    for (int c = 0; c < tx; ++c) {   // right-looking Cholesky: row c of U, then the trailing rows
+        const double d = C[up_idx(c, c)].x;
+        if (!(d > 0.0)) { bad = 1; break; }
+        const double is = 1.0 / sqrt(d);
+        __syncthreads();
+        for (int j = c + 1 + lane; j < tx; j += 64) C[up_idx(c, j)] = cscale(C[up_idx(c, j)], is);
+        __syncthreads();
+        for (int r2 = c + 1 + i; r2 < tx; r2 += 32)
+            for (int j = r2 + h; j < tx; j += 2) {
+                const d2 ur = C[up_idx(c, r2)], uj = C[up_idx(c, j)];
+                // A_rj -= conj(U_cr) U_cj
+                C[up_idx(r2, j)] = csub(C[up_idx(r2, j)], make_double2(ur.x * uj.x + ur.y * uj.y, ur.x * uj.y - ur.y * uj.x));
+            }
+        __syncthreads();
+    }
+    return !bad;
+}
+
 template <bool INIT>
 __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const int lane = threadIdx.x;
@@ -175,6 +363,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     __shared__ double wv[ZT], scl[ZT], rs2[ZT];
     __shared__ int ord[ZT], ascp[ZT];
     __shared__ int flag_any, flag_fast;
+    __shared__ double lz_tri[5 * LZ_MAX + 2];   // r1_top's tridiagonal and scratch
 
     const double mu = INIT ? 1.0 : st->mu;
     const d2* X = reinterpret_cast<const d2*>(xin ? a.Zn : a.X) + (long long)b * n;
@@ -545,6 +734,11 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     dbg_t1 = __builtin_amdgcn_s_memrealtime();
     sweeps = 0;
 #endif
+    // rank-one profile ([1] / [0.95]): the top eigenpair by Lanczos (r1_top) instead of every eigenpair
+    d2 r1y = make_double2(0.0, 0.0);
+    double r1th = 0.0;
+    const bool r1 = a.r1lz && pf.np == 1 && pf.rl[0] == 1 && r1_top(T0, T0 + ZPACK, lz_tri, tx, lane, tr, r1y, r1th);
+    if (!r1) {
 
     // ---- Jacobi sweeps in the position frame (see ace_zprox.hip for the scheme)
     const int kl = lane & 15, g = lane >> 4;
@@ -771,6 +965,38 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
         const int i = g + 4 * r;
         T0[i * ZHS + 2 * kl] = make_double2(Rt[r][0], Rt[r][1]);
         T0[i * ZHS + 2 * kl + 1] = make_double2(Rb[r][0], Rb[r][1]);
+    }
+    } else {
+        // the reference's rescale (:469-480) with vr = lambda_1 = theta and v = trace(H) = the eigenvalue sum:
+        // every eigenvalue but the largest scaled by c; then Qnew = Qprev Hw with the Householder
+        // reflector Hw = I - 2 w w^H / (w^H w), w = y + phi e_1 (phi = y_0 / |y_0|): Hw y = -phi e_1, so
+        // column 0 of Qnew is the top eigenvector (up to a phase) and Z = Qnew diag(sqrt(scl)) Qnew^H E
+        __syncthreads();
+        if (lane == 0) {
+            const double f = pf.fl[0], vr = r1th;
+            double c = 1.0;
+            if (vr < tr * f) c = fmin(1.0, vr / (tr - vr) * (1.0 / f - 1.0));
+            flag_any = c < 1.0;
+            lz_tri[0] = c;
+        }
+        d2* wsh = reinterpret_cast<d2*>(RotS);   // 32 complex
+        const double y0r = __shfl(r1y.x, 0, 64), y0i = __shfl(r1y.y, 0, 64);
+        const double a0 = sqrt(y0r * y0r + y0i * y0i);
+        const d2 phi = a0 > 0.0 ? make_double2(y0r / a0, y0i / a0) : make_double2(1.0, 0.0);
+        if (lane < 32) wsh[lane] = lane == 0 ? cadd(r1y, phi) : r1y;
+        __syncthreads();
+        const double c = lz_tri[0];
+        if (lane < ZT) {
+            scl[lane] = lane == 0 ? 1.0 : c;
+            ord[lane] = lane;
+        }
+        const double f2 = 2.0 / (2.0 + 2.0 * a0);   // 2 / (w^H w), ||y|| = 1
+        for (int e = lane; e < ZT * ZT; e += 64) {
+            const int i = e >> 5, j = e & 31;
+            const d2 wi = wsh[i], wj = wsh[j];
+            const d2 p = make_double2(wi.x * wj.x + wi.y * wj.y, wi.y * wj.x - wi.x * wj.y);   // w_i conj(w_j)
+            T0[i * ZHS + j] = make_double2((i == j ? 1.0 : 0.0) - f2 * p.x, -f2 * p.y);
+        }
     }
     __syncthreads();
     if (warm) {

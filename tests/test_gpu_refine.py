@@ -239,3 +239,36 @@ def test_partitions_drawn_by_the_build(gpu):
                                       dp(np.ascontiguousarray(B)), None, dp(X.view(np.float64)), dp(Y.view(np.float64)),
                                       None, its.ctypes.data_as(C.POINTER(C.c_int32)), None))
     assert np.array_equal(X, ref.X) and np.array_equal(its, ref.stage_iters)
+
+
+@pytest.mark.parametrize("tx,m,fixed", [(32, 256, True), (32, 256, False), (16, 64, False)])
+def test_rank_one_top_eigenpair_matches_jacobi(gpu, monkeypatch, tx, m, fixed):
+    """The rank-one profile's Z-step needs only (lambda_1, u_1) (every other eigenvalue takes one scale,
+    inferLowRankV4_multi.m:469-484): the one-wave Z-step finds them by Lanczos with a certified residual
+    and top-ness (r1_top) instead of the full Jacobi eigensolver.  Against the Jacobi path
+    (ACE_R1_LANCZOS=0) on the reference's refinement input (X_max of the pipeline, its own flags): equal
+    iteration counts, X within 1e-10; a sample against the C oracle within 1e-5."""
+    import torch
+    from ace_amd import infer_admm_batch, infer_low_rank_pipeline_batch, synth_problem, draw_partitions
+    batch = 512 if tx == 32 else 256
+    A, B, _, _ = synth_problem(4211 + tx, 0, batch, m, tx, tx)
+    tr = draw_partitions(np.random.default_rng(4211), m, 3, batch=batch)
+    pr = infer_low_rank_pipeline_batch(A, B, tx, tx, tr, stop_before_refine=True)
+    flags = torch.ones(batch, dtype=torch.uint8, device=A.device)
+    X0 = pr.X.contiguous()
+    kw = dict(maxiter=200 if fixed else 500, fixed_iters=fixed, use_rank_one=flags)
+    lz = infer_admm_batch(A, B, X0, tx, tx, **kw)
+    Xl, il = lz.X.cpu().numpy(), lz.iters.cpu().numpy()
+    monkeypatch.setenv("ACE_R1_LANCZOS", "0")
+    jc = infer_admm_batch(A, B, X0, tx, tx, **kw)
+    Xj, ij = jc.X.cpu().numpy(), jc.iters.cpu().numpy()
+    assert np.array_equal(il, ij), (il[il != ij][:8], ij[il != ij][:8])
+    e = _errs(Xl, Xj)
+    assert np.median(e) <= 1e-12 and e.max() <= 1e-10, (np.median(e), e.max())
+    idx = np.arange(0, batch, batch // 4)
+    U = OC.make_U(A[0].cpu().numpy())[None]
+    Xo, _, ito, _, _ = OC.infer_admm_r1_batch(A[0].cpu().numpy()[None], U, B.cpu().numpy()[idx], X0.cpu().numpy()[idx],
+                                              tx, tx, variant=0, use_rank_one=True, maxiter=kw["maxiter"],
+                                              fixed_iters=fixed)
+    assert np.array_equal(il[idx], ito), (il[idx], ito)
+    assert _errs(Xl[idx], Xo).max() <= TOL

@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--no-regime-p", action="store_true", help="unit mode: skip the regime-P measurement")
     ap.add_argument("--no-refine-input", action="store_true",
                     help="unit mode: skip the measurement on the pipeline's refinement input")
+    ap.add_argument("--no-default-profile", action="store_true",
+                    help="refine_input: skip the comparison run with the default rank profile for every realisation")
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
     ap.add_argument("--mode", default="unit",
@@ -668,8 +670,8 @@ def refine_input_bench(args, dev, rank, world):
     args.no_cpu_baseline = True
     line = unit_bench(args, False, dev, rank, world, {"X0": X0, "rank_one": flags, "x0_note": "pipeline X_max",
                                                       "tag": "refine"})
-    line0 = unit_bench(args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max, default profile",
-                                                       "tag": "refine"})
+    line0 = None if args.no_default_profile else unit_bench(
+        args, False, dev, rank, world, {"X0": X0, "x0_note": "pipeline X_max, default profile", "tag": "refine"})
     args.no_cpu_baseline = saved
     if rank != 0:
         return None
@@ -683,10 +685,10 @@ def refine_input_bench(args, dev, rank, world):
             "pipeline_s": round(t_pipe, 2), "quality_median": float(np.median(q)),
             "roofline": line["roofline"], "roofline_msr": line["roofline_msr"],
             "kernels_ms": line["kernels_ms"], "checks": line["checks"],
-            "default_profile": {"value": line0["value"], "ms_per_step": line0["ms_per_step"],
-                                "msp_frac": line0["msp_frac"],
-                                "note": "the same X0 with use_rank_one = 0 for every realisation (not the "
-                                        "reference's refinement for rank_one_frac of them)"}}
+            "default_profile": None if line0 is None else {
+                "value": line0["value"], "ms_per_step": line0["ms_per_step"], "msp_frac": line0["msp_frac"],
+                "note": "the same X0 with use_rank_one = 0 for every realisation (not the reference's refinement "
+                        "for rank_one_frac of them)"}}
 
 
 def config5_workload(args, rank, world, dev):

@@ -14,7 +14,7 @@ args() {
     config5) echo "--mode config5 --global-batch 16384 --steps 1 --warmup 1";;
     pipeline) echo "--mode pipeline --batch 1024 --steps 1 --warmup 0";;
     phaselift) echo "--mode phaselift --iters 20 --steps 1 --warmup 0";;
-    refine) echo "--mode refine --steps 1 --warmup 1";;
+    refine) echo "--mode refine --steps 1 --warmup 1 --no-default-profile";;
   esac
 }
 batch() { case $1 in config5) echo 16384;; pipeline) echo 1024;; phaselift) echo 512;; *) echo 4096;; esac; }

@@ -85,10 +85,16 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 //   ACE_MSR_START=<it>  first iteration at which an m-space run is tried (default 56)
 //   ACE_MSR_RETRY=<k>   after a run stopped early, the next try k iterations after its resume point
 //   ACE_MSR_WAVES=4     the m-space run as four waves of four output tiles (default eight of two)
+//   ACE_TK_EIG=<it>     the one-wave Z-step takes the full profile's top-K eigenpairs by tridiagonal reduction
+//                       (topk_tri) in the init Z-step and iterations <= it; later ones run the warm Jacobi
+//                       (default 6; 0: Jacobi throughout); ACE_TK_TRACE=1: its use and fallback counts
+//                       on stderr at the end of the solve
 //   ACE_ZCERT=0         the four-wave Z-step (r-column stages) always runs its eigensolver (no Ky Fan
 //                       certificate)
 struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8, msr_waves = 8;
+    int tkeig = 6;
+    bool tk_trace = false;
     bool msr = true;
     bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true, zcert = true;
     bool r1lz = true;   // rank-one profile: top eigenpair by Lanczos in the one-wave Z-step (ACE_R1_LANCZOS=0: Jacobi)
@@ -119,6 +125,8 @@ static Knobs read_knobs() {
     k.msr = on("ACE_MSR");
     k.zcert = on("ACE_ZCERT");
     k.r1lz = on("ACE_R1_LANCZOS");
+    k.tkeig = (int)num("ACE_TK_EIG", 6);
+    k.tk_trace = num("ACE_TK_TRACE", 0) != 0;
     k.msr_start = (int)num("ACE_MSR_START", 56);
     k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
     if (k.msr_retry < 1) k.msr_retry = 1;
@@ -702,6 +710,15 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
     return ACE_OK;
 }
 
+// ACE_TK_TRACE: the one-wave Z-step's tridiagonal uses and Jacobi fallbacks (ZArgs::tkcnt) of the solve
+static int tk_report(const Knobs& kn, const AdmmState& w, int rc, hipStream_t st) {
+    if (!kn.tk_trace || rc != ACE_OK) return rc;
+    int tkc[2] = {0, 0};
+    ACE_HIP(read_back(tkc, w.done + 32, sizeof(tkc), st));
+    fprintf(stderr, "[ace] tridiagonal Z-steps %d, Jacobi fallbacks %d\n", tkc[0], tkc[1]);
+    return rc;
+}
+
 int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch, const double* B,
              const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status, double* mu_out,
              hipStream_t st) {
@@ -766,6 +783,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.zcert = kn.zcert ? 1 : 0;
     za.mthr = p.part ? p.part->mt : 0;   // thresholds on the realisation's m_t train rows (:364-370)
     za.r1lz = kn.r1lz ? 1 : 0;
+    za.tkeig = kn.tkeig > 0 ? kn.tkeig : 0;
+    za.tkcnt = w.done + 32;
     za.wmode = 0;
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)
@@ -800,7 +819,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     const int poll = 8;
     const int nsplit = gyk ? split_count(batch) : 1;
     if (nsplit > 1 || (gyk && kn.mspace && p.variant != ACE_VARIANT_NUCLEAR))
-        return admm_iterate_split(L, p, w, za, batch, B, nsplit, kn, Xo, Yo, iters, status, mu_out, st);
+        return tk_report(kn, w, admm_iterate_split(L, p, w, za, batch, B, nsplit, kn, Xo, Yo, iters, status, mu_out, st), st);
     // algorithmic flops of the f64 GEMM-shaped applies as launched (all batch * r vectors; the
     // unit path's fused int8 kernels are accounted by the bench): ace_prof_work
     const double fl_mn = 8.0 * m * n * nv, fl_mm = 8.0 * m * m * nv;
@@ -950,7 +969,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                           (gyk || pc) ? w.Y[1] : nullptr);
     }
     ACE_HIP(hipGetLastError());
-    return ACE_OK;
+    return tk_report(kn, w, ACE_OK, st);
 }
 
 }  // namespace ace

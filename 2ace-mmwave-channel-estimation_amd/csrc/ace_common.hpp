@@ -456,6 +456,9 @@ struct ZArgs {
                            // (r1_top, ace_zprox1w.hip) instead of the full Jacobi eigensolver
     int mthr;              // rows of the convergence thresholds (:364-370) when they differ from the state's m:
                            // per-realisation train partitions keep m-space state, the reference's A_t has m_t rows
+    int tkeig;             // one-wave Z-step, full profile: the top-K eigenpairs by tridiagonal reduction (topk_tri,
+                           // ace_zprox1w.hip) in the init Z-step and iterations it <= tkeig (0: Jacobi throughout)
+    int* tkcnt;            // (diagnostics, nullable) [2]: topk_tri uses, and fallbacks to the Jacobi eigensolver
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

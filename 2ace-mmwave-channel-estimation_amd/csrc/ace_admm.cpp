@@ -513,7 +513,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
                 const MsrArgs ma{L.Gf, B + (long long)h * chunk * m, {wh.Y[0], wh.Y[1]}, wh.M, wh.AX,
                                  {wh.Sg[0], wh.Sg[1]}, wh.optS, wh.optY, wh.st, w.done + 8 + h, w.done + 1,
-                                 w.done + 12 + 4 * h, nb[h], m, it, p.maxiter};
+                                 w.done + 12 + 4 * h, w.done + 40 + h, nb[h], m, it, p.maxiter};
                 ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 8 + h), p.maxiter, 1, ss[h]));
                 ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 12 + 4 * h), 0, 4, ss[h]));
                 ProfScope ps(ACE_K_MSR, ss[h]);
@@ -531,6 +531,11 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 if (msr_trace())
                     fprintf(stderr, "msr h %d it %d: resume %d steps %d notready %d fail %d pend %d\n", h, it, rv[h],
                             rv[4 + 4 * h], rv[5 + 4 * h], rv[6 + 4 * h], rv[7 + 4 * h]);
+            }
+            if (msr_trace()) {   // m-vectors written (opt_Y / opt_S and the write-back; cumulative over the solve)
+                int vw[4] = {0, 0, 0, 0};
+                ACE_HIP(read_back(vw, w.done + 40, sizeof(vw), st));
+                fprintf(stderr, "msr it %d: vectors written %d %d %d %d (m = %d)\n", it, vw[0], vw[1], vw[2], vw[3], m);
             }
             int e = p.maxiter;
             for (int h = 0; h < nsplit; ++h)

@@ -309,6 +309,8 @@ struct MsrArgs {
     int* mspcount;   // m-space step counter (ace_prof_msp_steps)
     int* steps;      // [4]: realisation-iterations this launch ran (bench accounting); blocks not ready,
                      // runs stopped by a failed bound, by a pending test (diagnostics); the caller zeroes them
+    int* vecw;       // (nullable) += m-vectors the run wrote to memory: best iterates (opt_Y, opt_S) and the
+                     // state written back at a stop (Y twice, M, AX, S twice): its algorithmic write traffic
     int nb, m, it0, it_end;
 };
 bool msr_supported(int m);

@@ -1413,6 +1413,8 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
     auto off = [&](int r, int c) -> long long {
         return (long long)(lv[r] ? j0 + (lane >> 4) + 4 * r : j0) * m + 16 * (TPW * w + c) + (lane & 15);
     };
+    int vw = 0;   // m-vectors realisation t writes (MsrArgs::vecw)
+    if (t < GRB && live_s[t]) vw = ((flg_s[t] & 3) ? 1 : 0) + ((flg_s[t] >> 2) ? 1 : 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int fl = flg_s[(lane >> 4) + 4 * r];
@@ -1632,6 +1634,11 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
         }
         const bool alive = any & 32;
         const bool stop = (any & 24) || it + 1 >= a.it_end || !alive;
+        if (t < GRB) {
+            const int f = flg_s[t];
+            vw += (f & 1) + ((f >> 1) & 1);
+            if (f & (4 | 32) && (stop || (f & 4))) vw += 6 + ((f >> 6) & 1) + ((f >> 7) & 1);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             if (!lv[r]) continue;
@@ -1672,6 +1679,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 atomicAdd(a.mspcount, cnt);
                 atomicAdd(a.steps, cnt);
             }
+            if (t < GRB && vw && a.vecw) atomicAdd(a.vecw, vw);
             if (t < GRB && live_s[t]) {   // (stopped realisations were written back at their stop)
                 if (mylive) rsl[t].mres = rp;
                 a.rs[j0 + t] = rsl[t];

@@ -178,6 +178,10 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         d2 eb[4];
         cr = d4v{0.0, 0.0, 0.0, 0.0};
         ci = d4v{0.0, 0.0, 0.0, 0.0};
+#ifdef ACE_DEBUG_TK   // phase times of realisation 5 (10 ns units)
+        unsigned long long zt[6];
+        zt[0] = __builtin_amdgcn_s_memrealtime();
+#endif
         // tx, rx <= 16 (the driver's 16 x 16 arrays): E E^H is one 16 x 16 tile, so each wave
         // accumulates the blocks j = w, w + 4, ... straight from memory (16 MFMAs per block, no
         // LDS staging or barrier per block) and the four partial tiles are summed in LDS.
@@ -224,6 +228,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             }
             store32(L0, cr, ci, lane, w);
         }
+#ifdef ACE_DEBUG_TK
+        zt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
         const bool warm = (!INIT) && a.warm && a.Q;
         d2* Qg = a.Q ? reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx : nullptr;
         for (int e = t; e < TXMAX * TXMAX; e += nt) {
@@ -260,6 +267,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         // eigenvalues of H, so if the r_p largest diagonal entries clear f_p * trace with margin for
         // every profile entry, no tail rescaling fires (:475) and Z = E exactly (:482).  The
         // eigendecomposition is then skipped (Q stays the next warm start).
+#ifdef ACE_DEBUG_TK
+        zt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
         __shared__ int cert_s;
         if (t < tx) {   // descending order of the diagonal (ties by index)
             const double dk = L0[t * HS + t].x;
@@ -330,6 +340,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
         }
         __syncthreads();
+#ifdef ACE_DEBUG_TK
+        zt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (a.Q && (!cert || !warm)) {   // (a certified cold step stores I: a unitary warm start)
             for (int e = t; e < tx * tx; e += nt) Qg[e] = L1[(e / tx) * HS + (e % tx)];
         }
@@ -421,6 +434,12 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
                 }
             }
         }
+#ifdef ACE_DEBUG_TK
+        zt[4] = __builtin_amdgcn_s_memrealtime();
+        if (t == 0 && (b == 5 || b == 700) && r > 1)
+            printf("zs4 b %d it %d r %d: H %llu warm %llu eig(cert %d) %llu W+Z %llu (x10ns)\n", b, a.it, r, zt[1] - zt[0],
+                   zt[2] - zt[1], (int)cert, zt[3] - zt[2], zt[4] - zt[3]);
+#endif
     }
 #undef ACE_ZSTEP_LDS
     // bound for the next iteration's V = Z - N/mu (written after iter_control's mu update)

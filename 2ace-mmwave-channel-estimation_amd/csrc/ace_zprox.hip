@@ -18,6 +18,7 @@
 #include "ace_common.hpp"
 #include "ace_zcommon.hpp"
 #include "ace_eig.hpp"
+#include "ace_topk.hpp"
 
 namespace ace {
 
@@ -182,86 +183,92 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         unsigned long long zt[6];
         zt[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-        // tx, rx <= 16 (the driver's 16 x 16 arrays): E E^H is one 16 x 16 tile, so each wave
-        // accumulates the blocks j = w, w + 4, ... straight from memory (16 MFMAs per block, no
-        // LDS staging or barrier per block) and the four partial tiles are summed in LDS.
         const bool small = tx <= 16 && rx <= 16;
-        if (small) {
-            for (int j = w; j < r; j += 4) {
-                d2 ev[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {   // lane: E_j[l & 15][4u + (l >> 4)]
-                    const int i = lane & 15, kk = 4 * u + (lane >> 4);
-                    ev[u] = (i < tx && kk < rx) ? evalE(j * n + i + tx * kk) : make_double2(0.0, 0.0);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {   // A = E_j, B = E_j^H: the lane's operands are e and conj(e)
-                    const d2 av = ev[u];
-                    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, av.x, cr, 0, 0, 0);
-                    cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, -av.y, cr, 0, 0, 0);
-                    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, -av.y, ci, 0, 0, 0);
-                    ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, av.x, ci, 0, 0, 0);
-                }
-            }
-            d2* part = L1;   // [4][16][16] partial tiles (exactly the L1 tile's 32 x 33 budget)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
-                part[w * 256 + ((lane >> 4) + 4 * rr) * 16 + (lane & 15)] = make_double2(cr[rr], ci[rr]);
-            __syncthreads();
-            for (int e = t; e < TXMAX * TXMAX; e += nt) {   // H (zero padded), waves summed in order
-                const int i = e >> 5, c = e & 31;
-                d2 h = make_double2(0.0, 0.0);
-                if (i < 16 && c < 16)
-#pragma unroll
-                    for (int ww = 0; ww < 4; ++ww) h = cadd(h, part[ww * 256 + i * 16 + c]);
-                L0[i * HS + c] = h;
-            }
-            __syncthreads();
-        } else {
-            fetchE(0, eb);
-            for (int j = 0; j < r; ++j) {
-                putE(eb);
-                if (j + 1 < r) fetchE(j + 1, eb);
-                __syncthreads();
-                mm32_acc<false, true>(L0, L0, cr, ci, lane, w);  // H += E_j E_j^H  (:428)
-                __syncthreads();
-            }
-            store32(L0, cr, ci, lane, w);
-        }
-#ifdef ACE_DEBUG_TK
-        zt[1] = __builtin_amdgcn_s_memrealtime();
-#endif
         const bool warm = (!INIT) && a.warm && a.Q;
         d2* Qg = a.Q ? reinterpret_cast<d2*>(a.Q) + (long long)b * tx * tx : nullptr;
-        for (int e = t; e < TXMAX * TXMAX; e += nt) {
-            const int i = e >> 5, c = e & 31;
-            d2 q = make_double2(i == c ? 1.0 : 0.0, 0.0);
-            if (warm && i < tx && c < tx) q = Qg[i * tx + c];
-            L1[i * HS + c] = q;
-        }
-        __syncthreads();
-        if (warm) {  // H <- Q^H H Q: nearly diagonal when Q is last iteration's eigenbasis
-            mm32<false, false>(L0, L1, cr, ci, lane, w);  // T = H Q
-            __syncthreads();
-            store32(L0, cr, ci, lane, w);
-            __syncthreads();
-            mm32<true, false>(L1, L0, cr, ci, lane, w);   // Q^H T
-            __syncthreads();
-            store32(L0, cr, ci, lane, w);
-            __syncthreads();
-            for (int e = t; e < TXMAX * TXMAX; e += nt) {  // exact Hermitian symmetry
-                const int rr = e >> 5, c = e & 31;
-                if (rr < c) {
-                    const d2 u = L0[rr * HS + c], l = L0[c * HS + rr];
-                    const d2 h = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
-                    L0[rr * HS + c] = h;
-                    L0[c * HS + rr] = make_double2(h.x, -h.y);
-                } else if (rr == c) {
-                    L0[rr * HS + c].y = 0.0;
+        // H = E E^H into L0 (the warm frame Q^H H Q when warm), L1 = Q (or I): the Jacobi eigensolver's operands
+        auto form_h = [&]() {
+            cr = d4v{0.0, 0.0, 0.0, 0.0};
+            ci = d4v{0.0, 0.0, 0.0, 0.0};
+            // tx, rx <= 16 (the driver's 16 x 16 arrays): E E^H is one 16 x 16 tile, so each wave
+            // accumulates the blocks j = w, w + 4, ... straight from memory (16 MFMAs per block, no
+            // LDS staging or barrier per block) and the four partial tiles are summed in LDS.
+            if (small) {
+                for (int j = w; j < r; j += 4) {
+                    d2 ev[4];
+    #pragma unroll
+                    for (int u = 0; u < 4; ++u) {   // lane: E_j[l & 15][4u + (l >> 4)]
+                        const int i = lane & 15, kk = 4 * u + (lane >> 4);
+                        ev[u] = (i < tx && kk < rx) ? evalE(j * n + i + tx * kk) : make_double2(0.0, 0.0);
+                    }
+    #pragma unroll
+                    for (int u = 0; u < 4; ++u) {   // A = E_j, B = E_j^H: the lane's operands are e and conj(e)
+                        const d2 av = ev[u];
+                        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, av.x, cr, 0, 0, 0);
+                        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, -av.y, cr, 0, 0, 0);
+                        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, -av.y, ci, 0, 0, 0);
+                        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, av.x, ci, 0, 0, 0);
+                    }
                 }
+                d2* part = L1;   // [4][16][16] partial tiles (exactly the L1 tile's 32 x 33 budget)
+    #pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    part[w * 256 + ((lane >> 4) + 4 * rr) * 16 + (lane & 15)] = make_double2(cr[rr], ci[rr]);
+                __syncthreads();
+                for (int e = t; e < TXMAX * TXMAX; e += nt) {   // H (zero padded), waves summed in order
+                    const int i = e >> 5, c = e & 31;
+                    d2 h = make_double2(0.0, 0.0);
+                    if (i < 16 && c < 16)
+    #pragma unroll
+                        for (int ww = 0; ww < 4; ++ww) h = cadd(h, part[ww * 256 + i * 16 + c]);
+                    L0[i * HS + c] = h;
+                }
+                __syncthreads();
+            } else {
+                fetchE(0, eb);
+                for (int j = 0; j < r; ++j) {
+                    putE(eb);
+                    if (j + 1 < r) fetchE(j + 1, eb);
+                    __syncthreads();
+                    mm32_acc<false, true>(L0, L0, cr, ci, lane, w);  // H += E_j E_j^H  (:428)
+                    __syncthreads();
+                }
+                store32(L0, cr, ci, lane, w);
+            }
+            for (int e = t; e < TXMAX * TXMAX; e += nt) {
+                const int i = e >> 5, c = e & 31;
+                d2 q = make_double2(i == c ? 1.0 : 0.0, 0.0);
+                if (warm && i < tx && c < tx) q = Qg[i * tx + c];
+                L1[i * HS + c] = q;
             }
             __syncthreads();
-        }
+            if (warm) {  // H <- Q^H H Q: nearly diagonal when Q is last iteration's eigenbasis
+                mm32<false, false>(L0, L1, cr, ci, lane, w);  // T = H Q
+                __syncthreads();
+                store32(L0, cr, ci, lane, w);
+                __syncthreads();
+                mm32<true, false>(L1, L0, cr, ci, lane, w);   // Q^H T
+                __syncthreads();
+                store32(L0, cr, ci, lane, w);
+                __syncthreads();
+                for (int e = t; e < TXMAX * TXMAX; e += nt) {  // exact Hermitian symmetry
+                    const int rr = e >> 5, c = e & 31;
+                    if (rr < c) {
+                        const d2 u = L0[rr * HS + c], l = L0[c * HS + rr];
+                        const d2 h = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                        L0[rr * HS + c] = h;
+                        L0[c * HS + rr] = make_double2(h.x, -h.y);
+                    } else if (rr == c) {
+                        L0[rr * HS + c].y = 0.0;
+                    }
+                }
+                __syncthreads();
+            }
+        };
+        form_h();
+#ifdef ACE_DEBUG_TK
+        zt[1] = zt[0];
+#endif
         // Ky Fan certificate (the one-wave kernel's): the sum of any r diagonal entries
         // of Q^H H Q (Q unitary: the warm start, or I) is at most the sum of the r largest
         // eigenvalues of H, so if the r_p largest diagonal entries clear f_p * trace with margin for
@@ -300,6 +307,91 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             if (t < TXMAX) scl[t] = 1.0;
             if (t == 0) flag_any = 0;
         } else {
+        // the full profile's top-K eigenpairs by the one-wave tridiagonal reduction (topk_tri) in the cold
+        // iterations (ZArgs::tkeig): wave 0 reduces H (packed into L1), the result R is the eigenbasis in the
+        // warm frame (columns in descending order); a failed check forms H again for the Jacobi eigensolver
+        bool tk = false;
+        int maxr = 0;
+#pragma unroll
+        for (int pi = 0; pi < 4; ++pi) maxr = pi < pf.np ? max(maxr, pf.rl[pi]) : maxr;
+        const int tkK = min(maxr, tx);
+        if (a.tkeig > 0 && (INIT || a.it <= a.tkeig) && maxr <= TK_MAX && tx >= 2) {
+            for (int e = t; e < TXMAX * TXMAX; e += nt) {
+                const int i = e >> 5, c = e & 31;
+                if (i <= c) L1[up_idx(i, c)] = L0[i * HS + c];
+            }
+            __syncthreads();
+            __shared__ int tk_s;
+            double* sd = reinterpret_cast<double*>(L0 + 32);   // topk_tri's scalars: 176 doubles
+            if (w == 0) {
+                const bool ok = topk_tri(L1, L0, sd, sd + 80, sd + 112, sd + 144, tx, tkK, lane, [] {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                });
+                if (lane == 0) {
+                    tk_s = ok;
+                    if (a.tkcnt) atomicAdd(a.tkcnt + (ok ? 0 : 1), 1);
+                }
+            }
+            __syncthreads();
+            tk = tk_s;
+            if (tk && t == 0) {
+                // the rescale (:469-480) on the top-K eigenvalues and the tail as one sum (v = trace - top-K
+                // sum; the one-wave kernel's rule): groups inside the top K their own factor, the tail the
+                // common one
+                const double* thk = sd + 64;
+                double* s2 = wv;
+                double tr = 0.0, top = 0.0;
+                for (int k = 0; k < tx; ++k) tr += fmax(0.0, rs2[k]);
+                for (int k = 0; k < tkK; ++k) {
+                    s2[k] = fmax(0.0, thk[k]);
+                    top += s2[k];
+                }
+                double tail = fmax(0.0, tr - top), stail = 1.0;
+                for (int k = 0; k < TXMAX; ++k) scl[k] = 1.0;
+                #pragma unroll
+                for (int pi = 0; pi < 4; ++pi) {
+                    if (pi >= pf.np) break;
+                    const int rr = pf.rl[pi];
+                    const double f = pf.fl[pi];
+                    double vr = 0.0, v = 0.0;
+                    for (int k = 0; k < tkK; ++k) {
+                        if (k < rr) vr += s2[k];
+                        v += s2[k];
+                    }
+                    v += tail;
+                    if (vr < v * f) {
+                        const double sc = fmin(1.0, vr / (v - vr) * (1.0 / f - 1.0));
+                        for (int k = rr; k < tkK; ++k) {
+                            s2[k] *= sc;
+                            scl[k] *= sc;
+                        }
+                        tail *= sc;
+                        stail *= sc;
+                    }
+                }
+                for (int k = tkK; k < tx; ++k) scl[k] = stail;
+                int any = 0;
+                for (int k = 0; k < tx; ++k) any |= scl[k] < 1.0;
+                flag_any = any;
+            }
+            if (!tk) {
+                form_h();
+            } else if (warm) {   // the eigenbasis Q_prev R
+                __syncthreads();
+                for (int e = t; e < TXMAX * TXMAX; e += nt) {
+                    const int i = e >> 5, c = e & 31;
+                    L0[i * HS + c] = (i < tx && c < tx) ? Qg[i * tx + c] : make_double2(i == c ? 1.0 : 0.0, 0.0);
+                }
+                __syncthreads();
+                mm32<false, false>(L0, L1, cr, ci, lane, w);
+                __syncthreads();
+                store32(L1, cr, ci, lane, w);
+            }
+            __syncthreads();
+        }
+        if (!tk) {
         if (jacobi_eig32(L0, L1, tx, wv, jsh) >= JAC_MAX_SWEEPS && t == 0)
             atomicOr(&st->status, (int)ACE_ST_EIG_NOCONV);
         ascending_positions(wv, tx, ascp);           // LAPACK order of eig (:428)
@@ -338,6 +430,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
             for (int k = 0; k < tx; ++k) any |= scl[k] < 1.0;
             flag_any = any;
         }
+        }   // !tk
         }
         __syncthreads();
 #ifdef ACE_DEBUG_TK

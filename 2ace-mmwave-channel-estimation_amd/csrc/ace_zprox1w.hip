@@ -18,6 +18,7 @@
 // puts consecutive vec(Z) indices on consecutive lanes for coalesced stores.
 #include "ace_common.hpp"
 #include "ace_zcommon.hpp"
+#include "ace_topk.hpp"
 
 namespace ace {
 
@@ -147,7 +148,6 @@ __device__ __forceinline__ void msp_materialise(const ZArgs& a, int b) {
 // Cholesky).  Anything else returns false and the caller runs the full Jacobi eigensolver.
 constexpr int LZ_MAX = 16;   // Lanczos steps before giving up (the Jacobi path then runs)
 
-__device__ __forceinline__ d2 conj_d2(d2 v) { return make_double2(v.x, -v.y); }
 __device__ __forceinline__ double half_sum(double v) {   // sum over lanes 0..31 (both halves hold it)
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -321,282 +321,6 @@ __device__ __forceinline__ bool r1_top(const d2* H, d2* Vb, double* tri, int tx,
         __syncthreads();
     }
     return !bad;
-}
-
-// ---- the full rank profile: the top-K eigenpairs through a tridiagonal reduction ---------------------
-// The tail rescaling (:469-480) scales the sorted eigenvalues by one factor per profile group (1..r_0,
-// r_0+1..r_1, ...) and every eigenvalue past the largest rank K by one common factor, so Z = U diag(sqrt(
-// scale)) U^H E (:482-484) needs the top-K eigenvectors and ANY orthonormal completion of them.  topk_tri
-// reduces the packed H to a real tridiagonal T = Q_h^H H Q_h with LAPACK zhetd2's reflectors (lower form),
-// finds T's K largest eigenvalues by multisection on Sturm counts, their vectors by twisted factorisation
-// (dlar1v), orthonormalises them with a Householder QR whose Q_s also supplies the completion, checks every
-// Ritz residual ||T q_j - theta_j q_j|| <= 2^-44 ||T||, and writes R = Q_h Q_s (columns in descending
-// eigenvalue order) into T0 as a 32 x ZHS tile, theta_j into tk[64 + j].  A failed check (eigenvalues
-// clustered inside the top K, where separate twisted vectors lose orthogonality) returns false with H
-// destroyed: the caller rebuilds it and runs the Jacobi eigensolver.  One wave, O(n^3 / 64) per lane
-// against the Jacobi sweeps' O(sweeps n^3 / 64) with far longer dependency chains.
-// LDS: T0 (both packed buffers), vsh (32 complex), tk (>= 64 + TK_MAX doubles), dd and ee (32 doubles each).
-constexpr int TK_MAX = 16;   // largest profile rank taken this way (32-antenna profile: K = 12)
-constexpr int TK_LD = 65;    // LDS stride (doubles) of the per-eigenvalue vectors (spreads the banks)
-__device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd, double* ee, int n, int K,
-                                         int lane) {
-    const int i = lane & 31, h = lane >> 5;
-    const d2 zero = make_double2(0.0, 0.0);
-    d2* P = T0;              // packed H (up_idx), reduced in place
-    d2* VB = T0 + ZPACK;     // reflector k: v[2..L] at VB[off_k ..] (v[1] = 1), off_k = k (n - 2) - k (k - 1) / 2
-    d2* taus = reinterpret_cast<d2*>(tk);
-    double* th = tk + 64;
-    // ---- tridiagonalisation: step k annihilates H[k+2.., k] (x = H[k+1.., k], the reflector I - tau v v^H)
-    int off = 0;
-    for (int k = 0; k + 1 < n; ++k) {
-        const int L = n - k - 1;
-        const d2 x = i < L ? conj_d2(P[up_idx(k, k + 1 + i)]) : zero;
-        const double xn2 = half_sum(i >= 1 ? cabs2(x) : 0.0);
-        const double ar = __shfl(x.x, 0, 64), ai = __shfl(x.y, 0, 64);
-        d2 tau = zero, sc = zero;
-        double beta = ar;
-        if (xn2 > 0.0 || ai != 0.0) {   // zlarfg
-            beta = -copysign(sqrt(fma(ar, ar, fma(ai, ai, xn2))), ar);
-            tau = make_double2((beta - ar) / beta, -ai / beta);
-            const double dr = ar - beta, den = dr * dr + ai * ai;
-            sc = make_double2(dr / den, -ai / den);   // 1 / (alpha - beta)
-        }
-        const d2 v = i == 0 ? make_double2(1.0, 0.0) : (i < L ? cmul(x, sc) : zero);
-        if (lane == 0) {
-            dd[k] = P[up_idx(k, k)].x;
-            ee[k + 1] = beta;
-            taus[k] = tau;
-        }
-        if (h == 0) {
-            vsh[i] = v;
-            if (i >= 1 && i < L) VB[off + i - 1] = v;
-        }
-        off += L - 1;
-        __syncthreads();
-        if (tau.x != 0.0 || tau.y != 0.0) {
-            // p = tau A v, A = H[k+1.., k+1..]: row i over this half's 16 columns, then the halves combined
-            d2 pa = zero;
-            if (i < L) {
-                const int r = k + 1 + i;
-                for (int j = 16 * h; j < 16 * h + 16 && j < L; ++j) {
-                    const int c = k + 1 + j;
-                    const d2 a = r <= c ? P[up_idx(r, c)] : conj_d2(P[up_idx(c, r)]);
-                    pa = cadd(pa, cmul(a, vsh[j]));
-                }
-            }
-            pa.x += __shfl_xor(pa.x, 32, 64);
-            pa.y += __shfl_xor(pa.y, 32, 64);
-            const d2 p = cmul(tau, pa);
-            // w = p - (tau / 2) (p^H v) v
-            const double pvr = half_sum(p.x * v.x + p.y * v.y), pvi = half_sum(p.x * v.y - p.y * v.x);
-            const d2 al = cscale(cmul(tau, make_double2(pvr, pvi)), -0.5);
-            const d2 w = cadd(p, cmul(al, v));
-            __syncthreads();   // every lane is done with row k (x) and A
-            if (h == 0 && i < L) P[up_idx(k, k + 1 + i)] = w;   // row k is free now: w's scratch
-            __syncthreads();
-            // A -= v w^H + w v^H over the packed upper triangle of the trailing L x L block
-            const int cnt = L * (L + 1) / 2;
-            const float tl = (float)(2 * L + 1);
-            for (int e = lane; e < cnt; e += 64) {
-                // row a: start(a) = a L - a (a - 1) / 2 <= e < start(a + 1)
-                int a = (int)((tl - sqrtf(fmaxf(tl * tl - 8.0f * (float)e, 0.0f))) * 0.5f);
-                a = max(0, min(a, L - 1));
-                while (a > 0 && a * L - a * (a - 1) / 2 > e) --a;
-                while (a + 1 < L && (a + 1) * L - (a + 1) * a / 2 <= e) ++a;
-                const int bc = a + (e - (a * L - a * (a - 1) / 2));
-                const d2 va = vsh[a], vb = vsh[bc];
-                const d2 wa = P[up_idx(k, k + 1 + a)], wb = P[up_idx(k, k + 1 + bc)];
-                const int ix = up_idx(k + 1 + a, k + 1 + bc);
-                d2 nv = csub(P[ix], cadd(cmul(va, conj_d2(wb)), cmul(wa, conj_d2(vb))));
-                if (a == bc) nv.y = 0.0;
-                P[ix] = nv;
-            }
-            __syncthreads();
-        }
-    }
-    if (lane == 0) {
-        dd[n - 1] = P[up_idx(n - 1, n - 1)].x;
-        ee[0] = 0.0;
-    }
-    __syncthreads();
-    // ---- the K largest eigenvalues: G lanes per eigenvalue ej probe G points of its interval per round
-    double glo = INFINITY, ghi = -INFINITY;
-    if (lane < n) {
-        const double r = fabs(ee[lane]) + (lane + 1 < n ? fabs(ee[lane + 1]) : 0.0);
-        glo = dd[lane] - r;
-        ghi = dd[lane] + r;
-    }
-    glo = -wave_max(-glo);
-    ghi = wave_max(ghi);
-    const double scale = fmax(fabs(glo), fabs(ghi));
-    if (!(scale > 1e-200 && scale < 1e200)) return false;
-    const double tiny = 1e-46 * scale, tol = 0x1p-51 * scale;
-    const int G = 64 / K, ej = lane / G, pq = lane - ej * G;
-    const bool act = ej < K;
-    double lo = glo, hi = ghi;
-    for (int round = 0; round < 48; ++round) {
-        if (!__any(act && hi - lo > tol)) break;
-        const double x = lo + (hi - lo) * (double)(pq + 1) / (double)(G + 1);
-        double d = dd[0] - x;
-        if (fabs(d) < tiny) d = -tiny;
-        int neg = d < 0.0;
-        for (int j = 1; j < n; ++j) {
-            const double e = ee[j];
-            d = (dd[j] - x) - e * e * frcp(d);
-            if (fabs(d) < tiny) d = -tiny;
-            neg += d < 0.0;
-        }
-        const int above = n - neg;   // eigenvalues >= x
-        double nlo = above >= ej + 1 ? x : lo, nhi = above <= ej ? x : hi;
-        for (int t = 0; t < G; ++t) {   // combine the eigenvalue's G probes
-            const int src = (ej * G + t) & 63;
-            nlo = fmax(nlo, __shfl(nlo, src, 64));
-            nhi = fmin(nhi, __shfl(nhi, src, 64));
-        }
-        if (act) {
-            lo = nlo;
-            hi = nhi;
-        }
-    }
-    const double thv = 0.5 * (lo + hi);
-    if (act && pq == 0) th[ej] = thv;
-    // ---- their vectors: twisted factorisation at theta (lane ej G), stored over T0 (H is consumed)
-    double* S = reinterpret_cast<double*>(T0);   // vector j at S[j TK_LD ..] (rows 0..31), dm at + 32
-    __syncthreads();
-    if (act && pq == 0) {
-        double* dp = S + ej * TK_LD;
-        double* dm = dp + 32;
-        for (int j = 0; j < n; ++j) {
-            const double d = (dd[j] - thv) - (j > 0 ? ee[j] * ee[j] / dp[j - 1] : 0.0);
-            dp[j] = d == 0.0 ? tiny : d;
-        }
-        for (int j = n - 1; j >= 0; --j) {
-            const double d = (dd[j] - thv) - (j + 1 < n ? ee[j + 1] * ee[j + 1] / dm[j + 1] : 0.0);
-            dm[j] = d == 0.0 ? tiny : d;
-        }
-        int r = 0;
-        double gb = INFINITY;
-        for (int j = 0; j < n; ++j) {
-            const double g = fabs(dp[j] + dm[j] - (dd[j] - thv));
-            if (g < gb) {
-                gb = g;
-                r = j;
-            }
-        }
-        double nrm = 1.0, sv = 1.0;
-        for (int j = r - 1; j >= 0; --j) {
-            sv = -ee[j + 1] * sv / dp[j];
-            dp[j] = sv;
-            nrm += sv * sv;
-        }
-        sv = 1.0;
-        for (int j = r + 1; j < n; ++j) {
-            sv = -ee[j] * sv / dm[j];
-            dp[j] = sv;
-            nrm += sv * sv;
-        }
-        dp[r] = 1.0;
-        const double inv = 1.0 / sqrt(nrm);
-        for (int j = 0; j < 32; ++j) dp[j] = j < n ? dp[j] * inv : 0.0;
-    }
-    __syncthreads();
-    // ---- Householder QR of S = [s_0 .. s_{K-1}]: reflector j in place (u_j = 1 implicit), tau_j at + 32
-    for (int j = 0; j < K; ++j) {
-        double* cj = S + j * TK_LD;
-        const double xv = (i > j && i < n) ? cj[i] : 0.0;
-        const double a0 = cj[j];
-        const double sig = half_sum(xv * xv);
-        double tq = 0.0, iv = 0.0;
-        if (sig > 0.0) {
-            const double bt = -copysign(sqrt(fma(a0, a0, sig)), a0);
-            tq = (bt - a0) / bt;
-            iv = 1.0 / (a0 - bt);
-        }
-        __syncthreads();
-        if (h == 0 && i > j && i < n) cj[i] = xv * iv;
-        if (lane == 0) cj[32] = tq;
-        __syncthreads();
-        if (tq != 0.0) {
-            const double u = i == j ? 1.0 : ((i > j && i < n) ? cj[i] : 0.0);
-            for (int c0 = j + 1; c0 < K; c0 += 2) {   // half h takes column c0 + h
-                const int c = c0 + h;
-                double* cc = S + min(c, K - 1) * TK_LD;
-                const double dot = half_sum(c < K ? u * cc[i] : 0.0);
-                if (c < K && i >= j && i < n) cc[i] -= tq * u * dot;
-            }
-        }
-        __syncthreads();
-    }
-    // ---- Q_s = H_0 .. H_{K-1} I: lane (column i, rows 16 h ..)
-    double q[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) q[t] = (16 * h + t == i) ? 1.0 : 0.0;
-    for (int j = K - 1; j >= 0; --j) {
-        const double* cj = S + j * TK_LD;
-        const double tq = cj[32];
-        double dot = 0.0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int r = 16 * h + t;
-            const double u = r == j ? 1.0 : ((r > j && r < n) ? cj[r] : 0.0);
-            dot += u * q[t];
-        }
-        dot += __shfl_xor(dot, 32, 64);
-        const double td = tq * dot;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int r = 16 * h + t;
-            const double u = r == j ? 1.0 : ((r > j && r < n) ? cj[r] : 0.0);
-            q[t] -= u * td;
-        }
-    }
-    // ---- the Ritz residuals of columns 0..K-1 against T
-    {
-        const double tht = i < K ? th[i] : 0.0;
-        const double nb = __shfl_xor(h ? q[0] : q[15], 32, 64);   // the row across the halves' boundary
-        double r2 = 0.0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int r = 16 * h + t;
-            const double qm = t > 0 ? q[t - 1] : (h ? nb : 0.0);
-            const double qp = t < 15 ? q[t + 1] : (h ? 0.0 : nb);
-            const double rv = (dd[r] - tht) * q[t] + (r > 0 ? ee[r] * qm : 0.0) + (r + 1 < n ? ee[r + 1] * qp : 0.0);
-            r2 += r < n ? rv * rv : 0.0;
-        }
-        r2 += __shfl_xor(r2, 32, 64);
-        const double lim = 0x1p-44 * scale;
-        if (__any(i < K && !(r2 <= lim * lim))) return false;
-    }
-    // ---- R = Q_h Q_s: the tridiagonalisation's reflectors, last first
-    d2 qc[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) qc[t] = make_double2(q[t], 0.0);
-    for (int k = n - 2; k >= 0; --k) {
-        const d2 tau = taus[k];
-        if (tau.x == 0.0 && tau.y == 0.0) continue;
-        const int o = k * (n - 2) - k * (k - 1) / 2;
-        d2 dot = zero;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int r = 16 * h + t;
-            const d2 v = r == k + 1 ? make_double2(1.0, 0.0) : ((r > k + 1 && r < n) ? VB[o + r - k - 2] : zero);
-            dot = cadd(dot, cmulc(v, qc[t]));
-        }
-        dot.x += __shfl_xor(dot.x, 32, 64);
-        dot.y += __shfl_xor(dot.y, 32, 64);
-        const d2 td = cmul(tau, dot);
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const int r = 16 * h + t;
-            const d2 v = r == k + 1 ? make_double2(1.0, 0.0) : ((r > k + 1 && r < n) ? VB[o + r - k - 2] : zero);
-            qc[t] = csub(qc[t], cmul(v, td));
-        }
-    }
-    __syncthreads();   // every lane is done with VB and S
-#pragma unroll
-    for (int t = 0; t < 16; ++t) T0[(16 * h + t) * ZHS + i] = qc[t];
-    __syncthreads();
-    return true;
 }
 
 template <bool INIT>
@@ -1020,7 +744,7 @@ __device__ __forceinline__ void zstep1w_body(const ZArgs& a, int b) {
     const int tkK = min(maxr, tx);
     bool tk = false;
     if (!r1 && a.tkeig > 0 && (INIT || a.it <= a.tkeig) && maxr <= TK_MAX && tkK >= 1 && tx >= 2) {
-        tk = topk_tri(T0, reinterpret_cast<d2*>(RotS), lz_tri, wv, rs2, tx, tkK, lane);
+        tk = topk_tri(T0, reinterpret_cast<d2*>(RotS), lz_tri, wv, rs2, scl, tx, tkK, lane, [] { __syncthreads(); });
         if (lane == 0 && a.tkcnt) atomicAdd(a.tkcnt + (tk ? 0 : 1), 1);   // (diagnostics: uses, fallbacks)
         if (!tk) {
             __syncthreads();

@@ -282,7 +282,7 @@ PMC_KERNEL["refine"] = PMC_KERNEL["unit"]   # the unit on the pipeline's X_max (
 PMC_KERNEL["pipeline"] = {"apply_AH": "i8ah_kernel<false, false>", "apply_A": "i8a_kernel",
                           "apply_K": "i8ah_kernel<true, false>", "apply_G": "zgemm3m_kernel<0, false",
                           "zstep": "zstep_kernel", "ystep": "ystep_r_kernel", "pre": "pre_kernel"}
-PMC_KERNEL["phaselift"] = {"zstep": "hetrd_kernel"}
+PMC_KERNEL["phaselift"] = {"zstep": "hetrd"}   # hetrd_blk_kernel (or hetrd_kernel with ACE_HETRD_BLK=0)
 
 
 def _cpu_model():

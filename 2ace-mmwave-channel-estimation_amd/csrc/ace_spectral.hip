@@ -262,6 +262,184 @@ bool hetrd_lds_ok(int mt) {
     return need <= 64 * 1024 || (attr && need <= HT_MAXDYN);
 }
 
+// Blocked form of the same reduction (LAPACK zhetrd / zlatrd) for PhaseLift's prox (C already in the
+// scratch): the reflectors of a panel of HB_NB columns are generated against the panel-start matrix plus
+// the panel's own rank-2 corrections (V W^H + W V^H held in LDS), so a column's Hermitian product only
+// READS the trailing matrix, and the trailing matrix is written once per panel.  Per panel that is
+// HB_NB + 2 passes over the trailing matrix instead of hetrd_kernel's 2 HB_NB (read + write per step):
+// the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
+// d, e, tau and reflector k in row k of C.
+constexpr int HB_NB = 8;
+size_t hetrd_blk_lds(int mt) { return (size_t)mt * 16 * (2 * HB_NB + 2); }
+__global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (active && !active[b]) return;
+    extern __shared__ double smem[];
+    d2* Vp = reinterpret_cast<d2*>(smem);   // [HB_NB][mt]: the panel's reflectors by absolute row (0 elsewhere)
+    d2* Wp = Vp + HB_NB * mt;               // [HB_NB][mt]: their w
+    d2* v = Wp + HB_NB * mt;                // current reflector, entry i = row k + 1 + i
+    d2* w = v + mt;
+    __shared__ double red[16 * 4 * HB_NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
+    __shared__ d2 part[HT_RB][HT_COLS];
+    __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
+    double* base = scratch + b * lay.stride;
+    d2* C = reinterpret_cast<d2*>(base + lay.C);
+    double* dd = base + lay.dd;
+    double* ee = base + lay.ee;
+    d2* taus = reinterpret_cast<d2*>(base + lay.tau);
+    const int col = t % HT_COLS, rb = t / HT_COLS;
+    auto cj = [](d2 a) { return make_double2(a.x, -a.y); };
+    for (int k0 = 0; k0 + 1 < mt; k0 += HB_NB) {
+        const int nbp = min(HB_NB, mt - 1 - k0);
+        for (int e = t; e < 2 * HB_NB * mt; e += HT_THREADS) Vp[e] = make_double2(0.0, 0.0);
+        __syncthreads();
+        for (int p = 0; p < nbp; ++p) {
+            const int k = k0 + p, L = mt - k - 1;
+            // row k of the current matrix: the panel-start C minus the panel's earlier rank-2 updates
+            double s1[1] = {0.0};
+            for (int i = t; i < L; i += HT_THREADS) {
+                const int c = k + 1 + i;
+                d2 a = C[(long long)k * mt + c];
+                for (int q = 0; q < p; ++q)
+                    a = csub(a, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + c])), cmul(Wp[q * mt + k], cj(Vp[q * mt + c]))));
+                v[i] = cj(a);   // x_i = A[k + 1 + i][k]
+                if (i > 0) s1[0] += cabs2(a);
+            }
+            block_sum<1>(s1, red);
+            if (t == 0) {   // zlarfg
+                const d2 alpha = v[0];
+                const double xn2 = s1[0];
+                d2 tau = make_double2(0.0, 0.0), scal = make_double2(0.0, 0.0);
+                double beta = alpha.x;
+                if (!(xn2 == 0.0 && alpha.y == 0.0)) {
+                    beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn2), alpha.x);
+                    tau = make_double2((beta - alpha.x) / beta, -alpha.y / beta);
+                    const d2 den = make_double2(alpha.x - beta, alpha.y);
+                    const double dn = 1.0 / cabs2(den);
+                    scal = make_double2(den.x * dn, -den.y * dn);
+                }
+                s_tau = tau;
+                s_scal = scal;
+                ee[k] = beta;
+                d2 ckk = C[(long long)k * mt + k];
+                for (int q = 0; q < p; ++q)
+                    ckk = csub(ckk, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + k])), cmul(Wp[q * mt + k], cj(Vp[q * mt + k]))));
+                dd[k] = ckk.x;
+                taus[k] = tau;
+            }
+            __syncthreads();
+            const d2 tau = s_tau;
+            if (tau.x == 0.0 && tau.y == 0.0) continue;   // H = I (uniform): V, W of this column stay 0
+            const d2 scal = s_scal;
+            for (int i = t; i < L; i += HT_THREADS) {
+                const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
+                v[i] = vi;
+                C[(long long)k * mt + k + 1 + i] = vi;   // reflector k kept in row k (for the back transform)
+                Vp[p * mt + k + 1 + i] = vi;
+            }
+            // the panel's corrections to C22 v: s_q = W_q^H v, t_q = V_q^H v (L < 1024: one entry per thread)
+            __syncthreads();
+            for (int q = 0; q < p; ++q) {
+                d2 a = make_double2(0.0, 0.0), c2 = a;
+                for (int i = t; i < L; i += HT_THREADS) {
+                    const int r = k + 1 + i;
+                    a = cadd(a, cmulc(Wp[q * mt + r], v[i]));
+                    c2 = cadd(c2, cmulc(Vp[q * mt + r], v[i]));
+                }
+                const double a0 = wave_sum(a.x), a1 = wave_sum(a.y), c0 = wave_sum(c2.x), c1 = wave_sum(c2.y);
+                if ((t & 63) == 0) {
+                    red[(q * 16 + (t >> 6)) * 4 + 0] = a0;
+                    red[(q * 16 + (t >> 6)) * 4 + 1] = a1;
+                    red[(q * 16 + (t >> 6)) * 4 + 2] = c0;
+                    red[(q * 16 + (t >> 6)) * 4 + 3] = c1;
+                }
+            }
+            __syncthreads();
+            if (t < p) {   // fixed order over the 16 waves
+                double sw0 = 0.0, sw1 = 0.0, sv0 = 0.0, sv1 = 0.0;
+                for (int ww = 0; ww < HT_THREADS / 64; ++ww) {
+                    const double* r4 = red + (t * 16 + ww) * 4;
+                    sw0 += r4[0];
+                    sw1 += r4[1];
+                    sv0 += r4[2];
+                    sv1 += r4[3];
+                }
+                s_cw[t] = make_double2(sw0, sw1);
+                s_cv[t] = make_double2(sv0, sv1);
+            }
+            __syncthreads();
+            // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
+            const long long r0 = (long long)(k + 1) * mt + (k + 1);
+            for (int i0 = 0; i0 < L; i0 += HT_COLS) {
+                const int i = i0 + col;
+                double ar = 0.0, ai = 0.0;
+                if (i < L) {
+                    const d2* cc = C + r0 + i;
+#pragma unroll 4
+                    for (int j = rb; j < L; j += HT_RB) {
+                        const d2 c = cc[(long long)j * mt], vj = v[j];
+                        ar += c.x * vj.x + c.y * vj.y;
+                        ai += c.x * vj.y - c.y * vj.x;
+                    }
+                }
+                part[rb][col] = make_double2(ar, ai);
+                __syncthreads();
+                if (rb == 0 && i < L) {
+                    d2 acc = part[0][col];
+#pragma unroll
+                    for (int q = 1; q < HT_RB; ++q) acc = cadd(acc, part[q][col]);
+                    const int r = k + 1 + i;
+                    for (int q = 0; q < p; ++q)
+                        acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
+                    w[i] = cmul(tau, acc);
+                }
+                __syncthreads();
+            }
+            // w = p - (tau / 2) (p^H v) v
+            double s2[2] = {0.0, 0.0};
+            for (int i = t; i < L; i += HT_THREADS) {
+                const d2 q = cmulc(w[i], v[i]);
+                s2[0] += q.x;
+                s2[1] += q.y;
+            }
+            block_sum<2>(s2, red);
+            const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
+            for (int i = t; i < L; i += HT_THREADS) {
+                const d2 wi = cadd(w[i], cmul(alpha2, v[i]));
+                Wp[p * mt + k + 1 + i] = wi;
+            }
+            __syncthreads();
+        }
+        // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
+        const int kn = k0 + nbp, L2 = mt - kn;
+        for (int i0 = 0; i0 < L2; i0 += HT_COLS) {
+            const int i = i0 + col;
+            if (i >= L2) continue;
+            const int ci = kn + i;
+            d2 vq[HB_NB], wq[HB_NB];
+#pragma unroll
+            for (int q = 0; q < HB_NB; ++q) {
+                vq[q] = cj(Vp[q * mt + ci]);
+                wq[q] = cj(Wp[q * mt + ci]);
+            }
+            for (int j = rb; j < L2; j += HT_RB) {
+                const int rj = kn + j;
+                d2* cp = C + (long long)rj * mt + ci;
+                d2 c = *cp;
+#pragma unroll
+                for (int q = 0; q < HB_NB; ++q)
+                    c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
+                *cp = c;
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        dd[mt - 1] = C[(long long)(mt - 1) * mt + mt - 1].x;
+        ee[mt - 1] = 0.0;
+    }
+}
+
 // Sturm count: number of eigenvalues of the tridiagonal (d, e) below x.
 __device__ __forceinline__ int sturm_count(const double* d, const double* e, int n, double x, double pivmin) {
     int cnt = 0;
@@ -817,8 +995,22 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     const SpecLayout lay(d, kmax);
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 16;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
-                       nullptr, 0);
+    // the blocked reduction (hetrd_blk_kernel) with ACE_HETRD_BLK=1 (pending its GPU validation; read per call)
+    const char* hb = getenv("ACE_HETRD_BLK");
+    const bool blk = hb && hb[0] == '1' && hetrd_blk_lds(d) <= HT_MAXDYN;
+    if (blk) {
+        static const bool battr = [] {
+            const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&hetrd_blk_kernel),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)HT_MAXDYN) == hipSuccess;
+            (void)hipGetLastError();
+            return ok;
+        }();
+        if (!battr && hetrd_blk_lds(d) > 64 * 1024) return ACE_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HT_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
+    } else {
+        hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
+                           nullptr, 0);
+    }
     hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
     if (!wy_path(d, kmax)) {
         const int cv = backxf_chunk(d);

@@ -142,7 +142,7 @@ def test_work_roofline_attaches_class_kernel_traffic(tmp_path, monkeypatch):
     kw, kb, ko = [0.0] * 10, [0.0] * 10, [0.0] * 10
     kt[8], kn[8], kw[8] = 100.0, 10, 1e12        # zstep class: the prox eig
     r, shares = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="phaselift", batch=512)
-    assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "hetrd_kernel"
+    assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "hetrd"
     r, _ = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="pipeline", batch=512)
     assert r["traffic"] is None
 

@@ -1,7 +1,7 @@
 # Round-4 profiles: rocprofv3 kernel statistics and the HBM PMC passes (FETCH_SIZE, WRITE_SIZE, separate
 # runs) per bench workload; the PMC summaries record the profiled batch (_meta) so that bench.py can
 # rescale them to its own line.  Usage on the GPU box: bash tools/gpu/r04_profile.sh <out-dir> <rNN_vNN> <modes...>
-# modes: unit nuclear config5 pipeline phaselift refine
+# modes: unit nuclear config5 pipeline phaselift refine private
 set -o pipefail
 O=gpurun_out/${1:-prof}; R=${2:-r04_v1}; shift 2
 mkdir -p $O
@@ -15,6 +15,7 @@ args() {
     pipeline) echo "--mode pipeline --batch 1024 --steps 1 --warmup 0";;
     phaselift) echo "--mode phaselift --iters 20 --steps 1 --warmup 0";;
     refine) echo "--mode refine --steps 1 --warmup 1 --no-default-profile";;
+    private) echo "--private --steps 1 --warmup 1";;
   esac
 }
 batch() { case $1 in config5) echo 16384;; pipeline) echo 1024;; phaselift) echo 512;; *) echo 4096;; esac; }

@@ -132,6 +132,8 @@ def _load():
     lib.ace_spectral_init_host.restype = C.c_int
     lib.ace_path_counts.argtypes = [C.POINTER(C.c_int64), C.c_int]
     lib.ace_path_counts.restype = C.c_int
+    lib.ace_lds_request.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_size_t)]
+    lib.ace_lds_request.restype = C.c_int
     lib.ace_last_error.argtypes = []
     lib.ace_last_error.restype = C.c_char_p
     lib.ace_version.argtypes = []
@@ -156,6 +158,13 @@ def path_counts(reset=False):
     v = (C.c_int64 * 4)()
     check(LIB.ace_path_counts(v, int(bool(reset))))
     return dict(zip(PATHS, v))
+
+
+def lds_request(kernel: str, m: int) -> int:
+    """Dynamic LDS bytes the launcher of ``kernel`` requests at size m (ace_lds_request; no GPU call)."""
+    v = C.c_size_t()
+    check(LIB.ace_lds_request(kernel.encode(), int(m), C.byref(v)))
+    return v.value
 
 
 def default_cfg(**kw) -> AdmmCfg:

@@ -108,7 +108,8 @@ def _as_rows(t):
 
 def pack_results(fields):
     """Pack per-realisation results {name: tensor [count, ...]} into one uint8 tensor [count, row_bytes]
-    (fields in the given order, each row 8-byte aligned) and the layout needed to unpack it."""
+    (fields in the given order, each field 16-byte aligned in a row of a multiple of 16 bytes) and the layout
+    needed to unpack it."""
     import torch
     rows, layout, off = [], [], 0
     count = None
@@ -120,10 +121,15 @@ def pack_results(fields):
         if t.shape[0] != count:
             raise ValueError(f"field {name!r} has {t.shape[0]} rows, expected {count}")
         r = _as_rows(t)
+        # every field starts 16-byte aligned in the row (unpack views the bytes as the field's dtype)
+        lead = (-off) % 16
+        if lead:
+            rows.append(torch.zeros((count, lead), dtype=torch.uint8, device=r.device))
+            off += lead
         layout.append((name, off, r.shape[1], t.dtype, tuple(t.shape[1:])))
         rows.append(r)
         off += r.shape[1]
-    pad = (-off) % 8
+    pad = (-off) % 16
     if pad:
         rows.append(torch.zeros((count, pad), dtype=torch.uint8, device=rows[0].device))
     return torch.cat(rows, dim=1).contiguous(), layout
@@ -134,7 +140,7 @@ def unpack_results(buf, layout):
     import torch
     out = {}
     for name, off, nb, dtype, shape in layout:
-        cols = buf[:, off:off + nb].contiguous()
+        cols = buf[:, off:off + nb].clone()   # (own storage: the view below needs an aligned offset)
         if dtype.is_complex:
             real = torch.float64 if dtype == torch.complex128 else torch.float32
             v = torch.view_as_complex(cols.view(real).reshape((buf.shape[0],) + shape + (2,)))

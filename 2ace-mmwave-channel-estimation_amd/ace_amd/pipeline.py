@@ -74,6 +74,20 @@ def draw_partitions(rng, m, restarts, cc_frac=0.95, batch=None):
     return np.stack([rng.permutation(m)[:mt] for _ in range(restarts)]).astype(np.int32)
 
 
+PART_MAXTE = 96   # test rows per realisation the per-realisation form takes (csrc/ace_common.hpp PART_MAXTE)
+
+
+def _groups(tr, m):
+    """Realisation groups that share their partitions, when a [batch][restarts][m_t] layout exceeds the
+    per-realisation form's m - m_t <= PART_MAXTE (each group then runs as one shared-layout call), else None."""
+    if tr.ndim != 3 or m - tr.shape[-1] <= PART_MAXTE:
+        return None
+    groups = {}
+    for b in range(tr.shape[0]):
+        groups.setdefault(tr[b].tobytes(), []).append(b)
+    return list(groups.values())
+
+
 def _layout(tr, batch):
     """(contiguous int32 train_idx, ACE_TRAIN_*) of a [restarts][m_t] or [batch][restarts][m_t] array."""
     tr = np.ascontiguousarray(np.asarray(tr, dtype=np.int32))
@@ -98,6 +112,21 @@ def infer_low_rank_pipeline_host(A, B, tx, rx, train_idx, *, variant="A2only", r
         raise ValueError(f"shape mismatch: A{A.shape} B{B.shape}")
     n = A.shape[1]
     tr, layout = _layout(train_idx, batch)
+    grp = _groups(tr, m)
+    if grp is not None and len(grp) > 1:   # (m - m_t > PART_MAXTE: one shared-layout call per group)
+        parts = [(g, infer_low_rank_pipeline_host(A, B[g], tx, rx, tr[g[0]], variant=variant, restarts=restarts, r=r,
+                                                  mu0=mu0, rho=rho, cc_frac=cc_frac, tol_rel=tol_rel,
+                                                  tol_abs=tol_abs, maxiter=maxiter, eig_warm=eig_warm))
+                 for g in grp]
+        p0 = parts[0][1]
+        res = PipelineResult(*(np.empty((batch,) + f.shape[1:], f.dtype) for f in
+                               (p0.X, p0.Y, p0.quality, p0.stage_iters, p0.status)))
+        for g, p in parts:
+            for k in ("X", "Y", "quality", "stage_iters", "status"):
+                getattr(res, k)[g] = getattr(p, k)
+        return res
+    if grp is not None:   # one group: every realisation shares the partitions
+        tr, layout = tr[0], ACE_TRAIN_SHARED
     nres = tr.shape[-2] if restarts is None else int(restarts)
     cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
     if tr.shape[-2] != cfg.restarts:
@@ -174,6 +203,25 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
     batch, m = B.shape
     n = A.shape[1]
     tr, layout = _layout(train_idx, batch)
+    grp = _groups(tr, m)
+    if grp is not None and len(grp) > 1:   # (m - m_t > PART_MAXTE: one shared-layout call per group)
+        kw = dict(variant=variant, restarts=restarts, r=r, mu0=mu0, rho=rho, cc_frac=cc_frac, tol_rel=tol_rel,
+                  tol_abs=tol_abs, maxiter=maxiter, eig_warm=eig_warm, stop_before_refine=stop_before_refine,
+                  workspace=workspace, stream=stream)
+        outs = []
+        for g in grp:
+            gi = torch.as_tensor(g, device=B.device)
+            outs.append((gi, infer_low_rank_pipeline_batch(A, B.index_select(0, gi).contiguous(), tx, rx,
+                                                           tr[g[0]], **kw)))
+        o0 = outs[0][1]
+        res = PipelineResult(*(torch.empty((batch,) + tuple(f.shape[1:]), dtype=f.dtype, device=f.device) for f in
+                               (o0.X, o0.Y, o0.quality, o0.stage_iters, o0.status)))
+        for gi, o in outs:
+            for k in ("X", "Y", "quality", "stage_iters", "status"):
+                getattr(res, k).index_copy_(0, gi, getattr(o, k))
+        return res
+    if grp is not None:   # one group: every realisation shares the partitions
+        tr, layout = tr[0], ACE_TRAIN_SHARED
     nres = tr.shape[-2] if restarts is None else int(restarts)
     cfg = _cfg(variant, nres, r, mu0, rho, cc_frac, tol_rel, tol_abs, maxiter, eig_warm)
     cfg.stop_before_refine = int(bool(stop_before_refine))

@@ -209,6 +209,12 @@ def infer_admm_batch(A, B, X0, tx, rx, *, variant="A2only", scale_by_row=True, u
     ws = (workspace or _DEFAULT_WS).get(nbytes, dev)
     if stream is None:
         stream = torch.cuda.current_stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    if flags is not None and stream != cur:
+        # the flags were built on torch's current stream: the solve's stream waits for them, and their
+        # memory stays reserved for that stream until the solve has read them
+        stream.wait_stream(cur)
+        flags.record_stream(stream)
     check(LIB.ace_admm_solve_batch(C.byref(cfg), batch, m, n, tx, rx, A.data_ptr(), B.data_ptr(), X0.data_ptr(),
                                    out.X.data_ptr(), out.Y.data_ptr(), out.iters.data_ptr(),
                                    out.status.data_ptr(), out.mu.data_ptr(), ws.data_ptr(), ws.numel(),

@@ -145,8 +145,9 @@ static bool msr_trace() {
     }();
     return v;
 }
-static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= 160 * 1024 - 8192; }
-static bool gyf_ok(const Knobs& k, int m) { return k.gyf && gyf_lds_bytes(m) <= (size_t)GYK_MAXDYN; }
+// eligibility of the fused kernels: their dynamic LDS within the kernel's derived budget (lds_dyn_budget)
+static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= i8ah_budget(1); }
+static bool gyf_ok(const Knobs& k, int m) { return k.gyf && gyf_lds_bytes(m) <= gyf_budget(); }
 
 // ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
 static bool i8_disabled() {
@@ -171,7 +172,9 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     double c[2] = {0.0, 0.0};
     ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     ACE_HIP(read_back(c, L.c8, sizeof(double), st));
-    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= 160 * 1024 - 8192;
+    // apply_AH and K Y both hold the digit planes of an m-long operand in LDS
+    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= i8ah_budget(0) &&
+             i8ah_lds_bytes(m) <= i8ah_budget(2);
     if (!L.i8ok) return ACE_OK;
     c[1] = c[0] * c[0];
     ACE_HIP(upload(L.c8 + 1, c + 1, sizeof(double), st));
@@ -179,7 +182,7 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     launch_i8k_expand(m, L.K, L.c8, L.LK8, L.i8flag, st);
     ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     L.i8ok = flag == 0;
-    L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= (size_t)GYK_MAXDYN;
+    L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= gyk_budget();
     return ACE_OK;
 }
 
@@ -269,7 +272,7 @@ static int pc_setup(LinOps& L, int batch, hipStream_t st) {
     ACE_HIP(read_back(&flag, L.pcflag, sizeof(int), st));
     if (flag != 0) return ACE_OK;
     launch_pc_ginv(batch, m, n, L.pcodes, L.pcb, L.K, L.G, st);
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("private setup (code images, G_b)");
     L.pc_ok = true;
     return ACE_OK;
 }
@@ -300,7 +303,7 @@ int linops_setup(LinOps& L, int batch, hipStream_t st) {
         }
         ACE_TRY(i8_setup(L, st));
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("operator setup (K, G, A^H, fragments, digit planes)");
     return ACE_OK;
 }
 
@@ -517,12 +520,13 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 za.rank_one = za0.rank_one ? za0.rank_one + (long long)h * chunk : nullptr;
                 const MsrArgs ma{L.Gf, B + (long long)h * chunk * m, {wh.Y[0], wh.Y[1]}, wh.M, wh.AX,
                                  {wh.Sg[0], wh.Sg[1]}, wh.optS, wh.optY, wh.st, w.done + 8 + h, w.done + 1,
-                                 w.done + 12 + 4 * h, w.done + 40 + h, nb[h], m, it, p.maxiter};
+                                 w.done + 12 + 4 * h, msr_trace() ? w.done + 40 + h : nullptr, nb[h], m, it, p.maxiter};
                 ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 8 + h), p.maxiter, 1, ss[h]));
                 ACE_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.done + 12 + 4 * h), 0, 4, ss[h]));
                 ProfScope ps(ACE_K_MSR, ss[h]);
                 pidx[h] = ps.idx;
                 launch_msr(ma, za, kn.msr_waves, ss[h]);
+                ACE_LAUNCHED("m-space run (msr_kernel)");
             }
             for (int h = 1; h < nsplit; ++h) {   // (the caller's stream waits for the sub-batches)
                 ACE_HIP(hipEventRecord(cev[h], ss[h]));
@@ -601,20 +605,24 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
             } else if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, kn.gyf_ctl, sh);
+                ACE_LAUNCHED("g / Y-step / apply_AH (gyf_kernel)");
             } else {
                 {
                     ProfScope ps(ACE_K_APPLY_G, sh);
                     launch_gyk(nb[h], m, ga, sh);
                 }
+                ACE_LAUNCHED("g / Y-step (gyk_kernel)");
                 ACE_HIP(stagger_mark(h, it, 2));
                 ProfScope ps(ACE_K_APPLY_AH, sh);
                 launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh, za.xfuse ? &za : nullptr);
+                ACE_LAUNCHED("apply_AH (i8ah_kernel)");
             }
             ACE_HIP(stagger_mark(h, it, 3));
             if (pmask & 2) {
                 ProfScope ps(ACE_K_ZSTEP, sh);
                 if (lean && !za.xfuse) launch_zlean(za, nb[h], sh);
                 launch_zstep(p.variant, false, za, nb[h], sh);
+                ACE_LAUNCHED("Z-step");
             }
         }
         if (csync) ACE_TRY(barrier());
@@ -634,7 +642,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
         ACE_HIP(hipEventRecord(ev[h], ss[h]));
         ACE_HIP(hipStreamWaitEvent(st, ev[h], 0));
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("split iterations");
     {
         ProfScope ps(ACE_K_FINAL, st);
         // best iterates still in m-space form (RealState::optsrc 3): opt_X = Z0 + A^H opt_S
@@ -645,7 +653,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
         launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.V, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st, w.Z,
                           w.Z2, w.Y[0], w.Y[1]);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("finalize (split)");
     if (evs) ACE_HIP(hipEventDestroy(evs));
     return rc;
 }
@@ -694,6 +702,7 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
             ProfScope ps(ACE_K_APPLY_G, st);
             launch_nms(batch, m, a, za, false, st);
         }
+        ACE_LAUNCHED("A2nuclear m-space iteration (nms_kernel)");
         q = 1 - q;
         if (!p.fixed_iters && (it % 8 == 0) && it < p.maxiter) {
             int h_done = 0;
@@ -701,7 +710,6 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
             if (h_done >= batch) break;
         }
     }
-    ACE_HIP(hipGetLastError());
     {
         ProfScope ps(ACE_K_FINAL, st);
         // convergence tests the last iteration left pending (lazy dual residual)
@@ -715,7 +723,7 @@ static int admm_nuclear_msp(const LinOps& L, const AdmmParams& p, const AdmmStat
         launch_finalize_r(n, m, 1, 1, batch, w.optX, w.optY, w.optX, w.Y[q], Xo, Yo, iters, status, mu_out, w.st, st,
                           nullptr, nullptr, nullptr, nullptr);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("finalize (A2nuclear m-space)");
     return ACE_OK;
 }
 
@@ -807,7 +815,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.Kf = L.K;
 
     // A2nuclear r = 1 on a shared A: the m-space iteration (ace_nucmsp.hip)
-    const bool nms = L.shared && L.frag_ok && r == 1 && p.variant == ACE_VARIANT_NUCLEAR && kn.nuc_msp;
+    const bool nms = L.shared && L.frag_ok && r == 1 && p.variant == ACE_VARIANT_NUCLEAR && kn.nuc_msp && nms_supported(m);
     // ---- init (:296-310)
     ACE_HIP(hipMemsetAsync(w.done, 0, 256, st));
     ACE_HIP(hipMemsetAsync(w.zeros, 0, 16 * (size_t)n, st));
@@ -822,7 +830,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             if (!pc && !za.lazy_dual) applyMM(L.K, w.Y[0], w.KY[0]); // K*Y (for A'*Y terms; lazy: on demand)
         }
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("init (A X0, init, Z-step)");
     if (nms) return admm_nuclear_msp(L, p, w, za, batch, B, Xo, Yo, iters, status, mu_out, st);
 
     int q = 0;
@@ -858,11 +866,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             const PgkArgs pa{m, n, L.pcodes, L.pcodes + pc_codesA_off(batch, m, n), L.G, L.pcb, B, w.Y[q], w.M,
                              w.Y[1 - q], w.X, w.optY, w.st, w.AX, 2 - q, Zc, Nc, w.zeros};
             launch_pgk(batch, pa, st);
+            ACE_LAUNCHED("private g / Y-step / apply_AH (pgk_kernel)");
         } else if (gyk) {
             // T = (Y - M/mu) - A V is formed inside gyk_kernel (apply_A folded in)
         } else if (i8) {     // T = (Y - M/mu) - A (Z - N/mu), exact digit planes on the int8 matrix cores
             ProfScope ps(ACE_K_APPLY_A, st);
             launch_i8_apply_A(batch, n, m, L.LA8, Zc, Nc, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, gyk ? w.AX : nullptr, st);
+            ACE_LAUNCHED("apply_A (i8a_kernel)");
         } else if (fused) {  // pre_kernel folded into apply_A (V = Z - N/mu, S = Y - M/mu) and apply_AH / ystep
             ProfScope ps(ACE_K_APPLY_A, st, lv * (fl_mn));
             launch_zgemm_fused(true, m, n, batch, L.A, n, w.Z, w.N, n, w.T, w.Y[q], w.M, m, w.st, st);
@@ -874,6 +884,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             if (i8r) {   // T = (Y - M/mu) - A (Z - N/mu) per vector, digit planes
                 ProfScope ps(ACE_K_APPLY_A, st, 0.0, lv * (vb * (2.0 * n + 3.0 * m)), lv * (op_mn));
                 launch_i8_apply_A(nv, n, m, L.LA8, w.Z, w.N, w.Y[q], w.M, w.T, L.c8, w.st, w.zeros, nullptr, st, r);
+                ACE_LAUNCHED("r-column apply_A (i8a_kernel)");
             } else {
                 ProfScope ps(ACE_K_APPLY_A, st, lv * (fl_mn), lv * (vb * (n + 2.0 * m) + shA));
                 applyA(1, w.V, w.T, w.S);   // T = S - A V
@@ -887,6 +898,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                              w.AX, 2 - q, L.LA8, Zc, Nc, w.zeros, n, za.lazy_dual,
                              DualCtl{za.tol_abs, za.tol_rel, za.rho, za.fixed_iters, n, 1, w.done}};
             launch_gyk(batch, m, ga, st);
+            ACE_LAUNCHED("g / Y-step (gyk_kernel)");
         } else if (fused) {  // g = G T with the Y-step in its epilogue
             ProfScope ps(ACE_K_APPLY_G, st, lv * (fl_mm));
             const YsArgs ys{B, w.Y[q], w.M, w.Y[1 - q], w.ypart};
@@ -903,11 +915,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 else launch_ystep_r(row_mode, m, r, batch, w.S, w.g, w.M, B, w.Y[q], w.Y[1 - q], w.st, st, p.part);
             }
         }
+        ACE_LAUNCHED("apply_A / g = G T / Y-step");
         if (!gyk && !pc) {   // K Y
             ProfScope ps(ACE_K_APPLY_K, st, lv * ((i8 || i8r) ? 0.0 : fl_mm), lv * ((i8 && !i8r) ? 0.0 : vb * 2.0 * m + (i8r ? 0.0 : shM)), lv * (i8r ? op_mm : 0.0));
             if (i8) launch_i8_apply_K(batch, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st);
             else if (i8r) launch_i8_apply_K(nv, m, L.LK8, w.Y[1 - q], w.KY[1 - q], L.c8, w.st, st, r);
             else applyMM(L.K, w.Y[1 - q], w.KY[1 - q]);
+            ACE_LAUNCHED((i8 || i8r) ? "K Y (i8ah_kernel<KY>)" : "K Y (zgemm)");
         }
         if (!pc) {
             // X = V + A^H g
@@ -935,6 +949,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 zv.N = w.N;
                 launch_i8_apply_AH(nv, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st, nullptr, &zv);
             } else applyAH(w.g, w.X, w.V);
+            ACE_LAUNCHED((wmode || i8r) ? "apply_AH (i8ah_kernel)" : "apply_AH (zgemm)");
         }
         za.it = it;
         za.wmode = wmode;
@@ -958,6 +973,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             ProfScope ps(ACE_K_ZSTEP, st, lv * (zs_fl), lv * (zs_b));
             if (za.lean && !za.xfuse) launch_zlean(za, batch, st);
             launch_zstep(p.variant, false, za, batch, st);
+            ACE_LAUNCHED("Z-step");
         }
         q = 1 - q;
         if (wmode) {
@@ -971,14 +987,13 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
             lv = (double)(batch - h_done) / batch;
         }
     }
-    ACE_HIP(hipGetLastError());
     {
         ProfScope ps(ACE_K_FINAL, st);
         launch_finalize_r(n, m, r, row_mode ? r : 1, batch, w.optX, w.optY, wmode ? w.V : w.X, w.Y[q], Xo, Yo, iters, status,
                           mu_out, w.st, st, wmode ? w.Z : nullptr, wmode ? w.Z2 : nullptr, (gyk || pc) ? w.Y[0] : nullptr,
                           (gyk || pc) ? w.Y[1] : nullptr);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("finalize");
     return tk_report(kn, w, ACE_OK, st);
 }
 

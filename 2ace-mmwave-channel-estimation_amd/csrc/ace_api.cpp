@@ -4,6 +4,8 @@
 // wrapper, synthetic traces, kernel timing, error text and version.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "ace_host.hpp"
 
@@ -30,10 +32,77 @@ int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
 }
 }  // namespace
 
+namespace ace {
+namespace {
+std::mutex g_lds_mu;
+std::unordered_map<const void*, size_t> g_lds_budget;
+thread_local std::string t_refused;   // the first launch a launcher refused since the last launch_check
+}  // namespace
+
+size_t lds_dyn_budget(const void* kernel) {
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    const auto it = g_lds_budget.find(kernel);
+    if (it != g_lds_budget.end()) return it->second;
+    hipFuncAttributes fa{};
+    size_t budget = 0;
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess && fa.sharedSizeBytes < LDS_PER_CU) {
+        const size_t want = LDS_PER_CU - fa.sharedSizeBytes;
+        if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)want) == hipSuccess)
+            budget = want;
+    }
+    (void)hipGetLastError();   // (a failed query or setter leaves no sticky error behind)
+    g_lds_budget.emplace(kernel, budget);
+    return budget;
+}
+
+void launch_refused(const char* kernel, size_t need, size_t budget) {
+    if (!t_refused.empty()) return;
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s not launched: %zu B of dynamic LDS requested, budget %zu B", kernel, need, budget);
+    t_refused = buf;
+}
+
+bool lds_fits(const void* kernel, const char* name, size_t need) {
+    if (need <= 64 * 1024) return true;   // (the default limit; no attribute needed)
+    const size_t b = lds_dyn_budget(kernel);
+    if (need <= b) return true;
+    launch_refused(name, need, b);
+    return false;
+}
+
+int launch_check(const char* stage, const char* file, int line) {
+    if (!t_refused.empty()) {
+        const std::string why = t_refused;
+        t_refused.clear();
+        (void)hipGetLastError();
+        return fail(ACE_ERR_UNSUPPORTED, "%s: %s (%s:%d)", stage, why.c_str(), file, line);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ACE_ERR_HIP, "%s: launch failed: %s (%s:%d)", stage, hipGetErrorString(e), file, line);
+    return ACE_OK;
+}
+}  // namespace ace
+
 extern "C" {
 
 const char* ace_last_error(void) { return g_err.c_str(); }
 const char* ace_version(void) { return "ace-mi355x 0.1.0 (gfx950)"; }
+
+int ace_lds_request(const char* kernel, int m, size_t* bytes) {
+    g_err.clear();
+    if (!kernel || !bytes || m < 1) return fail(ACE_ERR_ARG, "bad ace_lds_request arguments");
+    const std::string k = kernel;
+    if (k == "i8ah" || k == "i8ah_ky") *bytes = i8ah_lds_bytes(m);
+    else if (k == "i8ah_fuse") *bytes = i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes();
+    else if (k == "gyk") *bytes = gyk_lds_bytes(m);
+    else if (k == "gyf") *bytes = gyf_lds_bytes(m);
+    else if (k == "msr") *bytes = msr_request_bytes();
+    else if (k == "nms") *bytes = nms_lds_bytes(m);
+    else if (k == "hetrd") *bytes = hetrd_request_bytes(m, 0);
+    else if (k == "hetrd_blk") *bytes = hetrd_request_bytes(m, 1);
+    else return fail(ACE_ERR_ARG, "unknown kernel '%s'", kernel);
+    return ACE_OK;
+}
 
 int ace_prof_sample(int stride, uint32_t full_mask) {
     g_err.clear();

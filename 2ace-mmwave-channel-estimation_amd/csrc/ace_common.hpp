@@ -187,6 +187,30 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
     __syncthreads();
 }
 
+// ------------------------------------------------------------------ dynamic LDS budgets (ace_api.cpp)
+// A kernel that takes more dynamic LDS than the 64 KiB default gets its limit raised, once, to the
+// CU's 160 KiB less its own static LDS as the code object reports it (hipFuncGetAttributes::
+// sharedSizeBytes).  The launchers and the eligibility tests of the paths (ace_admm.cpp, the Z-step
+// and spectral launchers) read that one number, so a kernel whose static LDS grows loses the path's
+// eligibility (and says so) instead of failing its launches.  0 when the attribute could not be set
+// (the HIP error is cleared and the kernel keeps the default budget: no launch above 64 KiB).
+constexpr size_t LDS_PER_CU = 160 * 1024;
+size_t lds_dyn_budget(const void* kernel);
+// A launcher whose dynamic LDS exceeds its kernel's budget does not launch and records it here;
+// launch_check (ACE_LAUNCHED, after every stage of a solve) turns that, or a pending HIP launch
+// error, into the solve's error naming the stage and the kernel.
+void launch_refused(const char* kernel, size_t need, size_t budget);
+int launch_check(const char* stage, const char* file, int line);
+#define ACE_LAUNCHED(stage)                                                 \
+    do {                                                                    \
+        const int lc_ = ::ace::launch_check(stage, __FILE__, __LINE__);     \
+        if (lc_) return lc_;                                                \
+    } while (0)
+// true (launch) when need fits the kernel's budget, else records the refusal
+bool lds_fits(const void* kernel, const char* name, size_t need);
+size_t msr_request_bytes();                  // dynamic LDS of msr_kernel
+size_t hetrd_request_bytes(int d, int blk);  // ... of hetrd_kernel (blk = 0) / hetrd_blk_kernel (blk = 1)
+
 // ------------------------------------------------------------------ launchers
 // GEMM (MFMA f64) with a shared complex LHS over a batch of realisation vectors:
 //   C[b][i] = epi( sum_k op(L)[i][k] * V[b][k] )   (complex)
@@ -222,7 +246,7 @@ void launch_i8_expand(int m, int n, const double* A, const double* cmax, int8_t*
 void launch_i8_apply_A(int nb, int n, int m, const int8_t* LA, const double* Z, const double* N, const double* Y,
                        const double* M, double* T, const double* cmax, const RealState* rs, const double* zeros,
                        const double* AX, hipStream_t st, int rcols = 1);
-// W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= 160 KiB
+// W = c A^H g  (the Z-step's wmode forms X = (Z - N/mu) + W); needs i8ah_lds_bytes(m) <= i8ah_budget(0)
 // fuse != nullptr: the steady-state Z-step runs in the epilogue (i8ah_kernel<false, true>)
 struct ZArgs;
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
@@ -230,6 +254,8 @@ void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g
                         const ZArgs* plain = nullptr);
 size_t i8ah_lds_bytes(int kc);
 size_t i8ah_fuse_lds_bytes();
+// dynamic LDS budget (lds_dyn_budget) of i8ah_kernel: kind 0 plain apply_AH, 1 the FUSE form, 2 the K Y form
+size_t i8ah_budget(int kind);
 // opt_X = Z0 + A^H opt_S for the realisations whose best iterate is in m-space form (optsrc 3;
 // Z0 in Zb1 / Zb2 by RealState::z0id), done or not; sets optsrc = 0
 void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* optS, double* optX, const double* cmax,
@@ -239,9 +265,10 @@ void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* o
 // 16-realisation blocks (shared phase-code A, r = 1, m <= GYK_MAXM).  Gf: G in f64 MFMA
 // fragment order (launch_gyk_gfrag at setup).
 constexpr int GYK_MAXM = 256;
-constexpr int GYK_MAXDYN = 160 * 1024 - 8192;   // dynamic LDS limit of gyk_kernel
 size_t gyk_gfrag_bytes(int m);
 size_t gyk_lds_bytes(int m);
+size_t gyk_budget();   // dynamic LDS budgets (lds_dyn_budget) of gyk_kernel, gyf_kernel
+size_t gyf_budget();
 void launch_gyk_gfrag(int m, const double* G, double* Gf, hipStream_t st);
 struct GykArgs {
     const double* Gf;
@@ -389,6 +416,7 @@ struct NmsArgs {
     DualCtl dc;
 };
 size_t nms_lds_bytes(int m);
+bool nms_supported(int m);   // nms_lds_bytes(m) within the kernels' LDS budgets
 // fin: only finish the convergence tests the previous (last) iteration left pending
 void launch_nms(int nb, int m, const NmsArgs& a, const ZArgs& za, bool fin, hipStream_t st);
 void launch_nms_init(int nb, int n, int m, const double* Xi, const NmsArgs& a, hipStream_t st);

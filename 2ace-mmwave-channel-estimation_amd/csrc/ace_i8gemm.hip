@@ -1792,6 +1792,7 @@ __global__ __launch_bounds__(256) void i8k_expand_kernel(int m, const double* __
     put(2 * i + 1, 2 * k + 1, kr);
 }
 }  // namespace
+size_t msr_request_bytes() { return msr_lds_bytes(); }
 
 // padded K-steps (of 32 reals) for a complex inner dimension kc: multiple of one stage
 int i8_nks(int kc) { return (2 * kc + KC - 1) / KC * KSC; }
@@ -1824,15 +1825,12 @@ void launch_i8k_expand(int m, const double* K, const double* cmax, int8_t* LK, i
 }
 void launch_i8_apply_K(int nb, int m, const int8_t* LK, const double* Y, double* KY, const double* cmax,
                        const RealState* rs, hipStream_t st, int rcols) {
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<true, false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512) == hipSuccess;
-    }();
-    (void)attr;
+    const size_t lds = i8ah_lds_bytes(m);
+    if (!lds_fits(reinterpret_cast<const void*>(&i8ah_kernel<true, false>), "i8ah_kernel<KY>", lds)) return;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
     ZArgs za{};
     za.r = rcols;
-    hipLaunchKernelGGL((i8ah_kernel<true, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, m, i8_nks(m),
+    hipLaunchKernelGGL((i8ah_kernel<true, false>), grid, block, lds, st, nb, m, m, i8_nks(m),
                        reinterpret_cast<const i4v*>(LK), Y, KY, cmax + 1, rs, za);
 }
 size_t gyk_gfrag_bytes(int m) { return (size_t)gyk_mp(m) * gyk_mp(m) * 16; }
@@ -1845,15 +1843,9 @@ void launch_gyk_gfrag(int m, const double* G, double* Gf, hipStream_t st) {
     hipLaunchKernelGGL(gyk_gfrag_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, G, Gf);
 }
 void launch_gyk(int nb, int m, const GykArgs& a, hipStream_t st) {
-    static const bool attr = [] {
-        // dynamic + static (the 7 KiB reduction scratch) must fit the 160 KiB of the CU
-        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gyk_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, GYK_MAXDYN) == hipSuccess;
-        (void)hipGetLastError();
-        return ok;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(gyk_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyk_lds_bytes(m), st, nb, m, a);
+    const size_t lds = gyk_lds_bytes(m);
+    if (!lds_fits(reinterpret_cast<const void*>(&gyk_kernel), "gyk_kernel", lds)) return;
+    hipLaunchKernelGGL(gyk_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), lds, st, nb, m, a);
 }
 size_t gyf_lds_bytes(int m) {
     const size_t ts = gyf_ts_bytes(m), ad = gyk_lds_bytes(m) - ts, zs = i8ah_fuse_lds_bytes();
@@ -1861,15 +1853,10 @@ size_t gyf_lds_bytes(int m) {
 }
 void launch_gyf(int nb, int m, int n, const GykArgs& a, const int8_t* LAH, double* W, const ZArgs& za, int ctl,
                 hipStream_t st) {
-    static const bool attr = [] {
-        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&gyf_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, GYK_MAXDYN) == hipSuccess;
-        (void)hipGetLastError();
-        return ok;
-    }();
-    (void)attr;
+    const size_t lds = gyf_lds_bytes(m);
+    if (!lds_fits(reinterpret_cast<const void*>(&gyf_kernel), "gyf_kernel", lds)) return;
     const size_t ad = gyk_lds_bytes(m) - gyf_ts_bytes(m);
-    hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), gyf_lds_bytes(m), st, nb, m, n, a,
+    hipLaunchKernelGGL(gyf_kernel, dim3((nb + GRB - 1) / GRB), dim3(NT), lds, st, nb, m, n, a,
                        reinterpret_cast<const i4v*>(LAH), W, za, ad, ctl);
 }
 // live realisations of [0, nb) that an m-space run starting at `it` could not take: not in the
@@ -1900,19 +1887,14 @@ void launch_msr_ready(int nb, const RealState* rs, int it, int* notready, hipStr
 void launch_msr(const MsrArgs& a, const ZArgs& za, int waves, hipStream_t st) {
     // waves = 4: four waves of four output tiles (one per SIMD, 256 VGPRs + 256 AGPRs) instead of
     // eight of two; measured 44 against 40 us per iteration (the 8-wave G T overlaps its waves)
-    static const bool attr = [] {
-        bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel<2>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
-        ok = ok && hipFuncSetAttribute(reinterpret_cast<const void*>(&msr_kernel<4>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)msr_lds_bytes()) == hipSuccess;
-        (void)hipGetLastError();
-        return ok;
-    }();
-    (void)attr;
-    if (waves == 8)
-        hipLaunchKernelGGL(msr_kernel<2>, dim3((a.nb + GRB - 1) / GRB), dim3(512), msr_lds_bytes(), st, a, za);
-    else
-        hipLaunchKernelGGL(msr_kernel<4>, dim3((a.nb + GRB - 1) / GRB), dim3(256), msr_lds_bytes(), st, a, za);
+    const size_t lds = msr_lds_bytes();
+    if (waves == 8) {
+        if (!lds_fits(reinterpret_cast<const void*>(&msr_kernel<2>), "msr_kernel<2>", lds)) return;
+        hipLaunchKernelGGL(msr_kernel<2>, dim3((a.nb + GRB - 1) / GRB), dim3(512), lds, st, a, za);
+    } else {
+        if (!lds_fits(reinterpret_cast<const void*>(&msr_kernel<4>), "msr_kernel<4>", lds)) return;
+        hipLaunchKernelGGL(msr_kernel<4>, dim3((a.nb + GRB - 1) / GRB), dim3(256), lds, st, a, za);
+    }
 }
 // best m-space iterates still in an S ping-pong buffer (optsrc 4 / 5) -> opt_S (optsrc 3)
 __global__ __launch_bounds__(256) void msp_opt_gather_kernel(int m, RealState* rs, const double* S0, const double* S1,
@@ -1937,24 +1919,27 @@ void launch_i8_msp_optx(int nb, int m, int n, const int8_t* LAH, const double* o
 }
 void launch_i8_apply_AH(int nb, int m, int n, const int8_t* LAH, const double* g, double* W, const double* cmax,
                         const RealState* rs, hipStream_t st, const ZArgs* fuse, const ZArgs* plain) {
-    static const bool attr = [] {   // dynamic LDS beyond the 64 KiB default
-        // dynamic + static (FUSE: 7.3 KiB of per-realisation state and partial sums) <= 160 KiB
-        const bool a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false, false>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192) == hipSuccess;
-        const bool a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&i8ah_kernel<false, true>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8192) == hipSuccess;
-        (void)hipGetLastError();
-        return a0 && a1;
-    }();
-    (void)attr;
     dim3 grid((nb + RB - 1) / RB, 1, 1), block(NT);
-    if (fuse)
-        hipLaunchKernelGGL((i8ah_kernel<false, true>), grid, block, i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes(), st, nb,
-                           m, n, i8_nks(m),
+    if (fuse) {
+        const size_t lds = i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes();
+        if (!lds_fits(reinterpret_cast<const void*>(&i8ah_kernel<false, true>), "i8ah_kernel<FUSE>", lds)) return;
+        hipLaunchKernelGGL((i8ah_kernel<false, true>), grid, block, lds, st, nb, m, n, i8_nks(m),
                            reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, *fuse);
-    else
-        hipLaunchKernelGGL((i8ah_kernel<false, false>), grid, block, i8ah_lds_bytes(m), st, nb, m, n, i8_nks(m),
+    } else {
+        const size_t lds = i8ah_lds_bytes(m);
+        if (!lds_fits(reinterpret_cast<const void*>(&i8ah_kernel<false, false>), "i8ah_kernel", lds)) return;
+        hipLaunchKernelGGL((i8ah_kernel<false, false>), grid, block, lds, st, nb, m, n, i8_nks(m),
                            reinterpret_cast<const i4v*>(LAH), g, W, cmax, rs, plain ? *plain : ZArgs{});
+    }
 }
+// dynamic LDS budgets of the i8 / fused kernels (lds_dyn_budget), for the eligibility tests of ace_admm.cpp
+size_t i8ah_budget(int kind) {
+    const void* k = kind == 1 ? reinterpret_cast<const void*>(&i8ah_kernel<false, true>)
+                  : kind == 2 ? reinterpret_cast<const void*>(&i8ah_kernel<true, false>)
+                              : reinterpret_cast<const void*>(&i8ah_kernel<false, false>);
+    return lds_dyn_budget(k);
+}
+size_t gyk_budget() { return lds_dyn_budget(reinterpret_cast<const void*>(&gyk_kernel)); }
+size_t gyf_budget() { return lds_dyn_budget(reinterpret_cast<const void*>(&gyf_kernel)); }
 
 }  // namespace ace

@@ -368,18 +368,19 @@ __global__ __launch_bounds__(256) void nms_out_kernel(int n, int m, const double
 size_t nms_lds_bytes(int m) { return (size_t)GRB * (nms_mp(m) + 1) * sizeof(d2); }
 
 void launch_nms(int nb, int m, const NmsArgs& a, const ZArgs& za, bool fin, hipStream_t st) {
-    static const bool attr = [] {
-        const bool a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_kernel<false>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
-        const bool a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_kernel<true>),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
-        (void)hipGetLastError();
-        return a0 && a1;
-    }();
-    (void)attr;
+    const size_t lds = nms_lds_bytes(m);
     const dim3 grid((nb + GRB - 1) / GRB);
-    if (fin) hipLaunchKernelGGL(nms_kernel<true>, grid, dim3(NT), nms_lds_bytes(m), st, nb, m, a, za);
-    else hipLaunchKernelGGL(nms_kernel<false>, grid, dim3(NT), nms_lds_bytes(m), st, nb, m, a, za);
+    if (fin) {
+        if (lds_fits(reinterpret_cast<const void*>(&nms_kernel<true>), "nms_kernel<fin>", lds))
+            hipLaunchKernelGGL(nms_kernel<true>, grid, dim3(NT), lds, st, nb, m, a, za);
+    } else if (lds_fits(reinterpret_cast<const void*>(&nms_kernel<false>), "nms_kernel", lds)) {
+        hipLaunchKernelGGL(nms_kernel<false>, grid, dim3(NT), lds, st, nb, m, a, za);
+    }
+}
+bool nms_supported(int m) {
+    const size_t lds = nms_lds_bytes(m);
+    return lds <= 64 * 1024 || (lds <= lds_dyn_budget(reinterpret_cast<const void*>(&nms_kernel<true>)) &&
+                                lds <= lds_dyn_budget(reinterpret_cast<const void*>(&nms_kernel<false>)));
 }
 void launch_nms_init(int nb, int n, int m, const double* Xi, const NmsArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(nms_init_kernel, dim3(nb), dim3(256), 0, st, n, m, Xi, a);

@@ -147,12 +147,15 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
     ACE_HIP(hipMemsetAsync(a.cnt, 0, 256, st));
     if (status) ACE_HIP(hipMemsetAsync(status, 0, 4 * (size_t)batch, st));
     launch_pl_init(a, st);
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("PhaseLift init");
 
     auto applyA = [&](const double* X, double* out) {  // out = A(X) = diag(R^H X R), active rows only
         launch_zgemm(0, false, m, d, batch * d, w.RT, d, 0, X, d, 0, w.T, nullptr, m, 0, 1, st);
         launch_pl_diagform(d, m, batch, a.R, w.T, out, a.act, st);
     };
+    // ACE_HETRD_BLK=1: the prox's panel-blocked tridiagonalisation (hetrd_blk_kernel), read once per solve
+    const char* hb = getenv("ACE_HETRD_BLK");
+    const int blk = hb && hb[0] == '1';
     int h[8];
     for (int outer = 0; outer < cfg->maxIts + 1; ++outer) {
         launch_pl_outer_begin(a, st);
@@ -179,7 +182,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             {
                 ProfScope ps(ACE_K_ZSTEP, st, 17.3 * dd3 * act);   // prox_trace: eig of z_old - step g_y, shrink
                 launch_pl_prox_in(a, st);
-                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st));
+                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st, blk));
                 launch_pl_assemble(a, st);
             }
             {
@@ -199,7 +202,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
                 }
                 launch_pl_backtrack(a, st);
             }
-            ACE_HIP(hipGetLastError());
+            ACE_LAUNCHED("PhaseLift inner iteration");
         }
         launch_pl_iterate(a, st);   // tfocs_iterate.m: stopping tests, restart
         int ndone = 0;
@@ -211,13 +214,13 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
         ProfScope ps(ACE_K_FINAL, st);
         const HeevLayout h1 = heev_layout(d, 1);
         launch_pl_final_in(d, batch, a.x, a.scratch, h1, st);
-        ACE_TRY(launch_heev(d, 1, batch, nullptr, a.scratch, a.V, (int*)status, nullptr, st));
+        ACE_TRY(launch_heev(d, 1, batch, nullptr, a.scratch, a.V, (int*)status, nullptr, st, blk));
         launch_pl_final_vec(d, batch, D.reduced, a.R, a.V, a.scratch, h1, D.reduced ? w.wfin : sig, st);
         if (D.reduced)   // sig = Phi^H w,  w = R^{-1} sig_d
             launch_zgemm(0, false, n, m, batch, w.AH, m, 0, w.wfin, m, 0, sig, nullptr, n, 0, 1, st);
         launch_pl_outputs(batch, a.st, iters, status, st);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("PhaseLift final eigenvector");
     return ACE_OK;
 }
 

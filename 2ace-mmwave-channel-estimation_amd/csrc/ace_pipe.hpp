@@ -72,7 +72,8 @@ struct HeevLayout {
 };
 HeevLayout heev_layout(int d, int kmax);
 size_t heev_scratch_bytes(int d, int kmax, int batch);
+// blk = 1: the panel-blocked reduction (hetrd_blk_kernel) instead of hetrd_kernel
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st);
+                const int* active, hipStream_t st, int blk = 0);
 
 }  // namespace ace

@@ -201,7 +201,7 @@ int run_impl(const PipeDims& d, RestartWs& w, const LinOps& L, const PartRows* p
     ACE_TRY(admm_run(L, p, w.sr, nb, Bt, w.X1, X2, Y2, w.iters, (uint32_t*)w.stat, nullptr, st));
     launch_put_col(nb, w.iters, idx, stage_dev, ld, col + 1, 0, st);
     launch_put_col(nb, w.stat, idx, w.status_dev, 1, 0, kStageBits, st);
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("r-column stage");
     return ACE_OK;
 }
 
@@ -232,7 +232,7 @@ int run_restart(int i, const PipeDims& d, const double* A, const double* anorm, 
             launch_zgemm(0, false, n, d.mt, batch * d.r, w.Lt.AH, d.mt, 0, w.W, d.mt, 0, w.Xs, nullptr, n, 0, 1, st);
         }
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("spectral initialisation");
     // ---- :65-68 impl (use_rank_one = false) and test quality
     AdmmParams p = base;
     p.use_rank_one = 0;
@@ -262,7 +262,7 @@ int run_restart(int i, const PipeDims& d, const double* A, const double* anorm, 
         launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
         launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("restart selection");
     return ACE_OK;
 }
 
@@ -292,7 +292,7 @@ int run_restart_part(int i, const PipeDims& d, const LinOps& Lf, const double* A
             launch_zgemm(0, false, n, m, batch * d.r, Lf.AH, m, 0, w.Wm, m, 0, w.Xs, nullptr, n, 0, 1, st);
         }
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("spectral initialisation (per-realisation partitions)");
     // ---- :65-68 impl (use_rank_one = false) and test quality
     AdmmParams p = base;
     p.use_rank_one = 0;
@@ -328,7 +328,7 @@ int run_restart_part(int i, const PipeDims& d, const LinOps& Lf, const double* A
         launch_move_rows(nf, 2LL * d.mt, w.Y2_s, w.Y2, w.idx_sub, true, st);
         launch_move_rows(nf, 1, w.q_s, w.q, w.idx_sub, true, st);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("restart selection (per-realisation partitions)");
     return ACE_OK;
 }
 
@@ -447,7 +447,7 @@ int ace_spectral_init_host(int batch, int m, int n, int r, const double* A, cons
             return fail(ACE_ERR_UNSUPPORTED, "spectral initialisation: m = %d too large", m);
         launch_zgemm(0, false, n, m, batch * r, dAH, m, 0, dW, m, 0, dX, nullptr, n, 0, 1, st);
     }
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("nuclear spectral initialisation");
     ACE_HIP(read_back(X, dX, nX, st));
     if (status) ACE_HIP(read_back(status, dst, 4 * (size_t)batch, st));
     return ACE_OK;
@@ -498,6 +498,10 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     if (!A || !B || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
     if (cfg->train_layout != ACE_TRAIN_SHARED && cfg->train_layout != ACE_TRAIN_PER_REALISATION)
         return fail(ACE_ERR_ARG, "unknown train_layout %d", cfg->train_layout);
+    // the build's draws are per realisation: ace_pipeline_workspace_size sizes that form only for that layout
+    if (!train_idx && cfg->train_layout != ACE_TRAIN_PER_REALISATION)
+        return fail(ACE_ERR_ARG, "train_idx = NULL (the build's per-realisation draws) needs train_layout = "
+                                 "ACE_TRAIN_PER_REALISATION");
     // partitions (host): train rows in sampled order, test rows = sorted complement (:48-49)
     Partitions P;
     ACE_TRY(build_partitions(cfg, d, train_idx, &P));
@@ -555,7 +559,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         ACE_HIP(hipMemcpyAsync(w.qlast, rw.q, 8 * (size_t)batch, hipMemcpyDeviceToDevice, st));
         ACE_HIP(hipMemcpyAsync(w.rank_one, rw.rank_one, batch, hipMemcpyDeviceToDevice, st));
         launch_put_col(batch, rw.status_dev, nullptr, w.status_dev, 1, 0, ~0u, st);
-        ACE_HIP(hipGetLastError());
+        ACE_LAUNCHED("refinement");
         return ACE_OK;
     };
     if (w.nrw == 1 || g_prof.on) {   // one after another (the kernel timer is not thread-safe)
@@ -632,7 +636,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
         if (stage_iters)
             ACE_HIP(hipMemcpyAsync(stage_iters, w.stage_dev, 4 * (size_t)batch * ld, hipMemcpyDeviceToDevice, st));
         if (status) ACE_HIP(hipMemcpyAsync(status, w.status_dev, 4 * (size_t)batch, hipMemcpyDeviceToDevice, st));
-        ACE_HIP(hipGetLastError());
+        ACE_LAUNCHED("pipeline outputs");
         return ACE_OK;
     }
     // ---- :89-101 refinement on the full A, r = 1, the last restart's use_rank_one
@@ -654,7 +658,7 @@ int ace_pipeline_solve_batch(const ace_pipeline_cfg* cfg, int batch, int m, int 
     if (stage_iters)
         ACE_HIP(hipMemcpyAsync(stage_iters, w.stage_dev, 4 * (size_t)batch * ld, hipMemcpyDeviceToDevice, st));
     if (status) ACE_HIP(hipMemcpyAsync(status, w.status_dev, 4 * (size_t)batch, hipMemcpyDeviceToDevice, st));
-    ACE_HIP(hipGetLastError());
+    ACE_LAUNCHED("pipeline outputs");
     return ACE_OK;
 }
 

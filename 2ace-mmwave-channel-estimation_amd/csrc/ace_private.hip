@@ -881,11 +881,7 @@ void launch_pc_pack(int batch, int m, int n, const double* A, double* cb, uint32
     uint32_t* cH = codes;
     uint32_t* cA = cH + (size_t)batch * d.nctH * d.nkgH * 128;
     uint32_t* cR = cA + (size_t)batch * d.nctA * d.nkgA * 128;
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_pack_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
-    }();
-    (void)attr;
+    if (!lds_fits(reinterpret_cast<const void*>(&pc_pack_kernel), "pc_pack_kernel", (size_t)32 * 16 * d.nksA)) return;
     hipLaunchKernelGGL(pc_pack_kernel, dim3(batch, d.nb32), dim3(PNT), (size_t)32 * 16 * d.nksA, st, m, n, A, cb, cH,
                        cA, cR, flag);
 }
@@ -969,21 +965,14 @@ void launch_pc_apply_a(int batch, int m, int n, const uint32_t* codesA, const do
                        hipStream_t st) {
     const PcDims d = pc_dims(m, n);
     const size_t lds = ((16 * (size_t)d.mp + 15) & ~(size_t)15) + 8 * (size_t)(32 * d.nksA + 16);
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_apply_a_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
-    }();
-    (void)attr;
+    if (!lds_fits(reinterpret_cast<const void*>(&pc_apply_a_kernel), "pc_apply_a_kernel", lds)) return;
     hipLaunchKernelGGL(pc_apply_a_kernel, dim3(batch), dim3(PNT), lds, st, m, n, codesA, cb, X0, P0);
 }
 
 void launch_pgk(int batch, const PgkArgs& a, hipStream_t st) {
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pgk_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(pgk_kernel, dim3(batch), dim3(PNT), (size_t)pgk_lds(a.m, a.n).total, st, a);
+    const size_t lds = (size_t)pgk_lds(a.m, a.n).total;
+    if (!lds_fits(reinterpret_cast<const void*>(&pgk_kernel), "pgk_kernel", lds)) return;
+    hipLaunchKernelGGL(pgk_kernel, dim3(batch), dim3(PNT), lds, st, a);
 }
 
 }  // namespace ace

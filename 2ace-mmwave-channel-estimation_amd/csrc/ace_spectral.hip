@@ -250,16 +250,9 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_kernel(int mt, const double*
     }
 }
 size_t hetrd_lds(int mt) { return (size_t)mt * (4 * 16 + 8); }
-constexpr size_t HT_MAXDYN = 140 * 1024;   // dynamic LDS above the static part (160 KiB per CU)
 bool hetrd_lds_ok(int mt) {
-    static const bool attr = [] {
-        const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&hetrd_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)HT_MAXDYN) == hipSuccess;
-        (void)hipGetLastError();
-        return ok;
-    }();
     const size_t need = hetrd_lds(mt);
-    return need <= 64 * 1024 || (attr && need <= HT_MAXDYN);
+    return need <= 64 * 1024 || need <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_kernel));
 }
 
 // Blocked form of the same reduction (LAPACK zhetrd / zlatrd) for PhaseLift's prox (C already in the
@@ -758,6 +751,8 @@ int backxf_chunk(int mt) {
     return cv < 1 ? 1 : (cv > 16 ? 16 : cv);
 }
 }  // namespace
+// dynamic LDS of hetrd_kernel / hetrd_blk_kernel at order d (ace_lds_request)
+size_t hetrd_request_bytes(int d, int blk) { return blk ? hetrd_blk_lds(d) : hetrd_lds(d); }
 
 namespace {
 // ---- primal form for m_t > n: the n x n Gram As^H As itself (a smaller eigenproblem)
@@ -991,21 +986,14 @@ size_t heev_scratch_bytes(int d, int kmax, int batch) {
 }
 
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st) {
+                const int* active, hipStream_t st, int blk) {
     const SpecLayout lay(d, kmax);
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 16;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
-    // the blocked reduction (hetrd_blk_kernel) with ACE_HETRD_BLK=1 (pending its GPU validation; read per call)
-    const char* hb = getenv("ACE_HETRD_BLK");
-    const bool blk = hb && hb[0] == '1' && hetrd_blk_lds(d) <= HT_MAXDYN;
+    // the blocked reduction (hetrd_blk_kernel): blk = 1 (the caller reads ACE_HETRD_BLK once per solve)
+    if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel), "hetrd_blk_kernel", hetrd_blk_lds(d)))
+        blk = 0;   // (the unblocked reduction takes any d hetrd_lds_ok admits)
     if (blk) {
-        static const bool battr = [] {
-            const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&hetrd_blk_kernel),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)HT_MAXDYN) == hipSuccess;
-            (void)hipGetLastError();
-            return ok;
-        }();
-        if (!battr && hetrd_blk_lds(d) > 64 * 1024) return ACE_ERR_UNSUPPORTED;
         hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HT_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
     } else {
         hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,

@@ -36,6 +36,7 @@ import os
 import pathlib
 import sys
 import time
+import traceback
 
 import numpy as np
 
@@ -1096,16 +1097,31 @@ def main():
     else:
         line = unit_bench(args, args.private, dev, rank, world)
         if not args.private and args.variant == "A2only":
+            # The secondary measurements ride on the headline line; a failure in one of them is reported
+            # in its own field ({"error": ...}, the traceback on stderr) instead of discarding the
+            # headline measurement already taken (round 4 lost its line that way)
+            def leg(fn):
+                try:
+                    return fn()
+                except Exception as e:   # noqa: BLE001
+                    traceback.print_exc()
+                    return {"error": f"{type(e).__name__}: {e}"}
             if not args.no_regime_p:
                 # both codebook regimes, each against its own bound; the headline value is
                 # regime S (one codebook for the batch, as in Vs_M.m:192-194 and main.py's one cb_train per call)
-                lp = unit_bench(args, True, dev, rank, world)
+                def regime_p():
+                    lp = unit_bench(args, True, dev, rank, world)
+                    if rank != 0:
+                        return None
+                    d = {k: lp[k] for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline",
+                                            "kernels_ms", "checks")}
+                    d["codebook"] = lp["config"]["codebook"]
+                    return d
+                rp = leg(regime_p)
                 if rank == 0:
-                    line["regime_P"] = {k: lp[k] for k in ("value", "unit", "ms_per_step", "roofline", "cpu_baseline",
-                                                           "kernels_ms", "checks")}
-                    line["regime_P"]["codebook"] = lp["config"]["codebook"]
+                    line["regime_P"] = rp
             if not args.no_refine_input and world == 1 and args.tx == 32:
-                ri = refine_input_bench(args, dev, rank, world)
+                ri = leg(lambda: refine_input_bench(args, dev, rank, world))
                 if rank == 0:
                     line["refine_input"] = ri
         if rank == 0:

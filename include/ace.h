@@ -144,11 +144,13 @@ int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx
  *   ACE_TRAIN_PER_REALISATION [batch][restarts][m_t], each realisation its own (a Monte-Carlo batch
  *                             of calls, each drawing its own randsample).
  * train_idx = NULL draws per-realisation partitions with the build's counter RNG from
- * ace_pipeline_cfg::train_seed (randperm prefixes, stream b * restarts + restart).  Test rows are the
+ * ace_pipeline_cfg::train_seed (randperm prefixes, stream b * restarts + restart); it needs
+ * train_layout = ACE_TRAIN_PER_REALISATION (ACE_ERR_ARG otherwise: the workspace size follows the layout).  Test rows are the
  * sorted complement (setdiff, :49).  Per-realisation partitions keep the stage state in m-space on the
  * full A (test rows held at zero) and apply (I + K_t)^{-1} through the full (I + K)^{-1} and a
- * per-realisation m_te x m_te block (the Schur identity; m - m_t <= 96); realisations whose partitions
- * coincide for every restart take the shared-A_t path.
+ * per-realisation m_te x m_te block (the Schur identity; m - m_t <= 96, ACE_ERR_UNSUPPORTED beyond: the
+ * Python mirror then solves the groups of realisations that share their partitions one call each);
+ * realisations whose partitions coincide for every restart take the shared-A_t path.
  * Per realisation, stage_iters holds 4*restarts + 1 counts: for each restart the two
  * inferLowRankImpl stages (:258, :270), then the two stages of the rank-one retry (:73-77;
  * 0 when not run), then the refinement (:92/:100) -- the order of the oracle's stage_iters. */
@@ -356,6 +358,13 @@ int ace_prof_work_ex(double* flops, double* bytes, double* int8_ops);
  * A, counts[3] f64 applies on private A.  reset != 0 zeroes the counters after reading them;
  * counts may be NULL.  Tells a caller whether its codebook reached the phase-code path. */
 int ace_path_counts(int64_t* counts, int reset);
+
+/* Dynamic LDS (bytes) the launcher of `kernel` requests at operand size `m` (host arithmetic, no
+ * GPU call): "i8ah" (apply_AH), "i8ah_fuse", "i8ah_ky" (K Y), "gyk", "gyf", "msr", "nms" (m = the
+ * measurement count), "hetrd", "hetrd_blk" (m = the Hermitian order).  With the kernel's static LDS
+ * (compiler resource report) it must stay within the CU's 160 KiB for every shape the path takes;
+ * tests/test_lds_budget.py checks that.  ACE_ERR_ARG for an unknown name. */
+int ace_lds_request(const char* kernel, int m, size_t* bytes);
 
 /* Last error text for this thread ("" if none). */
 const char* ace_last_error(void);

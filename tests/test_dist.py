@@ -209,7 +209,21 @@ def test_pack_roundtrip_single_process():
     it = torch.randint(0, 500, (3, 13), dtype=torch.int32)
     st = torch.randint(0, 255, (3,), dtype=torch.int32)
     buf, layout = pack_results({"X": X, "q": q, "it": it, "st": st})
-    assert buf.dtype == torch.uint8 and buf.shape == (3, 16 * 5 + 8 + 4 * 13 + 4) and buf.shape[1] % 8 == 0
+    # X (80 B), q at 80 (8 B), it at 96 (52 B), st at 160 (4 B), the row padded to 176
+    assert buf.dtype == torch.uint8 and buf.shape == (3, 176) and buf.shape[1] % 16 == 0
+    assert [off for _, off, *_ in layout] == [0, 80, 96, 160]
     out = unpack_results(buf, layout)
     assert torch.equal(out["X"], X) and torch.equal(out["q"], q) and torch.equal(out["it"], it)
     assert torch.equal(out["st"], st)
+
+
+def test_pack_unaligned_fields_single_row():
+    """A float64 / complex field after an odd number of 4-byte entries, one realisation (the gathered
+    column slice is then contiguous with an unaligned storage offset unless pack_results aligns it)."""
+    from ace_amd.dist import pack_results, unpack_results
+    st = torch.tensor([[7, 8, 9]], dtype=torch.int32)
+    q = torch.tensor([1.25], dtype=torch.float64)
+    X = torch.randn(1, 3, dtype=torch.complex128)
+    buf, layout = pack_results({"st": st, "q": q, "X": X})
+    out = unpack_results(buf, layout)
+    assert torch.equal(out["st"], st) and torch.equal(out["q"], q) and torch.equal(out["X"], X)

@@ -117,3 +117,21 @@ def test_phaselift_config4_batch512_invariance(gpu):
         one = phaselift_host(Phi, b[r:r + 1], maxIts=200)
         assert np.array_equal(one.sig[0], full.sig[r]) and one.iters[0] == full.iters[r], r
 
+
+
+def test_phaselift_blocked_tridiagonalisation(gpu, monkeypatch):
+    """The prox eig's blocked Householder reduction (hetrd_blk_kernel, panels of 8 columns, zlatrd;
+    ACE_HETRD_BLK=1) against the unblocked one at config 4's geometry: the same iterations and
+    solutions within 1e-9 at 60 TFOCS iterations (the oracle's own stable horizon), and the blocked
+    path against the oracle (test_phaselift_config4_geometry holds the default path to 1e-8)."""
+    from ace_amd import phaselift_host
+    Phi, b = _problem(19, 32, 256, 4)
+    monkeypatch.setenv("ACE_HETRD_BLK", "0")
+    unb = phaselift_host(Phi, b, maxIts=60)
+    monkeypatch.setenv("ACE_HETRD_BLK", "1")
+    blk = phaselift_host(Phi, b, maxIts=60)
+    assert np.array_equal(blk.iters, unb.iters)
+    for r in range(4):
+        assert O.phase_aligned_rel_err(blk.sig[r], unb.sig[r]) <= 1e-9, r
+    sig, _ = T.my_phaselift_reduced(b[0], Phi, maxIts=60)
+    assert O.phase_aligned_rel_err(blk.sig[0], sig) <= 1e-8

@@ -241,6 +241,46 @@ def test_partitions_drawn_by_the_build(gpu):
     assert np.array_equal(X, ref.X) and np.array_equal(its, ref.stage_iters)
 
 
+def test_null_partitions_need_the_per_realisation_layout(gpu):
+    """train_idx = NULL with the default (shared) layout is an argument error, not a workspace error:
+    ace_pipeline_workspace_size sizes the per-realisation form only for ACE_TRAIN_PER_REALISATION."""
+    import ctypes as C
+    from ace_amd import synth
+    from ace_amd._lib import LIB, pipeline_cfg, ACE_ERR_ARG
+    A, B, _, _ = synth.problem(4159, 0, 3, 64, 16, 16)
+    cfg = pipeline_cfg(0, train_seed=77)
+    X = np.empty((3, 256), np.complex128)
+    Y = np.empty((3, 64), np.complex128)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    rc = LIB.ace_pipeline_solve_host(C.byref(cfg), 3, 64, 256, 16, 16, dp(A[0].view(np.float64)),
+                                     dp(np.ascontiguousarray(B)), None, dp(X.view(np.float64)),
+                                     dp(Y.view(np.float64)), None, None, None)
+    assert rc == ACE_ERR_ARG and b"ACE_TRAIN_PER_REALISATION" in LIB.ace_last_error()
+
+
+def test_partitions_beyond_the_schur_block_run_per_group(gpu):
+    """Per-realisation partitions with m - m_t > 96 test rows (cc_frac 0.5 at m = 256: 128) are beyond the
+    per-realisation form's LDS inverse; the Python mirror then solves each group of realisations that
+    share their partitions as one shared-layout call.  Against one call per realisation (bit-identical:
+    the same calls), with two realisations sharing a partition set (one group of 2)."""
+    from ace_amd import infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, synth, draw_partitions
+    import torch
+    A, B, _, _ = synth.problem(4163, 0, 3, 256, 16, 16)
+    tr = draw_partitions(np.random.default_rng(4163), 256, 3, cc_frac=0.5, batch=3)
+    tr[2] = tr[0]
+    kw = dict(cc_frac=0.5, maxiter=120)
+    full = infer_low_rank_pipeline_host(A[0], B, 16, 16, tr, **kw)
+    for b in range(3):
+        one = infer_low_rank_pipeline_host(A[0], B[b:b + 1], 16, 16, tr[b], **kw)
+        assert np.array_equal(one.stage_iters[0], full.stage_iters[b]), b
+        assert O.phase_aligned_rel_err(full.X[b], one.X[0]) <= 1e-12, b
+    dev = torch.device("cuda:0")
+    bt = infer_low_rank_pipeline_batch(torch.as_tensor(A[0], device=dev), torch.as_tensor(B, device=dev), 16, 16,
+                                       tr, **kw)
+    assert np.array_equal(bt.stage_iters.cpu().numpy(), full.stage_iters)
+    assert max(O.phase_aligned_rel_err(bt.X.cpu().numpy()[b], full.X[b]) for b in range(3)) <= 1e-12
+
+
 @pytest.mark.parametrize("tx,m,fixed", [(32, 256, True), (32, 256, False), (16, 64, False)])
 def test_rank_one_top_eigenpair_matches_jacobi(gpu, monkeypatch, tx, m, fixed):
     """The rank-one profile's Z-step needs only (lambda_1, u_1) (every other eigenvalue takes one scale,

@@ -96,7 +96,6 @@ void linops_carve(Carver& cv, bool shared, int batch, int m, int n, LinOps* L) {
 struct Knobs {
     int zcompact = 0, cold_sync = 0, msp_fail_it = -1, gyf_ctl = 1, msr_start = 56, msr_retry = 8, msr_waves = 8;
     int tkeig = 6;
-    int i8compact = 0;
     bool tk_trace = false;
     bool msr = true;
     bool fuse = true, gyf = true, mspace = true, lazy_dual = true, lean = true, nuc_msp = true, i8r = true, zcert = true;
@@ -130,7 +129,6 @@ static Knobs read_knobs() {
     k.r1lz = on("ACE_R1_LANCZOS");
     k.tkeig = (int)num("ACE_TK_EIG", 6);
     k.tk_trace = num("ACE_TK_TRACE", 0) != 0;
-    k.i8compact = (int)num("ACE_I8_COMPACT", 0);
     k.msr_start = (int)num("ACE_MSR_START", 56);
     k.msr_retry = (int)num("ACE_MSR_RETRY", 8);
     if (k.msr_retry < 1) k.msr_retry = 1;
@@ -802,7 +800,6 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.r1lz = kn.r1lz ? 1 : 0;
     za.tkeig = kn.tkeig > 0 ? kn.tkeig : 0;
     za.tkcnt = w.done + 32;
-    za.i8compact = kn.i8compact ? 1 : 0;
     za.wmode = 0;
     za.Xcur = w.V;     // wmode: X of never-improved realisations (finalize's fallback)
     za.Zn = nullptr;   // in place (init, and every kernel outside wmode)

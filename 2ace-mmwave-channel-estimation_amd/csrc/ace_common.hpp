@@ -489,7 +489,6 @@ struct ZArgs {
     int tkeig;             // one-wave Z-step, full profile: the top-K eigenpairs by tridiagonal reduction (topk_tri,
                            // ace_zprox1w.hip) in the init Z-step and iterations it <= tkeig (0: Jacobi throughout)
     int* tkcnt;            // (diagnostics, nullable) [2]: topk_tri uses, and fallbacks to the Jacobi eigensolver
-    int i8compact;         // i8ah_body: compact the live slots of a block onto the first MFMA row tiles
 };
 // X = V + W with V = Z - N/mu, the one rounding sequence used by every producer of X in wmode
 __device__ __forceinline__ double2 xw(double2 z, double2 n, double2 w, double imu) {

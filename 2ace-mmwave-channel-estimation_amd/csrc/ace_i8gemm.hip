@@ -36,8 +36,6 @@
 #include "ace_i8.hpp"
 #include "ace_zcommon.hpp"
 
-#include <type_traits>
-
 namespace ace {
 
 namespace {
@@ -140,27 +138,6 @@ __device__ __forceinline__ void stage_mma(const int8_t* arow, int rstride, const
     kstep(a0, b.f[0][0], b.f[0][1], acc);
     kstep(a1, b.f[1][0], b.f[1][1], acc);
 }
-// the same on the first NRT row tiles only (i8ah_body's compacted live slots)
-template <int NRT>
-__device__ __forceinline__ void stage_mma_t(const int8_t* arow, int rstride, const BSet& b, i16v (&acc)[4][2]) {
-    i4v a0[NRT], a1[NRT];
-#pragma unroll
-    for (int R = 0; R < NRT; ++R) {
-        a0[R] = *reinterpret_cast<const i4v*>(arow + 32 * R * rstride);
-        a1[R] = *reinterpret_cast<const i4v*>(arow + 32 + 32 * R * rstride);
-    }
-#pragma unroll
-    for (int R = 0; R < NRT; ++R) {
-        acc[R][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[R], b.f[0][0], acc[R][0], 0, 0, 0);
-        acc[R][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[R], b.f[0][1], acc[R][1], 0, 0, 0);
-    }
-#pragma unroll
-    for (int R = 0; R < NRT; ++R) {
-        acc[R][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[R], b.f[1][0], acc[R][0], 0, 0, 0);
-        acc[R][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[R], b.f[1][1], acc[R][1], 0, 0, 0);
-    }
-}
-
 // apply_A:  T = (Y - M/mu) - c A V,  V = Z - N/mu  (K = n complex, outputs m complex).
 constexpr int SKR = SK * 32;       // K reals per stage
 constexpr int RSA = SKR + 16;      // LDS row stride of a stage image (bytes): conflict-free b128 reads
@@ -360,32 +337,6 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     // a block none of whose realisations needs the pass (all settled in m-space, done, or past nb)
     // skips it whole (uniform across the work-group)
     if (!__syncthreads_or(live)) return;
-    // the live slots are compacted to the first MFMA row positions (slot order kept): ceil(live / 4) of
-    // the four 32-row tiles run, so a block with few realisations left outside the m-space form costs
-    // that much less; inv_s maps a position back to its slot
-    // (ZArgs::i8compact, ACE_I8_COMPACT=1: pending its GPU validation the default keeps every slot at its
-    // own position and all four tiles, the arithmetic of the uncompacted sweep)
-    __shared__ int pos_s[RB], inv_s[RB], nl_s;
-    if (cp == 0) pos_s[bl] = live;
-    __syncthreads();
-    if (t == 0) {
-        int k = 0;
-        for (int r = 0; r < RB; ++r) {
-            const int lv = pos_s[r];
-            if (!za.i8compact) {
-                pos_s[r] = r;
-                inv_s[r] = r;
-                continue;
-            }
-            pos_s[r] = lv ? k : -1;
-            if (lv) inv_s[k++] = r;
-        }
-        if (za.i8compact)
-            for (int r = k; r < RB; ++r) inv_s[r] = -1;
-        nl_s = za.i8compact ? k : RB;
-    }
-    __syncthreads();
-    const int mypos = pos_s[bl], nR = (nl_s + 3) >> 2;
     const int zn_id = 1 + (za.it & 1);
     if constexpr (!FUSE && !KY) {
         if (matz && t < RB) z0_s[t] = j0 + t < nb ? rs[j0 + t].z0id : 0;
@@ -463,10 +414,8 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
         const double v[4] = {x0.x, x0.y, x1.x, x1.y};
         uint32_t d[8];
         digits4(v, p2, d);
-        if (mypos >= 0)
 #pragma unroll
-            for (int tt = 0; tt < 8; ++tt)
-                *reinterpret_cast<uint32_t*>(&Ad[lds_row(mypos, tt) * rst + KC * s + 4 * cp]) = d[tt];
+        for (int tt = 0; tt < 8; ++tt) *reinterpret_cast<uint32_t*>(&Ad[lds_row(bl, tt) * rst + KC * s + 4 * cp]) = d[tt];
     }
     __syncthreads();
     STAMP(1);
@@ -501,12 +450,11 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
         for (int R = 0; R < 4; ++R)
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const int pb = 4 * R + 2 * q + (lane >> 5), blo = pb < RB ? inv_s[pb] : -1;
-                const int j = min(j0 + max(blo, 0), nb - 1);
+                const int blo = 4 * R + 2 * q + (lane >> 5), j = min(j0 + blo, nb - 1);
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const int col = min((ct0 + c) * 32 + (lane & 31), 2 * Mc - 1);
-                    zv[R][q][c] = (blo >= 0 && fs_s[blo].el) ? za.Z[(long long)j * 2 * Mc + col] : 0.0;
+                    zv[R][q][c] = fs_s[blo].el ? za.Z[(long long)j * 2 * Mc + col] : 0.0;
                 }
             }
     };
@@ -517,8 +465,8 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
             for (int R = 0; R < 4; ++R)
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const int blo = inv_s[4 * R + 2 * q + h], j = j0 + blo;
-                    if (blo < 0 || j >= nb || !live_s[blo] || col >= ldo) continue;
+                    const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                    if (j >= nb || !live_s[blo] || col >= ldo) continue;
                     i16v cmb;
 #pragma unroll
                     for (int e = 0; e < 16; ++e) cmb[e] = acc[R][0][e] + 128 * acc[R][1][e];
@@ -534,8 +482,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
             for (int R = 0; R < 4; ++R)
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    const int blo = inv_s[4 * R + 2 * q + h], j = j0 + blo;
-                    if (blo < 0) continue;   // (slot past the live ones: its zsum slot is never read)
+                    const int blo = 4 * R + 2 * q + h, j = j0 + blo;
                     const bool el = fs_s[blo].el, kc = fs_s[blo].keep_cur;
                     double p0 = 0.0, p3 = 0.0;
                     if (j < nb && live_s[blo]) {
@@ -568,8 +515,8 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
         for (int R = 0; R < 4; ++R)
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const int blo = inv_s[4 * R + 2 * q + h], j = j0 + blo;
-                if (blo < 0 || j >= nb || !live_s[blo]) continue;
+                const int blo = 4 * R + 2 * q + h, j = j0 + blo;
+                if (j >= nb || !live_s[blo]) continue;
                 const double scb = sc_s[blo];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
@@ -586,63 +533,56 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
 #pragma unroll
         for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
     };
-    // the sweep over the column blocks, on the first NRT row tiles (1, 2 or all 4: the compacted live slots)
-    auto sweep = [&](auto nrc) {
-        constexpr int NRT = decltype(nrc)::value;
-        i16v acc[4][2];
-    #pragma unroll
-        for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
-        BSet bA, bB;
-        bfl(bA, 0);
-        if constexpr (FUSE) {
-            // the last loop step of every block is peeled: its Z loads go out right after the stage's
-            // codebook loads, so no wait before the epilogue's own waits for them (vmcnt retires in
-            // order: a load issued under a branch would make every wait a full drain)
-            double zv[4][2][2];
-            const int per = nks / (2 * SK);
-            for (int cbk = 0; cbk < ncb; ++cbk) {
-                const int f0 = cbk * nks;
-                for (int i = 0; i < per - 1; ++i) {
-                    const int f = f0 + 2 * SK * i;
-                    bfl(bB, f + SK);
-                    __builtin_amdgcn_sched_barrier(0);
-                    stage_mma_t<NRT>(arow + 32 * (f % nks), rst, bA, acc);
-                    __builtin_amdgcn_sched_barrier(0);
-                    bfl(bA, f + 2 * SK);
-                    __builtin_amdgcn_sched_barrier(0);
-                    stage_mma_t<NRT>(arow + 32 * ((f + SK) % nks), rst, bB, acc);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                const int f = f0 + 2 * SK * (per - 1);
+    i16v acc[4][2];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R][0] = acc[R][1] = i16v{};
+    BSet bA, bB;
+    bfl(bA, 0);
+    if constexpr (FUSE) {
+        // the last loop step of every block is peeled: its Z loads go out right after the stage's
+        // codebook loads, so no wait before the epilogue's own waits for them (vmcnt retires in
+        // order: a load issued under a branch would make every wait a full drain)
+        double zv[4][2][2];
+        const int per = nks / (2 * SK);
+        for (int cbk = 0; cbk < ncb; ++cbk) {
+            const int f0 = cbk * nks;
+            for (int i = 0; i < per - 1; ++i) {
+                const int f = f0 + 2 * SK * i;
                 bfl(bB, f + SK);
-                zload(cbk, zv);
                 __builtin_amdgcn_sched_barrier(0);
-                stage_mma_t<NRT>(arow + 32 * (f % nks), rst, bA, acc);
+                stage_mma(arow + 32 * (f % nks), rst, bA, acc);
                 __builtin_amdgcn_sched_barrier(0);
                 bfl(bA, f + 2 * SK);
                 __builtin_amdgcn_sched_barrier(0);
-                stage_mma_t<NRT>(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+                stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
                 __builtin_amdgcn_sched_barrier(0);
-                epilogue(cbk, acc, zv);
             }
-        } else {
-            const double zv0[4][2][2] = {};
-            for (int f = 0; f < total; f += 2 * SK) {
-                bfl(bB, f + SK);
-                __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
-                stage_mma_t<NRT>(arow + 32 * (f % nks), rst, bA, acc);
-                __builtin_amdgcn_sched_barrier(0);
-                bfl(bA, f + 2 * SK);
-                __builtin_amdgcn_sched_barrier(0);
-                stage_mma_t<NRT>(arow + 32 * ((f + SK) % nks), rst, bB, acc);
-                __builtin_amdgcn_sched_barrier(0);
-                if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc, zv0);
-            }
+            const int f = f0 + 2 * SK * (per - 1);
+            bfl(bB, f + SK);
+            zload(cbk, zv);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            bfl(bA, f + 2 * SK);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            epilogue(cbk, acc, zv);
         }
-    };
-    if (nR <= 1) sweep(std::integral_constant<int, 1>{});
-    else if (nR <= 2) sweep(std::integral_constant<int, 2>{});
-    else sweep(std::integral_constant<int, 4>{});
+    } else {
+        const double zv0[4][2][2] = {};
+        for (int f = 0; f < total; f += 2 * SK) {
+            bfl(bB, f + SK);
+            __builtin_amdgcn_sched_barrier(0);   // keep the loads at the stage start
+            stage_mma(arow + 32 * (f % nks), rst, bA, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            bfl(bA, f + 2 * SK);
+            __builtin_amdgcn_sched_barrier(0);
+            stage_mma(arow + 32 * ((f + SK) % nks), rst, bB, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            if ((f + 2 * SK) % nks == 0) epilogue(f / nks, acc, zv0);
+        }
+    }
     STAMP(2);
     if (!KY && !FUSE) STAMP_PRINT("i8ah prologue|sweep:", 3);
     if constexpr (!FUSE && !KY) {
@@ -650,12 +590,10 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     }
     if constexpr (FUSE) {
         __syncthreads();
-        {   // half-wave t >> 5 = position pb (realisation blo): its 8 waves x 32 lanes of slots, fixed order
-            const int pb = t >> 5, sub = t & 31, R = pb >> 2, q = (pb >> 1) & 1, hh = pb & 1;
-            const int blo = max(inv_s[pb], 0);
-            const bool pv = inv_s[pb] >= 0;
+        {   // half-wave t >> 5 = realisation blo: its 8 waves x 32 lanes of slots, fixed order
+            const int blo = t >> 5, sub = t & 31, R = blo >> 2, q = (blo >> 1) & 1, hh = blo & 1;
             double s0 = 0.0, s3 = 0.0;
-            if (pv && fs_s[blo].el && live_s[blo])
+            if (fs_s[blo].el && live_s[blo])
                 for (int ww = 0; ww < 8; ++ww) {
                     const double* zs = zsum + ((ww * 8 + 2 * R + q) * 2) * 64 + 32 * hh + sub;
                     s0 += zs[0];
@@ -666,7 +604,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                 s0 += __shfl_xor(s0, o, 64);
                 s3 += __shfl_xor(s3, o, 64);
             }
-            if (sub == 0 && pv && fs_s[blo].el && live_s[blo]) {
+            if (sub == 0 && fs_s[blo].el && live_s[blo]) {
                 RealState* st = za.st + j0 + blo;
                 st->fs0 = s0;   // ||E||^2 = ||X||^2
                 st->fs3 = s3;   // ||E - E_prev||^2 = ||X - Z||^2

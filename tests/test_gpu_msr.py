@@ -84,16 +84,3 @@ def test_msr_against_oracle(gpu, monkeypatch):
     assert err <= 1e-5, err
     assert np.array_equal(got[2][idx], ito)
 
-
-@pytest.mark.parametrize("fixed", [True, False])
-def test_i8_compaction_bit_identical(gpu, monkeypatch, fixed):
-    """ACE_I8_COMPACT=1 (i8ah_body packs the live slots of a 16-realisation block into the first MFMA
-    row tiles and runs ceil(live / 4) of the four) against the uncompacted sweep at batch 4096: the
-    digit-plane products are exact integer MFMAs per row, so X, Y, iteration counts and status must
-    be bit-identical, in fixed-horizon and in convergence mode (where blocks thin out)."""
-    from ace_amd import synth_problem
-    A, B, X0, _ = synth_problem(75, 0, 4096, 256, 32, 32)
-    ref, _ = _solve(monkeypatch, A, B, X0, {"ACE_I8_COMPACT": "0"}, fixed)
-    got, _ = _solve(monkeypatch, A, B, X0, {"ACE_I8_COMPACT": "1"}, fixed)
-    assert np.isfinite(got[0]).all()
-    _same(got, ref)

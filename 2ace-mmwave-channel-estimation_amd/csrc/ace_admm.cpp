@@ -113,7 +113,7 @@ static Knobs read_knobs() {
         return e ? atof(e) : dflt;
     };
     k.zcompact = (int)num("ACE_ZCOMPACT", 0);
-    k.cold_sync = (int)num("ACE_COLD_SYNC", 0);
+    k.cold_sync = exp_env("ACE_COLD_SYNC") ? atoi(exp_env("ACE_COLD_SYNC")) : 0;
     k.msp_fail_it = (int)num("ACE_MSP_FAIL_IT", -1);
     k.gyf_ctl = (int)num("ACE_GYF_CTL", 1);
     k.msp_room = num("ACE_MSP_ROOM", 32.0);
@@ -138,7 +138,7 @@ static Knobs read_knobs() {
 // ACE_MSR_TRACE=1: one stderr line per m-space run (resume point, steps, exit reasons)
 static bool msr_trace() {
     static const bool v = [] {
-        const char* e = getenv("ACE_MSR_TRACE");
+        const char* e = exp_env("ACE_MSR_TRACE");
         return e && e[0] == '1';
     }();
     return v;
@@ -456,7 +456,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
     // kernels of it, so that the sub-batches run different kernels (HBM- vs matrix-core-bound)
     // side by side instead of the same one (ACE_STAGGER, 0 = start together)
     static const int stg = [] {
-        const char* e = getenv("ACE_STAGGER");
+        const char* e = exp_env("ACE_STAGGER");
         return e ? atoi(e) : 0;
     }();
     hipEvent_t evs = nullptr;

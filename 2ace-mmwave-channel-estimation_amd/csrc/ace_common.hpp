@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "../../include/ace.h"
 
@@ -204,6 +205,18 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
         v[i] = s;
     }
     __syncthreads();
+}
+
+// Experiment and diagnostic switches (A/B measurements that were not kept, traces, workspace poisoning):
+// read only by a build with -DACE_EXPERIMENTS (make EXTRA=-DACE_EXPERIMENTS); the default build keeps
+// their defaults.  The switches the GPU tests use to pin bit-identity between paths stay plain getenv.
+inline const char* exp_env(const char* name) {
+#ifdef ACE_EXPERIMENTS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
 }
 
 // ------------------------------------------------------------------ dynamic LDS budgets (ace_api.cpp)

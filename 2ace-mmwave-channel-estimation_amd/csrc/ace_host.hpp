@@ -110,7 +110,7 @@ inline hipError_t upload(void* dst, const void* src, size_t bytes, hipStream_t s
 // it is carved, so that a read of memory the solve did not write shows up in its results
 inline void poison_workspace(void* ws, size_t bytes, hipStream_t st) {
     static const bool on = [] {
-        const char* e = getenv("ACE_POISON");
+        const char* e = exp_env("ACE_POISON");
         return e && e[0] == '1';
     }();
     if (on) (void)hipMemsetAsync(ws, 0xFF, bytes, st);

@@ -919,7 +919,7 @@ static void pc_inv_rec(int nb, int s, double* H, int ld, long long hs, double* s
 
 static bool pc_use_gj() {   // ACE_PC_GJ=1: the blocked Gauss-Jordan of r01 (A/B comparisons)
     static const bool v = [] {
-        const char* e = getenv("ACE_PC_GJ");
+        const char* e = exp_env("ACE_PC_GJ");
         return e && e[0] == '1';
     }();
     return v;
@@ -943,7 +943,7 @@ void launch_pc_ginv(int batch, int m, int n, const uint32_t* codes, const double
     const PcDims d = pc_dims(m, n);
     const uint32_t* cR = codes + (size_t)batch * d.nctH * d.nkgH * 128 + (size_t)batch * d.nctA * d.nkgA * 128;
     static const int chunk_env = [] {
-        const char* e = getenv("ACE_PC_CHUNK");
+        const char* e = exp_env("ACE_PC_CHUNK");
         return e ? atoi(e) : 0;
     }();
     const int chunk = chunk_env > 0 ? chunk_env : batch;

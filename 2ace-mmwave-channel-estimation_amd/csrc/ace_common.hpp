@@ -118,25 +118,6 @@ __device__ __forceinline__ int dual_finish(const DualCtl& c, RealState* st, doub
     return 0;
 }
 
-// Stores of per-realisation state that this launch does not read back (the next iteration's launch finds
-// it evicted from L2 anyway): with ACE_NT_STORES nontemporal, so that the operands every work-group
-// re-reads (G fragments, the codebook digit planes, Y / M between T and the Y-step) keep the L2.
-typedef double dvec2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_stream(d2* p, d2 v) {
-#ifdef ACE_NT_STORES
-    __builtin_nontemporal_store(dvec2{v.x, v.y}, reinterpret_cast<dvec2*>(p));
-#else
-    *p = v;
-#endif
-}
-__device__ __forceinline__ void st_stream(double* p, double v) {
-#ifdef ACE_NT_STORES
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
-
 // wave64 reduction of a double
 // 16-lane butterfly reductions with DPP partners instead of ds_bpermute (__shfl_xor): step o pairs
 // lane l with quad_perm l^1, quad_perm l^2, row_half_mirror (7 - l within 8) and row_mirror (15 - l).

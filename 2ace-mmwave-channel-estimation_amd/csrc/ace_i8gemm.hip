@@ -495,12 +495,12 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                             const double wv = scb * recombine(acc[R][c], q);
                             if (el) {
                                 const double x = zv[R][q][c] + wv, d = x - zv[R][q][c];
-                                st_stream(za.Zn + off, x);
-                                if (kc) st_stream(za.Xcur + off, x);
+                                za.Zn[off] = x;
+                                if (kc) za.Xcur[off] = x;
                                 p0 += x * x;
                                 p3 += d * d;
                             } else {
-                                st_stream(Wp + off, wv);
+                                Wp[off] = wv;
                             }
                         }
                     }
@@ -1076,9 +1076,9 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
             d2 gv, ax, mn, y;
             ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mii, yo, biv[c][r], gv, ax, mn, y, v7[r]);
             if constexpr (!GLDS) reinterpret_cast<d2*>(a.g)[off] = gv;
-            if (a.AX) st_stream(reinterpret_cast<d2*>(a.AX) + off, ax);
-            st_stream(reinterpret_cast<d2*>(a.M) + off, mn);
-            st_stream(reinterpret_cast<d2*>(a.Yn) + off, y);
+            if (a.AX) reinterpret_cast<d2*>(a.AX)[off] = ax;
+            reinterpret_cast<d2*>(a.M)[off] = mn;
+            reinterpret_cast<d2*>(a.Yn)[off] = y;
             if constexpr (GLDS) {
                 if (msp_s[jl]) {   // m-space candidate: Re (A Z)^H g, g^H K g = Re g^H (T - g), S' = S + g
                     msp_sums_elem(yo, mii, 1.0 / mu, Ts[jl * tst + i], gv, v7[r]);
@@ -1087,7 +1087,7 @@ __device__ __forceinline__ void gyk_body(int nb, int m, const GykArgs& a, unsign
                     // deferred opt_S (RealState::optsrc 4 / 5): the best iterate's S is the one this
                     // store overwrites -- keep it first (rare: no better iterate for two iterations)
                     if (oss_s[jl] == 4 + (a.it & 1)) reinterpret_cast<d2*>(a.optS)[off] = *sn;
-                    st_stream(sn, cadd(so, gv));
+                    *sn = cadd(so, gv);
                 }
                 Ts[jl * tst + i] = gv;   // g stays on chip for the fused apply_AH
             } else {

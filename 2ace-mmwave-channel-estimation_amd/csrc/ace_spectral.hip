@@ -255,6 +255,34 @@ bool hetrd_lds_ok(int mt) {
     return need <= 64 * 1024 || need <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_kernel));
 }
 
+// C = D (K + K^H)/2 D and dv into the scratch (hetrd_kernel's own prologue as a kernel of its own), for
+// the blocked reduction of the spectral initialisation: the same expressions per element
+__global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* Kp, const double* Bt, double* scratch,
+                                                           SpecLayout lay, const int* rows, int ldk) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    extern __shared__ double dvs[];   // [mt]
+    double* base = scratch + b * lay.stride;
+    d2* C = reinterpret_cast<d2*>(base + lay.C);
+    const d2* K = reinterpret_cast<const d2*>(Kp);
+    const int* rw = rows ? rows + (long long)b * ldk : nullptr;
+    const int ld = rows ? ldk : mt;
+    auto ri = [&](int i) { return rw ? rw[i] : i; };
+    for (int i = t; i < mt; i += 256) {
+        const double kii = K[(long long)ri(i) * ld + ri(i)].x;
+        const double d = kii > 0.0 ? Bt[(long long)b * ld + ri(i)] / sqrt(kii) : 0.0;
+        dvs[i] = d;
+        base[lay.dv + i] = d;
+    }
+    __syncthreads();
+    for (long long e = t; e < (long long)mt * mt; e += 256) {
+        const int i = (int)(e / mt), j = (int)(e % mt);
+        const d2 kij = K[(long long)ri(i) * ld + ri(j)], kji = K[(long long)ri(j) * ld + ri(i)];
+        const double s = dvs[i] * dvs[j];
+        C[e] = i == j ? make_double2(s * kij.x, 0.0)
+                      : make_double2(0.5 * s * (kij.x + kji.x), 0.5 * s * (kij.y - kji.y));
+    }
+}
+
 // Blocked form of the same reduction (LAPACK zhetrd / zlatrd) for PhaseLift's prox (C already in the
 // scratch): the reflectors of a panel of HB_NB columns are generated against the panel-start matrix plus
 // the panel's own rank-2 corrections (V W^H + W V^H held in LDS), so a column's Hermitian product only
@@ -814,12 +842,23 @@ size_t spectral_scratch_bytes(int mt, int n, int batch, int r) {
     return sizeof(double) * (size_t)lay.stride * chunk;
 }
 
+// the spectral initialisation's tridiagonalisation: the panel-blocked reduction when its LDS fits (order
+// <= ~560); ACE_HETRD_BLK=0 keeps hetrd_kernel (A/B; read once per process)
+static bool spectral_blk() {
+    static const bool v = [] {
+        const char* e = getenv("ACE_HETRD_BLK");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, const double* AH, const double* Bt,
                            double* scratch, double* X, int* status, hipStream_t st, const PartRows* pr) {
     if (pr) mt = pr->m;   // the full A^H, B and K; test rows weighted zero
     const SpecLayout lay(n, r);
     const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 16;
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
+    const bool blk = spectral_blk() && hetrd_blk_lds(n) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
     const int chunk = primal_chunk(mt, n, batch);
     double* Ast = scratch + (((size_t)lay.stride * chunk + 31) & ~(size_t)31);
     for (int b0 = 0; b0 < batch; b0 += chunk) {
@@ -832,8 +871,11 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
         launch_zgemm(0, true, n, mt, n, Ast, mt, (long long)n * mt, AH, mt, 0, scratch + lay.C, nullptr, n,
                      lay.stride / 2, nb, st);
         hipLaunchKernelGGL(spec_herm_kernel, dim3((n + 15) / 16, nb, (n + 15) / 16), dim3(256), 0, st, n, scratch, lay);
-        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
-                           nullptr, nullptr, 0);
+        if (blk)
+            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HT_THREADS), hetrd_blk_lds(n), st, n, scratch, lay, nullptr);
+        else
+            hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
+                               nullptr, nullptr, 0);
         hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, n, nullptr, scratch, lay, status, b0, nullptr);
         const int cv = backxf_chunk(n);
         double* Xb = X + 2LL * b0 * r * n;
@@ -849,11 +891,19 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
     const SpecLayout lay(mt, r);
     const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 16;
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
+    const bool blk = spectral_blk() && hetrd_blk_lds(mt) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
     const int ldb = pr ? pr->m : mt;   // per-realisation partitions: the full K and B, rows per realisation
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
-        hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
-                           lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
+        if (blk) {   // C formed first, then the panel-blocked reduction (r05)
+            hipLaunchKernelGGL(spec_form_c_kernel, dim3(nb), dim3(256), (size_t)mt * sizeof(double), st, mt, K,
+                               Bt + (long long)b0 * ldb, scratch, lay, pr ? pr->rows + (long long)b0 * pr->m : nullptr,
+                               pr ? pr->m : 0);
+            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HT_THREADS), hetrd_blk_lds(mt), st, mt, scratch, lay, nullptr);
+        } else {
+            hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
+                               lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
+        }
         hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr);
         const int cv = backxf_chunk(mt);
         hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * mt * 16, st, mt, r, scratch, lay,

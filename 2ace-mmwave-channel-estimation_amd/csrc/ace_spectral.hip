@@ -1044,14 +1044,9 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel), "hetrd_blk_kernel", hetrd_blk_lds(d)))
         blk = 0;   // (the unblocked reduction takes any d hetrd_lds_ok admits)
     if (blk) {
-#ifndef ACE_HB_CHUNK
-#define ACE_HB_CHUNK 0
-#endif
-        // (ACE_HB_CHUNK > 0, A/B build: that many matrices per launch, so the working set stays in the MALL)
-        const int chunk = ACE_HB_CHUNK > 0 ? ACE_HB_CHUNK : batch;
-        for (int b0 = 0; b0 < batch; b0 += chunk)
-            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(std::min(chunk, batch - b0)), dim3(HT_THREADS), hetrd_blk_lds(d), st,
-                               d, scratch + (size_t)b0 * lay.stride, lay, active ? active + b0 : nullptr);
+        // (all matrices in one launch: launches of 128 / 256 matrices, whose working set would stay in the MALL,
+        // measured 37.8 / 54.1 against 60.4 rec/s -- the reduction is bound by its work-groups' latency, not HBM)
+        hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HT_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
     } else {
         hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
                            nullptr, 0);

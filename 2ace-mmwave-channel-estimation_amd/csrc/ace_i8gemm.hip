@@ -320,6 +320,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
     __shared__ int live_s[RB];
     __shared__ FuseState fs_s[FUSE ? RB : 1];
     __shared__ int z0_s[(!FUSE && !KY) ? RB : 1];
+    __shared__ int nz_s[(!FUSE && !KY) ? RB : 1];   // (xzn, r-column stages: N held as exact zero, RealState::nzero)
     const int rst = 32 * nks + 16;   // LDS row stride (bytes)
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -397,6 +398,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
         sc_s[bl] = sc;
         live_s[bl] = live;
         imu_s[bl] = (!KY && !FUSE && za.xzn && live) ? 1.0 / rs[jb / rc].mu : 0.0;
+        if constexpr (!FUSE && !KY) nz_s[bl] = za.xzn && live && rc > 1 && rs[jb / rc].nzero;
     }
     for (int s = 0; s < nst; ++s) {
         d2 x0, x1;
@@ -525,7 +527,7 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                     const long long off = (long long)j * ldo + col;
                     const double wv = scb * recombine(acc[R][c], q);
                     if (matz) Wp[off] = (z0_s[blo] == 1 ? za.Z : za.Zn)[off] + wv;   // Z0 + A^H opt_S
-                    else if (za.xzn) Wp[off] = fma(-za.N[off], imu_s[blo], za.Z[off]) + wv;   // X = V + A^H g
+                    else if (za.xzn) Wp[off] = (nz_s[blo] ? za.Z[off] : fma(-za.N[off], imu_s[blo], za.Z[off])) + wv;   // X = V + A^H g
                     else Wp[off] = wv;
                 }
             }

@@ -474,6 +474,33 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     }
     return cnt;
 }
+// 1 / x from the v_rcp_f64 seed and two Newton steps (~1 ulp; x finite and nonzero here)
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return y;
+}
+// Sturm counts at two points at once (two independent chains: the bisection's trisection probes), with
+// e2 = e^2 precomputed and the reciprocal instead of the IEEE division on the dependent chain
+__device__ __forceinline__ void sturm_count2(const double* d, const double* e2, int n, double x0, double x1,
+                                             double pivmin, int& c0, int& c1) {
+    double q0 = d[0] - x0, q1 = d[0] - x1;
+    if (fabs(q0) < pivmin) q0 = -pivmin;
+    if (fabs(q1) < pivmin) q1 = -pivmin;
+    int n0 = q0 < 0.0, n1 = q1 < 0.0;
+    for (int i = 1; i < n; ++i) {
+        const double di = d[i], ei = e2[i - 1];
+        q0 = (di - x0) - ei * rcp_nr(q0);
+        q1 = (di - x1) - ei * rcp_nr(q1);
+        if (fabs(q0) < pivmin) q0 = -pivmin;
+        if (fabs(q1) < pivmin) q1 = -pivmin;
+        n0 += q0 < 0.0;
+        n1 += q1 < 0.0;
+    }
+    c0 = n0;
+    c1 = n1;
+}
 
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
@@ -491,12 +518,14 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     extern __shared__ double smem[];
     double* d = smem;
     double* e = smem + mt;
+    double* e2 = smem + 2 * mt;
     __shared__ double red[3 * 4];
     __shared__ int s_k, s_ncl;
     double* base = scratch + b * lay.stride;
     for (int i = t; i < mt; i += 256) {
         d[i] = base[lay.dd + i];
         e[i] = base[lay.ee + i];
+        e2[i] = e[i] * e[i];
     }
     __syncthreads();
     // Gershgorin interval and pivmin (LAPACK dstebz)
@@ -536,14 +565,24 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
-    for (int q = t; q < k; q += 256) {  // bisection for the (mt-1-q)-th ascending eigenvalue
+    for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
         for (int it = 0; it < 200; ++it) {
             if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
-            const double mid = 0.5 * (lo + hi);
-            if (sturm_count(d, e, mt, mid, pivmin) > j) hi = mid;
-            else lo = mid;
+            const double stp = (hi - lo) * (1.0 / 3.0);
+            const double x0 = lo + stp, x1 = fmax(x0, hi - stp);
+            int c0, c1;
+            sturm_count2(d, e2, mt, x0, x1, pivmin, c0, c1);
+            // eigenvalue j lies below x iff more than j eigenvalues do
+            if (c0 > j) {
+                hi = x0;
+            } else if (c1 > j) {
+                lo = x0;
+                hi = x1;
+            } else {
+                lo = x1;
+            }
         }
         lam[q] = 0.5 * (lo + hi);
     }
@@ -856,7 +895,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
                            double* scratch, double* X, int* status, hipStream_t st, const PartRows* pr) {
     if (pr) mt = pr->m;   // the full A^H, B and K; test rows weighted zero
     const SpecLayout lay(n, r);
-    const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 16;
+    const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 24;
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() && hetrd_blk_lds(n) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
     const int chunk = primal_chunk(mt, n, batch);
@@ -889,7 +928,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
                     int* status, hipStream_t st, const PartRows* pr) {
     const SpecLayout lay(mt, r);
-    const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 16;
+    const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 24;
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() && hetrd_blk_lds(mt) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
     const int ldb = pr ? pr->m : mt;   // per-realisation partitions: the full K and B, rows per realisation
@@ -1038,7 +1077,7 @@ size_t heev_scratch_bytes(int d, int kmax, int batch) {
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
                 const int* active, hipStream_t st, int blk) {
     const SpecLayout lay(d, kmax);
-    const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 16;
+    const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
     // the blocked reduction (hetrd_blk_kernel): blk = 1 (the caller reads ACE_HETRD_BLK once per solve)
     if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel), "hetrd_blk_kernel", hetrd_blk_lds(d)))

@@ -43,6 +43,13 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
     d2* N = reinterpret_cast<d2*>(a.N) + (long long)b * rn;
     d2* Z = reinterpret_cast<d2*>(a.Z) + (long long)b * rn;
 
+    // The r-column A2only stages keep N as exact zero after a Z-step with Z = E (no tail rescaling), as the
+    // unit path does (RealState::nzero, ace_zprox1w.hip): N + mu (X - E) is zero up to the rounding of
+    // E = X + N/mu.  While it holds, N is neither read nor written here, nor read by the applies of the next
+    // iteration (i8a, i8ah's X = Z - N/mu + W, pre_kernel): they take the zero vector.
+    const bool nzr = !INIT && VARIANT == ACE_VARIANT_A2ONLY && r > 1;
+    const bool nz_in = nzr && st->nzero;
+    const d2 zero2 = make_double2(0.0, 0.0);
     // accumulators: nX2, nZ2, nJN2, dZ2
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     VMax vz, vn;   // max |Z|, |N| of the outputs: the next apply's bound on |Z - N/mu|
@@ -60,15 +67,18 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
         Z[k] = znew;
     };
-    auto emit = [&](int k, d2 znew) {  // per-element update + reductions
+    // zeq: Z = E (no rescaling) -- with nzr the new N is the exact zero vector (not stored)
+    auto emit = [&](int k, d2 znew, bool zeq = false) {  // per-element update + reductions
         const d2 x = X[k];
         vz.add(znew);
         if (!INIT) {
             const d2 zo = Z[k];
             const d2 d = csub(x, znew);
-            const d2 nnew = cadd(N[k], cscale(d, mu));
-            N[k] = nnew;
-            vn.add(nnew);
+            if (!(nzr && zeq)) {
+                const d2 nnew = cadd(nz_in ? zero2 : N[k], cscale(d, mu));
+                N[k] = nnew;
+                vn.add(nnew);
+            }
             acc[0] += cabs2(x);
             acc[1] += cabs2(znew);
             acc[2] += cabs2(d);
@@ -76,7 +86,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
         }
         Z[k] = znew;
     };
-    auto evalE = [&](int k) -> d2 { return cadd(X[k], cscale(N[k], imu)); };  // X + N/mu (:424)
+    auto evalE = [&](int k) -> d2 { return nz_in ? X[k] : cadd(X[k], cscale(N[k], imu)); };  // X + N/mu (:424)
 
     // The spectral branches use two 32x32 complex LDS tiles (operands / H in L0,
     // eigenvectors in L1); their 32x32 complex products run on the f64 matrix cores.
@@ -488,7 +498,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
                     if (k < n) {
                         px[u] = X[j * n + k];
                         pz[u] = INIT ? make_double2(0.0, 0.0) : Z[j * n + k];
-                        pn[u] = N[j * n + k];
+                        pn[u] = nz_in ? zero2 : N[j * n + k];
                     }
                 }
             };
@@ -523,7 +533,7 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int k = k0 + t + nt * u;
-                    if (k < rn) emit(k, ev[u]);
+                    if (k < rn) emit(k, ev[u], true);
                 }
             }
         }
@@ -535,6 +545,9 @@ __global__ __launch_bounds__(256) void zstep_kernel(ZArgs a) {
 #endif
     }
 #undef ACE_ZSTEP_LDS
+    if constexpr (VARIANT == ACE_VARIANT_A2ONLY) {
+        if (nzr && t == 0) st->nzero = flag_any ? 0 : 1;
+    }
     // bound for the next iteration's V = Z - N/mu (written after iter_control's mu update)
     double vb[3] = {wave_max(vz.m), wave_max(vn.m), wave_sum(vz.s + vn.s)};
     __syncthreads();
@@ -602,7 +615,8 @@ __global__ __launch_bounds__(256) void pre_kernel(int n, int m, const double* Zp
     const d2* N = reinterpret_cast<const d2*>(Np) + (long long)b * n;
     if (Vp) {   // (the int8 r-column stages form V inside their applies: S only)
         d2* V = reinterpret_cast<d2*>(Vp) + (long long)b * n;
-        for (int k = threadIdx.x; k < n; k += blockDim.x) V[k] = csub(Z[k], cscale(N[k], imu));
+        const bool nz = st[b].nzero;   // (N held as exact zero: the r-column stages, zstep_kernel)
+        for (int k = threadIdx.x; k < n; k += blockDim.x) V[k] = nz ? Z[k] : csub(Z[k], cscale(N[k], imu));
     }
     const d2* Y = reinterpret_cast<const d2*>(Yp) + (long long)b * m;
     const d2* M = reinterpret_cast<const d2*>(Mp) + (long long)b * m;

@@ -944,6 +944,7 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
                 zv.xzn = 1;
                 zv.Z = w.Z;
                 zv.N = w.N;
+                zv.zeros = w.zeros;   // (rows of realisations whose N is held as exact zero)
                 launch_i8_apply_AH(nv, m, n, L.LAH8, w.g, w.X, L.c8, w.st, st, nullptr, &zv);
             } else applyAH(w.g, w.X, w.V);
             ACE_LAUNCHED((wmode || i8r) ? "apply_AH (i8ah_kernel)" : "apply_AH (zgemm)");

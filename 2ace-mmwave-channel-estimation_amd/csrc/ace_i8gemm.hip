@@ -527,7 +527,10 @@ __device__ __forceinline__ void i8ah_body(int nb, int Kc, int Mc, int nks, const
                     const long long off = (long long)j * ldo + col;
                     const double wv = scb * recombine(acc[R][c], q);
                     if (matz) Wp[off] = (z0_s[blo] == 1 ? za.Z : za.Zn)[off] + wv;   // Z0 + A^H opt_S
-                    else if (za.xzn) Wp[off] = (nz_s[blo] ? za.Z[off] : fma(-za.N[off], imu_s[blo], za.Z[off])) + wv;   // X = V + A^H g
+                    else if (za.xzn) {   // X = V + A^H g; N held as exact zero reads the zero row (no branch)
+                        const double* nrow = nz_s[blo] ? za.zeros : za.N + (long long)j * ldo;
+                        Wp[off] = fma(-nrow[col], imu_s[blo], za.Z[off]) + wv;
+                    }
                     else Wp[off] = wv;
                 }
             }

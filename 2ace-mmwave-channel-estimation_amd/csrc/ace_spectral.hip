@@ -651,16 +651,33 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
             at(4, mt - 1) = 0.0;
             for (int i = 0; i < mt; ++i) at(5, i) = 1.0 + 0.01 * sin(1.0 + 0.7 * i + 1.3 * q);  // start vector
             double* zq = Z + (long long)q * mt;
+            // The solves below walk the lane's LU arrays (lane-interleaved global scratch) one row after the
+            // other; the loads of a block of TE_PF rows are issued together ahead of the block's dependent
+            // chain (they depend on the row index only), so the chain waits for one memory round trip per
+            // block instead of one per row.  Same operations in the same order as the row-by-row form.
+            constexpr int TE_PF = 8;
             for (int sweep = 0; sweep < 3; ++sweep) {
                 double cur = at(5, 0);
-                for (int i = 0; i + 1 < mt; ++i) {  // dgttrs, L
-                    const double nxt = at(5, i + 1), f = at(0, i);
-                    if (at(4, i) == 0.0) {
-                        at(5, i) = cur;
-                        cur = nxt - f * cur;
-                    } else {
-                        at(5, i) = nxt;
-                        cur = cur - f * nxt;
+                for (int i0 = 0; i0 + 1 < mt; i0 += TE_PF) {  // dgttrs, L
+                    double nx[TE_PF], fv[TE_PF], pv[TE_PF];
+#pragma unroll
+                    for (int u = 0; u < TE_PF; ++u) {
+                        const int i = min(i0 + u, mt - 2);
+                        nx[u] = at(5, i + 1);
+                        fv[u] = at(0, i);
+                        pv[u] = at(4, i);
+                    }
+#pragma unroll
+                    for (int u = 0; u < TE_PF; ++u) {
+                        const int i = i0 + u;
+                        if (i + 1 >= mt) break;
+                        if (pv[u] == 0.0) {
+                            at(5, i) = cur;
+                            cur = nx[u] - fv[u] * cur;
+                        } else {
+                            at(5, i) = nx[u];
+                            cur = cur - fv[u] * nx[u];
+                        }
                     }
                 }
                 // U back substitution, y_{i+1} and y_{i+2} carried in registers
@@ -672,12 +689,26 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                     at(5, mt - 2) = y1;
                     nrm += y1 * y1;
                 }
-                for (int i = mt - 3; i >= 0; --i) {
-                    const double y = (at(5, i) - at(2, i) * y1 - at(3, i) * y2) / at(1, i);
-                    at(5, i) = y;
-                    nrm += y * y;
-                    y2 = y1;
-                    y1 = y;
+                for (int i0 = mt - 3; i0 >= 0; i0 -= TE_PF) {
+                    double yv[TE_PF], u1v[TE_PF], u2v[TE_PF], u3v[TE_PF];
+#pragma unroll
+                    for (int u = 0; u < TE_PF; ++u) {
+                        const int i = max(i0 - u, 0);
+                        yv[u] = at(5, i);
+                        u1v[u] = at(1, i);
+                        u2v[u] = at(2, i);
+                        u3v[u] = at(3, i);
+                    }
+#pragma unroll
+                    for (int u = 0; u < TE_PF; ++u) {
+                        const int i = i0 - u;
+                        if (i < 0) break;
+                        const double y = (yv[u] - u2v[u] * y1 - u3v[u] * y2) / u1v[u];
+                        at(5, i) = y;
+                        nrm += y * y;
+                        y2 = y1;
+                        y1 = y;
+                    }
                 }
                 if (q > q0) {   // project out the cluster's earlier vectors
                     for (int p = q0; p < q; ++p) {

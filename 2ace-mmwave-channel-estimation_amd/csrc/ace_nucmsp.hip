@@ -177,19 +177,31 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
     }
     if constexpr (FIN) return;
 
-    // ---- T = (Y - M/mu) - A V,  V = c_v E_prev
-    for (int idx = t; idx < GRB * tst; idx += NT) {
-        const int jl = idx / tst, k = idx - jl * tst;
-        d2 v = make_double2(0.0, 0.0);
-        if (k < m && live_s[jl]) {
-            const long long o = (long long)(j0 + jl) * m + k;
-            const double imu = 1.0 / mu_s[jl], cv = az_s[jl] - an_s[jl] * imu;
-            const d2 y = reinterpret_cast<const d2*>(a.Yo)[o], mm = reinterpret_cast<const d2*>(a.M)[o];
+    // ---- T = (Y - M/mu) - A V,  V = c_v E_prev, formed on this lane's pass-1 outputs (realisation
+    // (lane >> 4) + 4 r, entry 16 (2 w + c) + (lane & 15)): Y and M stay in registers for the Y-step instead
+    // of being read again after G T (by then other work-groups' streams have evicted them from the L2)
+    d2 yh[2][4], mh[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int ct = 2 * w + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int jl = (lane >> 4) + 4 * r, i = 16 * ct + (lane & 15);
+            const bool in = ct < nct && i < m && live_s[jl];
+            const long long o = (long long)(live_s[jl] ? j0 + jl : j0) * m + min(i, m - 1);   // (clamped: loads
+            const d2 y = reinterpret_cast<const d2*>(a.Yo)[o], mm = reinterpret_cast<const d2*>(a.M)[o];   //  batched)
             const d2 aep = reinterpret_cast<const d2*>(a.AEo)[o];
-            v = make_double2(fma(-mm.x, imu, y.x) - cv * aep.x, fma(-mm.y, imu, y.y) - cv * aep.y);
+            yh[c][r] = y;
+            mh[c][r] = mm;
+            d2 v = make_double2(0.0, 0.0);
+            if (in) {
+                const double imu = 1.0 / mu_s[jl], cv = az_s[jl] - an_s[jl] * imu;
+                v = make_double2(fma(-mm.x, imu, y.x) - cv * aep.x, fma(-mm.y, imu, y.y) - cv * aep.y);
+            }
+            if (ct < nct) Ts[jl * tst + i] = v;
         }
-        Ts[idx] = v;
     }
+    if (t < GRB) Ts[t * tst + mp] = make_double2(0.0, 0.0);   // (the row stride's pad column)
     __syncthreads();
     // ---- g = G T
     d4v p1[2], p2[2], p3[2];
@@ -211,7 +223,7 @@ __global__ __launch_bounds__(NT, 1) void nms_kernel(int nb, int m, NmsArgs a, ZA
             const long long off = (long long)(j0 + jl) * m + i;
             const d2 gv = frag_out(p1, p2, p3, c, r), tv = Ts[jl * tst + i];
             const double mu = mu_s[jl], imu = 1.0 / mu, az = az_s[jl];
-            const d2 mii = reinterpret_cast<const d2*>(a.M)[off], yo = reinterpret_cast<const d2*>(a.Yo)[off];
+            const d2 mii = mh[c][r], yo = yh[c][r];   // (read with T's inputs)
             const double Bi = a.B[off];
             // Y-step (:326-337), the reference's expressions
             const d2 ax = csub(csub(yo, cscale(mii, imu)), gv);

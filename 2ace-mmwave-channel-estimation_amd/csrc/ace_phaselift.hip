@@ -170,20 +170,52 @@ __global__ __launch_bounds__(256) void pl_grad_kernel(PlArgs a) {
 // prox_trace input (tfocs_AT.m:52-53, prox_trace.m:88-92): (W + W^H)/2, W = z_old - step g_y,
 // written where the eigensolver reads its matrix.
 __global__ __launch_bounds__(256) void pl_prox_in_kernel(PlArgs a) {
+    // C = (W + W^H) / 2 with W = z_old - step G, by 32 x 32 tile pairs (I, J), (J, I) staged in LDS, so
+    // every entry is read once and both tiles' reads and writes are row-coalesced (the element-wise form
+    // read W[j][i] down a column: 7x the matrix bytes fetched).  Same expressions per entry.
     const int b = blockIdx.x, t = threadIdx.x;
     if (!a.act[b]) return;
     const double st = a.st[b].step;
-    const int d = a.d;
+    const int d = a.d, nt = (d + 31) / 32;
     const long long o = (long long)b * d * d;
     const d2* zo = reinterpret_cast<const d2*>(a.zo) + o;
     const d2* G = reinterpret_cast<const d2*>(a.G) + o;
     d2* C = reinterpret_cast<d2*>(a.scratch + (long long)b * a.hl.stride + a.hl.C);
-    for (long long e = t; e < (long long)d * d; e += 256) {
-        const int i = (int)(e / d), j = (int)(e % d);
-        const long long f = (long long)j * d + i;
-        const d2 w1 = csub(zo[e], cscale(G[e], st)), w2 = csub(zo[f], cscale(G[f], st));
-        C[e] = make_double2(0.5 * (w1.x + w2.x), 0.5 * (w1.y - w2.y));
-    }
+    __shared__ d2 tu[32][33], tl[32][33];   // W(I, J) and W(J, I)
+    const int cc = t & 31, r0 = t >> 5;      // column within the tile, first row (8 rows per pass)
+    for (int I = 0; I < nt; ++I)
+        for (int J = I; J < nt; ++J) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = r0 + 8 * q;
+                const int i1 = 32 * I + rr, j1 = 32 * J + cc;   // W(I, J) entry (i1, j1)
+                const int i2 = 32 * J + rr, j2 = 32 * I + cc;   // W(J, I) entry (i2, j2)
+                if (i1 < d && j1 < d) {
+                    const long long e = (long long)i1 * d + j1;
+                    tu[rr][cc] = csub(zo[e], cscale(G[e], st));
+                }
+                if (i2 < d && j2 < d) {
+                    const long long e = (long long)i2 * d + j2;
+                    tl[rr][cc] = csub(zo[e], cscale(G[e], st));
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = r0 + 8 * q;
+                const int i1 = 32 * I + rr, j1 = 32 * J + cc;
+                if (i1 < d && j1 < d) {   // C[i1][j1] from w1 = W[i1][j1], w2 = W[j1][i1]
+                    const d2 w1 = tu[rr][cc], w2 = tl[cc][rr];
+                    C[(long long)i1 * d + j1] = make_double2(0.5 * (w1.x + w2.x), 0.5 * (w1.y - w2.y));
+                }
+                const int i2 = 32 * J + rr, j2 = 32 * I + cc;
+                if (I != J && i2 < d && j2 < d) {   // C[i2][j2] from W[i2][j2], W[j2][i2]
+                    const d2 w1 = tl[rr][cc], w2 = tu[cc][rr];
+                    C[(long long)i2 * d + j2] = make_double2(0.5 * (w1.x + w2.x), 0.5 * (w1.y - w2.y));
+                }
+            }
+            __syncthreads();
+        }
 }
 
 // prox_trace.m:140-147: keep s = lam - tau > 0; P = V^T diag(s), VT = V^T (zero beyond k), so

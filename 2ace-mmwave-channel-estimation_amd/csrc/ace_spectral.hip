@@ -290,9 +290,29 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 // HB_NB + 2 passes over the trailing matrix instead of hetrd_kernel's 2 HB_NB (read + write per step):
 // the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
 // d, e, tau and reflector k in row k of C.
-constexpr int HB_NB = 8;
-size_t hetrd_blk_lds(int mt) { return (size_t)mt * 16 * (2 * HB_NB + 2); }
-__global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
+#ifndef ACE_HB_NB
+#define ACE_HB_NB 8
+#endif
+#ifndef ACE_HB_THREADS
+#define ACE_HB_THREADS 1024
+#endif
+constexpr int HB_NB = ACE_HB_NB;             // panel width
+constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
+constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
+constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
+// ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
+// the trailing matrix -- half the bytes of the full square (the kernel is bound by them)
+#ifndef ACE_HB_LOWER
+#define ACE_HB_LOWER 0
+#endif
+constexpr int HB_NW = HB_THREADS / 64;   // waves
+__host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
+size_t hetrd_blk_lds(int mt) {
+    size_t b = (size_t)mt * 16 * (2 * HB_NB + 2);
+    if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
+    return b;
+}
+__global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
     extern __shared__ double smem[];
@@ -301,29 +321,41 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
     d2* v = Wp + HB_NB * mt;                // current reflector, entry i = row k + 1 + i
     d2* w = v + mt;
     __shared__ double red[16 * 4 * HB_NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
-    __shared__ d2 part[HT_RB][HT_COLS];
+#if ACE_HB_LOWER
+    d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
+    d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
+#else
+    __shared__ d2 part[HB_RB][HB_COLS];
+#endif
     __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
     double* dd = base + lay.dd;
     double* ee = base + lay.ee;
     d2* taus = reinterpret_cast<d2*>(base + lay.tau);
-    const int col = t % HT_COLS, rb = t / HT_COLS;
+    const int col = t % HB_COLS, rb = t / HB_COLS;
     auto cj = [](d2 a) { return make_double2(a.x, -a.y); };
     for (int k0 = 0; k0 + 1 < mt; k0 += HB_NB) {
         const int nbp = min(HB_NB, mt - 1 - k0);
-        for (int e = t; e < 2 * HB_NB * mt; e += HT_THREADS) Vp[e] = make_double2(0.0, 0.0);
+        for (int e = t; e < 2 * HB_NB * mt; e += HB_THREADS) Vp[e] = make_double2(0.0, 0.0);
         __syncthreads();
         for (int p = 0; p < nbp; ++p) {
             const int k = k0 + p, L = mt - k - 1;
             // row k of the current matrix: the panel-start C minus the panel's earlier rank-2 updates
             double s1[1] = {0.0};
-            for (int i = t; i < L; i += HT_THREADS) {
+            for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
+#if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
+                d2 a = C[(long long)c * mt + k];
+                for (int q = 0; q < p; ++q)
+                    a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
+                v[i] = a;   // x_i = A[k + 1 + i][k]
+#else
                 d2 a = C[(long long)k * mt + c];
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + c])), cmul(Wp[q * mt + k], cj(Vp[q * mt + c]))));
                 v[i] = cj(a);   // x_i = A[k + 1 + i][k]
+#endif
                 if (i > 0) s1[0] += cabs2(a);
             }
             block_sum<1>(s1, red);
@@ -352,7 +384,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
             const d2 tau = s_tau;
             if (tau.x == 0.0 && tau.y == 0.0) continue;   // H = I (uniform): V, W of this column stay 0
             const d2 scal = s_scal;
-            for (int i = t; i < L; i += HT_THREADS) {
+            for (int i = t; i < L; i += HB_THREADS) {
                 const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
                 v[i] = vi;
                 C[(long long)k * mt + k + 1 + i] = vi;   // reflector k kept in row k (for the back transform)
@@ -362,7 +394,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             for (int q = 0; q < p; ++q) {
                 d2 a = make_double2(0.0, 0.0), c2 = a;
-                for (int i = t; i < L; i += HT_THREADS) {
+                for (int i = t; i < L; i += HB_THREADS) {
                     const int r = k + 1 + i;
                     a = cadd(a, cmulc(Wp[q * mt + r], v[i]));
                     c2 = cadd(c2, cmulc(Vp[q * mt + r], v[i]));
@@ -378,7 +410,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             if (t < p) {   // fixed order over the 16 waves
                 double sw0 = 0.0, sw1 = 0.0, sv0 = 0.0, sv1 = 0.0;
-                for (int ww = 0; ww < HT_THREADS / 64; ++ww) {
+                for (int ww = 0; ww < HB_THREADS / 64; ++ww) {
                     const double* r4 = red + (t * 16 + ww) * 4;
                     sw0 += r4[0];
                     sw1 += r4[1];
@@ -391,13 +423,99 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
-            for (int i0 = 0; i0 < L; i0 += HT_COLS) {
+#if ACE_HB_LOWER
+            // From the lower triangle only: element (j, i), j >= i, adds conj(c) v_j to p_i (column sums) and,
+            // for j > i, c v_i to p_j (row sums).  Tasks are 4-row groups of 64-column strips (strip s: columns
+            // 64s.., rows 64s..L-1), dealt to the waves in contiguous runs; lane (jr, ic) reads row jr of the
+            // group at columns ic + 16q (four 256-B rows per load).  A row's sum over a strip is reduced over
+            // the 16 ic lanes; a wave's column sums over its run in a strip over the 4 jr lanes at the end of
+            // the run (slot wave + strip: unique, since the runs are contiguous).
+            {
+                const int ns = hb_strips(L), wv = t >> 6, jr = (t & 63) >> 4, ic = t & 15;
+                auto ngr = [&](int s) { return (L - 64 * s + 3) >> 2; };
+                int G = 0;
+                for (int s = 0; s < ns; ++s) G += ngr(s);
+                const int g0 = wv * G / HB_NW, g1 = (wv + 1) * G / HB_NW;
+                const d2* C22 = C + r0;
+                int s = 0, gb = 0;
+                while (s < ns && g0 >= gb + ngr(s)) gb += ngr(s++);
+                d2 ca[4];
+                auto strip_start = [&]() {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ca[q] = make_double2(0.0, 0.0);
+                };
+                auto flush = [&]() {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        double x = ca[q].x, y = ca[q].y;
+#pragma unroll
+                        for (int o = 16; o < 64; o <<= 1) {
+                            x += __shfl_xor(x, o, 64);
+                            y += __shfl_xor(y, o, 64);
+                        }
+                        if (jr == 0) colp[(wv + s) * 64 + ic + 16 * q] = make_double2(x, y);
+                    }
+                };
+                if (g0 < g1) strip_start();
+                for (int g = g0; g < g1; ++g) {
+                    if (g - gb >= ngr(s)) {
+                        flush();
+                        gb += ngr(s++);
+                        strip_start();
+                    }
+                    const int j = 64 * s + 4 * (g - gb) + jr;
+                    const bool jv = j < L;
+                    const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
+                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s + ic;
+                    d2 c[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        c[q] = (jv && 64 * s + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
+                    double rx = 0.0, ry = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        ca[q].x += c[q].x * vj.x + c[q].y * vj.y;
+                        ca[q].y += c[q].x * vj.y - c[q].y * vj.x;
+                        if (64 * s + ic + 16 * q < j) {   // (then i < L: v[i] is live)
+                            const d2 vi = v[64 * s + ic + 16 * q];
+                            rx += c[q].x * vi.x - c[q].y * vi.y;
+                            ry += c[q].x * vi.y + c[q].y * vi.x;
+                        }
+                    }
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        rx += __shfl_xor(rx, o, 64);
+                        ry += __shfl_xor(ry, o, 64);
+                    }
+                    if (ic == 0 && jv) rowp[s * mt + j] = make_double2(rx, ry);
+                }
+                if (g0 < g1) flush();
+                __syncthreads();
+                for (int i = t; i < L; i += HB_THREADS) {
+                    const int si = i >> 6;
+                    int bs = 0;
+                    for (int q = 0; q < si; ++q) bs += ngr(q);
+                    const int be = bs + ngr(si);
+                    d2 acc = make_double2(0.0, 0.0);
+                    for (int ww = 0; ww < HB_NW; ++ww)   // the runs that cover strip si, in wave order
+                        if (ww * G / HB_NW < be && (ww + 1) * G / HB_NW > bs && ww * G / HB_NW < (ww + 1) * G / HB_NW)
+                            acc = cadd(acc, colp[(ww + si) * 64 + (i & 63)]);
+                    for (int q = 0; q <= si; ++q) acc = cadd(acc, rowp[q * mt + i]);
+                    const int r = k + 1 + i;
+                    for (int q = 0; q < p; ++q)
+                        acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
+                    w[i] = cmul(tau, acc);
+                }
+                __syncthreads();
+            }
+#else
+            for (int i0 = 0; i0 < L; i0 += HB_COLS) {
                 const int i = i0 + col;
                 double ar = 0.0, ai = 0.0;
                 if (i < L) {
                     const d2* cc = C + r0 + i;
 #pragma unroll 4
-                    for (int j = rb; j < L; j += HT_RB) {
+                    for (int j = rb; j < L; j += HB_RB) {
                         const d2 c = cc[(long long)j * mt], vj = v[j];
                         ar += c.x * vj.x + c.y * vj.y;
                         ai += c.x * vj.y - c.y * vj.x;
@@ -408,7 +526,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
                 if (rb == 0 && i < L) {
                     d2 acc = part[0][col];
 #pragma unroll
-                    for (int q = 1; q < HT_RB; ++q) acc = cadd(acc, part[q][col]);
+                    for (int q = 1; q < HB_RB; ++q) acc = cadd(acc, part[q][col]);
                     const int r = k + 1 + i;
                     for (int q = 0; q < p; ++q)
                         acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
@@ -416,16 +534,17 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
                 }
                 __syncthreads();
             }
+#endif
             // w = p - (tau / 2) (p^H v) v
             double s2[2] = {0.0, 0.0};
-            for (int i = t; i < L; i += HT_THREADS) {
+            for (int i = t; i < L; i += HB_THREADS) {
                 const d2 q = cmulc(w[i], v[i]);
                 s2[0] += q.x;
                 s2[1] += q.y;
             }
             block_sum<2>(s2, red);
             const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
-            for (int i = t; i < L; i += HT_THREADS) {
+            for (int i = t; i < L; i += HB_THREADS) {
                 const d2 wi = cadd(w[i], cmul(alpha2, v[i]));
                 Wp[p * mt + k + 1 + i] = wi;
             }
@@ -433,7 +552,7 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
         }
         // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
         const int kn = k0 + nbp, L2 = mt - kn;
-        for (int i0 = 0; i0 < L2; i0 += HT_COLS) {
+        for (int i0 = 0; i0 < L2; i0 += HB_COLS) {
             const int i = i0 + col;
             if (i >= L2) continue;
             const int ci = kn + i;
@@ -443,7 +562,11 @@ __global__ __launch_bounds__(HT_THREADS) void hetrd_blk_kernel(int mt, double* s
                 vq[q] = cj(Vp[q * mt + ci]);
                 wq[q] = cj(Wp[q * mt + ci]);
             }
-            for (int j = rb; j < L2; j += HT_RB) {
+#if ACE_HB_LOWER
+            for (int j = i + (((rb - i) % HB_RB) + HB_RB) % HB_RB; j < L2; j += HB_RB) {   // rows j >= i
+#else
+            for (int j = rb; j < L2; j += HB_RB) {
+#endif
                 const int rj = kn + j;
                 d2* cp = C + (long long)rj * mt + ci;
                 d2 c = *cp;
@@ -942,7 +1065,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
                      lay.stride / 2, nb, st);
         hipLaunchKernelGGL(spec_herm_kernel, dim3((n + 15) / 16, nb, (n + 15) / 16), dim3(256), 0, st, n, scratch, lay);
         if (blk)
-            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HT_THREADS), hetrd_blk_lds(n), st, n, scratch, lay, nullptr);
+            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(n), st, n, scratch, lay, nullptr);
         else
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
                                nullptr, nullptr, 0);
@@ -969,7 +1092,7 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
             hipLaunchKernelGGL(spec_form_c_kernel, dim3(nb), dim3(256), (size_t)mt * sizeof(double), st, mt, K,
                                Bt + (long long)b0 * ldb, scratch, lay, pr ? pr->rows + (long long)b0 * pr->m : nullptr,
                                pr ? pr->m : 0);
-            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HT_THREADS), hetrd_blk_lds(mt), st, mt, scratch, lay, nullptr);
+            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(mt), st, mt, scratch, lay, nullptr);
         } else {
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
                                lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
@@ -1116,7 +1239,7 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     if (blk) {
         // (all matrices in one launch: launches of 128 / 256 matrices, whose working set would stay in the MALL,
         // measured 37.8 / 54.1 against 60.4 rec/s -- the reduction is bound by its work-groups' latency, not HBM)
-        hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HT_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
+        hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HB_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
     } else {
         hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
                            nullptr, 0);

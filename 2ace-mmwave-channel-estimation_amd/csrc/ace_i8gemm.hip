@@ -1437,9 +1437,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
     // state of iterate it0 - 1.  AX lives in the T tile between iterations: the thread's slot (jl, i) holds
     // AX from its Y-step until its T formation reads it and writes T there (registers: 32 VGPRs fewer)
     d2 yv[TPW][4], mv[TPW][4];
-#ifndef ACE_MSR_BLOAD
     double bv[TPW][4];
-#endif
     {
         const int p = (a.it0 - 1) & 1;
 #pragma unroll
@@ -1450,9 +1448,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 yv[c][r] = reinterpret_cast<const d2*>(a.Y[p])[o];
                 mv[c][r] = reinterpret_cast<const d2*>(a.M)[o];
                 Ts[((lane >> 4) + 4 * r) * tst + 16 * (TPW * w + c) + (lane & 15)] = reinterpret_cast<const d2*>(a.AX)[o];
-#ifndef ACE_MSR_BLOAD
                 bv[c][r] = a.B[o];
-#endif
                 Ss[(4 * c + r) * NTW + t] = reinterpret_cast<const d2*>(a.S[p])[o];
             }
     }
@@ -1566,12 +1562,7 @@ __global__ __launch_bounds__(64 * 16 / TPW, 1) void msr_kernel(MsrArgs a, ZArgs 
                 if (!lv[r]) continue;
                 const double mu = mu_s[jl];
                 d2 gv, ax, mn, y;
-#ifdef ACE_MSR_BLOAD   // B read again each iteration (L2-resident) instead of held in 16 VGPRs
-                const double bcr = a.B[off(r, c)];
-#else
-                const double bcr = bv[c][r];
-#endif
-                ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mv[c][r], yv[c][r], bcr, gv, ax, mn, y, v7);
+                ystep_elem(p1[c][r], p2[c][r], p3[c][r], mu, mv[c][r], yv[c][r], bv[c][r], gv, ax, mn, y, v7);
                 msp_sums_elem(yv[c][r], mv[c][r], 1.0 / mu, Ts[jl * tst + i], gv, v7);
                 sn[c][r] = cadd(Ss[(4 * c + r) * NTW + t], gv);
                 yn[c][r] = y;

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 // the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
 // d, e, tau and reflector k in row k of C.
 #ifndef ACE_HB_NB
-#define ACE_HB_NB 8
+#define ACE_HB_NB 4   // (r05: 4 against 8 at 1024 threads: PhaseLift 64.6 -> 67.5 rec/s; 2, and 512 / 256 threads, slower)
 #endif
 #ifndef ACE_HB_THREADS
 #define ACE_HB_THREADS 1024
@@ -300,18 +300,7 @@ constexpr int HB_NB = ACE_HB_NB;             // panel width
 constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
 constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
 constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
-// ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
-// the trailing matrix -- half the bytes of the full square (the kernel is bound by them)
-#ifndef ACE_HB_LOWER
-#define ACE_HB_LOWER 0
-#endif
-constexpr int HB_NW = HB_THREADS / 64;   // waves
-__host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
-size_t hetrd_blk_lds(int mt) {
-    size_t b = (size_t)mt * 16 * (2 * HB_NB + 2);
-    if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
-    return b;
-}
+size_t hetrd_blk_lds(int mt) { return (size_t)mt * 16 * (2 * HB_NB + 2); }
 __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
@@ -321,12 +310,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
     d2* v = Wp + HB_NB * mt;                // current reflector, entry i = row k + 1 + i
     d2* w = v + mt;
     __shared__ double red[16 * 4 * HB_NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
-#if ACE_HB_LOWER
-    d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
-    d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
-#else
     __shared__ d2 part[HB_RB][HB_COLS];
-#endif
     __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
@@ -345,17 +329,10 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             double s1[1] = {0.0};
             for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
-#if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
-                d2 a = C[(long long)c * mt + k];
-                for (int q = 0; q < p; ++q)
-                    a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
-                v[i] = a;   // x_i = A[k + 1 + i][k]
-#else
                 d2 a = C[(long long)k * mt + c];
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + c])), cmul(Wp[q * mt + k], cj(Vp[q * mt + c]))));
                 v[i] = cj(a);   // x_i = A[k + 1 + i][k]
-#endif
                 if (i > 0) s1[0] += cabs2(a);
             }
             block_sum<1>(s1, red);
@@ -423,92 +400,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
-#if ACE_HB_LOWER
-            // From the lower triangle only: element (j, i), j >= i, adds conj(c) v_j to p_i (column sums) and,
-            // for j > i, c v_i to p_j (row sums).  Tasks are 4-row groups of 64-column strips (strip s: columns
-            // 64s.., rows 64s..L-1), dealt to the waves in contiguous runs; lane (jr, ic) reads row jr of the
-            // group at columns ic + 16q (four 256-B rows per load).  A row's sum over a strip is reduced over
-            // the 16 ic lanes; a wave's column sums over its run in a strip over the 4 jr lanes at the end of
-            // the run (slot wave + strip: unique, since the runs are contiguous).
-            {
-                const int ns = hb_strips(L), wv = t >> 6, jr = (t & 63) >> 4, ic = t & 15;
-                auto ngr = [&](int s) { return (L - 64 * s + 3) >> 2; };
-                int G = 0;
-                for (int s = 0; s < ns; ++s) G += ngr(s);
-                const int g0 = wv * G / HB_NW, g1 = (wv + 1) * G / HB_NW;
-                const d2* C22 = C + r0;
-                int s = 0, gb = 0;
-                while (s < ns && g0 >= gb + ngr(s)) gb += ngr(s++);
-                d2 ca[4];
-                auto strip_start = [&]() {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) ca[q] = make_double2(0.0, 0.0);
-                };
-                auto flush = [&]() {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        double x = ca[q].x, y = ca[q].y;
-#pragma unroll
-                        for (int o = 16; o < 64; o <<= 1) {
-                            x += __shfl_xor(x, o, 64);
-                            y += __shfl_xor(y, o, 64);
-                        }
-                        if (jr == 0) colp[(wv + s) * 64 + ic + 16 * q] = make_double2(x, y);
-                    }
-                };
-                if (g0 < g1) strip_start();
-                for (int g = g0; g < g1; ++g) {
-                    if (g - gb >= ngr(s)) {
-                        flush();
-                        gb += ngr(s++);
-                        strip_start();
-                    }
-                    const int j = 64 * s + 4 * (g - gb) + jr;
-                    const bool jv = j < L;
-                    const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
-                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s + ic;
-                    d2 c[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        c[q] = (jv && 64 * s + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
-                    double rx = 0.0, ry = 0.0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        ca[q].x += c[q].x * vj.x + c[q].y * vj.y;
-                        ca[q].y += c[q].x * vj.y - c[q].y * vj.x;
-                        if (64 * s + ic + 16 * q < j) {   // (then i < L: v[i] is live)
-                            const d2 vi = v[64 * s + ic + 16 * q];
-                            rx += c[q].x * vi.x - c[q].y * vi.y;
-                            ry += c[q].x * vi.y + c[q].y * vi.x;
-                        }
-                    }
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        rx += __shfl_xor(rx, o, 64);
-                        ry += __shfl_xor(ry, o, 64);
-                    }
-                    if (ic == 0 && jv) rowp[s * mt + j] = make_double2(rx, ry);
-                }
-                if (g0 < g1) flush();
-                __syncthreads();
-                for (int i = t; i < L; i += HB_THREADS) {
-                    const int si = i >> 6;
-                    int bs = 0;
-                    for (int q = 0; q < si; ++q) bs += ngr(q);
-                    const int be = bs + ngr(si);
-                    d2 acc = make_double2(0.0, 0.0);
-                    for (int ww = 0; ww < HB_NW; ++ww)   // the runs that cover strip si, in wave order
-                        if (ww * G / HB_NW < be && (ww + 1) * G / HB_NW > bs && ww * G / HB_NW < (ww + 1) * G / HB_NW)
-                            acc = cadd(acc, colp[(ww + si) * 64 + (i & 63)]);
-                    for (int q = 0; q <= si; ++q) acc = cadd(acc, rowp[q * mt + i]);
-                    const int r = k + 1 + i;
-                    for (int q = 0; q < p; ++q)
-                        acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
-                    w[i] = cmul(tau, acc);
-                }
-                __syncthreads();
-            }
-#else
             for (int i0 = 0; i0 < L; i0 += HB_COLS) {
                 const int i = i0 + col;
                 double ar = 0.0, ai = 0.0;
@@ -534,7 +425,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 }
                 __syncthreads();
             }
-#endif
             // w = p - (tau / 2) (p^H v) v
             double s2[2] = {0.0, 0.0};
             for (int i = t; i < L; i += HB_THREADS) {
@@ -562,11 +452,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 vq[q] = cj(Vp[q * mt + ci]);
                 wq[q] = cj(Wp[q * mt + ci]);
             }
-#if ACE_HB_LOWER
-            for (int j = i + (((rb - i) % HB_RB) + HB_RB) % HB_RB; j < L2; j += HB_RB) {   // rows j >= i
-#else
             for (int j = rb; j < L2; j += HB_RB) {
-#endif
                 const int rj = kn + j;
                 d2* cp = C + (long long)rj * mt + ci;
                 d2 c = *cp;
@@ -597,6 +483,13 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     }
     return cnt;
 }
+#ifndef ACE_TE_NEWTON
+#define ACE_TE_NEWTON 0
+#endif
+#ifndef ACE_TE_SWEEPS
+#define ACE_TE_SWEEPS 3
+#endif
+constexpr int TE_SWEEPS = ACE_TE_SWEEPS;   // inverse-iteration solves per eigenvector
 // 1 / x from the v_rcp_f64 seed and two Newton steps (~1 ulp; x finite and nonzero here)
 __device__ __forceinline__ double rcp_nr(double x) {
     double y = __builtin_amdgcn_rcp(x);
@@ -625,6 +518,38 @@ __device__ __forceinline__ void sturm_count2(const double* d, const double* e2, 
     c1 = n1;
 }
 
+// sturm_count2 with the logarithmic derivative of det(T - x I) at both points: S = sum_i q_i' / q_i, so
+// that x - 1 / S is Newton's step for the eigenvalue nearest x (q_i' = -1 + e^2 q_{i-1}' / q_{i-1}^2)
+__device__ __forceinline__ void sturm_newton2(const double* d, const double* e2, int n, double x0, double x1,
+                                              double pivmin, int& c0, int& c1, double& S0, double& S1) {
+    double q0 = d[0] - x0, q1 = d[0] - x1;
+    if (fabs(q0) < pivmin) q0 = -pivmin;
+    if (fabs(q1) < pivmin) q1 = -pivmin;
+    int n0 = q0 < 0.0, n1 = q1 < 0.0;
+    double r0 = rcp_nr(q0), r1 = rcp_nr(q1), p0 = -1.0, p1 = -1.0;
+    double s0 = -r0, s1 = -r1;
+    for (int i = 1; i < n; ++i) {
+        const double di = d[i], ei = e2[i - 1];
+        const double t0 = ei * r0, t1 = ei * r1;
+        q0 = (di - x0) - t0;
+        q1 = (di - x1) - t1;
+        p0 = fma(t0 * r0, p0, -1.0);
+        p1 = fma(t1 * r1, p1, -1.0);
+        if (fabs(q0) < pivmin) q0 = -pivmin;
+        if (fabs(q1) < pivmin) q1 = -pivmin;
+        r0 = rcp_nr(q0);
+        r1 = rcp_nr(q1);
+        s0 = fma(p0, r0, s0);
+        s1 = fma(p1, r1, s1);
+        n0 += q0 < 0.0;
+        n1 += q1 < 0.0;
+    }
+    c0 = n0;
+    c1 = n1;
+    S0 = s0;
+    S1 = s1;
+}
+
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
@@ -638,6 +563,9 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                                                      int* status, int status_off, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (active && !active[b]) return;
+#ifdef ACE_TE_STAMPS   // phase times of work-groups 0..3 (10 ns units): bisection, clusters, inverse iteration
+    const unsigned long long te0 = __builtin_amdgcn_s_memrealtime();
+#endif
     extern __shared__ double smem[];
     double* d = smem;
     double* e = smem + mt;
@@ -688,6 +616,52 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
+#if ACE_TE_NEWTON
+    // Trisection on Sturm counts until the bracket holds eigenvalue j alone, then Newton steps on det(T - x I)
+    // from both probe points (kept only inside the bracket, which the counts at the probes keep shrinking):
+    // the probes converge on the eigenvalue from both sides.  Every lane evaluates two chains with their
+    // derivatives per round, whichever phase it is in (no divergence between the phases).
+    for (int q = t; q < k; q += 256) {
+        const int j = mt - 1 - q;
+        double lo = gl, hi = gu, lamv = 0.0;
+        int clo = 0, chi = mt;
+        bool have = false;
+        double x0 = lo + (hi - lo) * (1.0 / 3.0), x1 = fmax(x0, hi - (hi - lo) * (1.0 / 3.0));
+        for (int it = 0; it < 200; ++it) {
+            int c0, c1;
+            double S0, S1;
+            sturm_newton2(d, e2, mt, x0, x1, pivmin, c0, c1, S0, S1);
+            // eigenvalue j lies below x iff more than j eigenvalues do
+            if (c1 > j) {
+                if (x1 < hi) { hi = x1; chi = c1; }
+            } else if (x1 > lo) { lo = x1; clo = c1; }
+            if (c0 > j) {
+                if (x0 < hi) { hi = x0; chi = c0; }
+            } else if (x0 > lo) { lo = x0; clo = c0; }
+            if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+            const double n0 = x0 - 1.0 / S0, n1 = x1 - 1.0 / S1;
+            const bool v0 = chi - clo == 1 && n0 > lo && n0 < hi, v1 = chi - clo == 1 && n1 > lo && n1 < hi;
+            if (v0 && v1 && fabs(n0 - n1) <= 2.0 * eps * fmax(fabs(n0), fabs(n1)) + pivmin) {
+                lamv = 0.5 * (n0 + n1);
+                have = true;
+                break;
+            }
+            const double stp = (hi - lo) * (1.0 / 3.0);
+            if (v0 && v1) {
+                x0 = fmin(n0, n1);
+                x1 = fmax(n0, n1);
+            } else if (v0 || v1) {   // the Newton point and the midpoint of the side it leaves open
+                const double nx = v0 ? n0 : n1, mid = 0.5 * (lo + hi);
+                x0 = fmin(nx, mid);
+                x1 = fmax(nx, mid);
+            } else {
+                x0 = lo + stp;
+                x1 = fmax(x0, hi - stp);
+            }
+        }
+        lam[q] = have ? lamv : 0.5 * (lo + hi);
+    }
+#else
     for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
@@ -709,7 +683,11 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         }
         lam[q] = 0.5 * (lo + hi);
     }
+#endif
     __syncthreads();
+#ifdef ACE_TE_STAMPS
+    const unsigned long long te1 = __builtin_amdgcn_s_memrealtime();
+#endif
     double* cl = base + lay.cl;
     if (t == 0) {
         int nc = 0;
@@ -779,7 +757,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
             // chain (they depend on the row index only), so the chain waits for one memory round trip per
             // block instead of one per row.  Same operations in the same order as the row-by-row form.
             constexpr int TE_PF = 8;
-            for (int sweep = 0; sweep < 3; ++sweep) {
+            for (int sweep = 0; sweep < TE_SWEEPS; ++sweep) {
                 double cur = at(5, 0);
                 for (int i0 = 0; i0 + 1 < mt; i0 += TE_PF) {  // dgttrs, L
                     double nx[TE_PF], fv[TE_PF], pv[TE_PF];
@@ -844,7 +822,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                     for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
                 }
                 const double inv = 1.0 / sqrt(nrm);
-                if (sweep < 2)
+                if (sweep < TE_SWEEPS - 1)
                     for (int i = 0; i < mt; ++i) at(5, i) *= inv;
                 else
                     for (int i = 0; i < mt; ++i) zq[i] = at(5, i) * inv;
@@ -852,6 +830,15 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         }
     }
     if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+#ifdef ACE_TE_STAMPS
+    __syncthreads();
+    if (t == 0 && b < 4) {
+        int mx = 0;
+        for (int c = 0; c < ncl; ++c) mx = max(mx, (int)(cl[c + 1] - cl[c]));
+        printf("trieig b %d mt %d k %d ncl %d maxcl %d lanes %d: bisect %llu invit %llu (x10ns)\n", b, mt, k, ncl, mx,
+               lay.lanes, te1 - te0, __builtin_amdgcn_s_memrealtime() - te1);
+    }
+#endif
 #ifdef ACE_DEBUG_SPEC
     __syncthreads();
     if (t == 0 && b < 2) {

@@ -483,13 +483,22 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     }
     return cnt;
 }
-#ifndef ACE_TE_NEWTON
-#define ACE_TE_NEWTON 0
+// Bisection stops at LAPACK dstebz's width max(2 ulp |lambda|, ulp ||T||, pivmin) (its default ABSTOL <= 0); the
+// relative-only test (ACE_TE_ABSTOL=0) refined eigenvalues far below ||T|| to their own ulp, ~20 rounds more
+#ifndef ACE_TE_ABSTOL
+#define ACE_TE_ABSTOL 1
 #endif
 #ifndef ACE_TE_SWEEPS
-#define ACE_TE_SWEEPS 3
+#define ACE_TE_SWEEPS 2
 #endif
-constexpr int TE_SWEEPS = ACE_TE_SWEEPS;   // inverse-iteration solves per eigenvector
+// inverse-iteration solves per eigenvector: with the eigenvalue to full precision, one solve leaves the other
+// eigenvectors at <= eps ||T|| / gap of the vector (gap >= kOrtol ||T||, closer ones are a cluster and projected
+// out), the second squares that (r05: 3 -> 2, PhaseLift 67.6 -> 69.3 rec/s; LAPACK dstein stops 2 solves after
+// its growth test passes)
+constexpr int TE_SWEEPS = ACE_TE_SWEEPS;
+#ifndef ACE_TE_PF
+#define ACE_TE_PF 8
+#endif
 // 1 / x from the v_rcp_f64 seed and two Newton steps (~1 ulp; x finite and nonzero here)
 __device__ __forceinline__ double rcp_nr(double x) {
     double y = __builtin_amdgcn_rcp(x);
@@ -518,42 +527,10 @@ __device__ __forceinline__ void sturm_count2(const double* d, const double* e2, 
     c1 = n1;
 }
 
-// sturm_count2 with the logarithmic derivative of det(T - x I) at both points: S = sum_i q_i' / q_i, so
-// that x - 1 / S is Newton's step for the eigenvalue nearest x (q_i' = -1 + e^2 q_{i-1}' / q_{i-1}^2)
-__device__ __forceinline__ void sturm_newton2(const double* d, const double* e2, int n, double x0, double x1,
-                                              double pivmin, int& c0, int& c1, double& S0, double& S1) {
-    double q0 = d[0] - x0, q1 = d[0] - x1;
-    if (fabs(q0) < pivmin) q0 = -pivmin;
-    if (fabs(q1) < pivmin) q1 = -pivmin;
-    int n0 = q0 < 0.0, n1 = q1 < 0.0;
-    double r0 = rcp_nr(q0), r1 = rcp_nr(q1), p0 = -1.0, p1 = -1.0;
-    double s0 = -r0, s1 = -r1;
-    for (int i = 1; i < n; ++i) {
-        const double di = d[i], ei = e2[i - 1];
-        const double t0 = ei * r0, t1 = ei * r1;
-        q0 = (di - x0) - t0;
-        q1 = (di - x1) - t1;
-        p0 = fma(t0 * r0, p0, -1.0);
-        p1 = fma(t1 * r1, p1, -1.0);
-        if (fabs(q0) < pivmin) q0 = -pivmin;
-        if (fabs(q1) < pivmin) q1 = -pivmin;
-        r0 = rcp_nr(q0);
-        r1 = rcp_nr(q1);
-        s0 = fma(p0, r0, s0);
-        s1 = fma(p1, r1, s1);
-        n0 += q0 < 0.0;
-        n1 += q1 < 0.0;
-    }
-    c0 = n0;
-    c1 = n1;
-    S0 = s0;
-    S1 = s1;
-}
-
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
-// LU of LAPACK dgttrf/dgttrs, three solves, one thread per eigenvalue cluster with the
+// LU of LAPACK dgttrf/dgttrs, TE_SWEEPS solves, one thread per eigenvalue cluster with the
 // cluster's earlier vectors projected out after every solve (as dstein).  Clusters are runs of
 // eigenvalues closer than kOrtol ||T||.  LAPACK's dstein uses 1e-3; on PhaseLift's prox inputs
 // that chains up to ~100 eigenvalues into one sequential cluster, while at 1e-5 the largest
@@ -616,57 +593,15 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
-#if ACE_TE_NEWTON
-    // Trisection on Sturm counts until the bracket holds eigenvalue j alone, then Newton steps on det(T - x I)
-    // from both probe points (kept only inside the bracket, which the counts at the probes keep shrinking):
-    // the probes converge on the eigenvalue from both sides.  Every lane evaluates two chains with their
-    // derivatives per round, whichever phase it is in (no divergence between the phases).
-    for (int q = t; q < k; q += 256) {
-        const int j = mt - 1 - q;
-        double lo = gl, hi = gu, lamv = 0.0;
-        int clo = 0, chi = mt;
-        bool have = false;
-        double x0 = lo + (hi - lo) * (1.0 / 3.0), x1 = fmax(x0, hi - (hi - lo) * (1.0 / 3.0));
-        for (int it = 0; it < 200; ++it) {
-            int c0, c1;
-            double S0, S1;
-            sturm_newton2(d, e2, mt, x0, x1, pivmin, c0, c1, S0, S1);
-            // eigenvalue j lies below x iff more than j eigenvalues do
-            if (c1 > j) {
-                if (x1 < hi) { hi = x1; chi = c1; }
-            } else if (x1 > lo) { lo = x1; clo = c1; }
-            if (c0 > j) {
-                if (x0 < hi) { hi = x0; chi = c0; }
-            } else if (x0 > lo) { lo = x0; clo = c0; }
-            if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
-            const double n0 = x0 - 1.0 / S0, n1 = x1 - 1.0 / S1;
-            const bool v0 = chi - clo == 1 && n0 > lo && n0 < hi, v1 = chi - clo == 1 && n1 > lo && n1 < hi;
-            if (v0 && v1 && fabs(n0 - n1) <= 2.0 * eps * fmax(fabs(n0), fabs(n1)) + pivmin) {
-                lamv = 0.5 * (n0 + n1);
-                have = true;
-                break;
-            }
-            const double stp = (hi - lo) * (1.0 / 3.0);
-            if (v0 && v1) {
-                x0 = fmin(n0, n1);
-                x1 = fmax(n0, n1);
-            } else if (v0 || v1) {   // the Newton point and the midpoint of the side it leaves open
-                const double nx = v0 ? n0 : n1, mid = 0.5 * (lo + hi);
-                x0 = fmin(nx, mid);
-                x1 = fmax(nx, mid);
-            } else {
-                x0 = lo + stp;
-                x1 = fmax(x0, hi - stp);
-            }
-        }
-        lam[q] = have ? lamv : 0.5 * (lo + hi);
-    }
-#else
     for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
         for (int it = 0; it < 200; ++it) {
+#if ACE_TE_ABSTOL   // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
+            if (hi - lo <= fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), fmax(eps * tn, pivmin))) break;
+#else
             if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+#endif
             const double stp = (hi - lo) * (1.0 / 3.0);
             const double x0 = lo + stp, x1 = fmax(x0, hi - stp);
             int c0, c1;
@@ -683,7 +618,6 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         }
         lam[q] = 0.5 * (lo + hi);
     }
-#endif
     __syncthreads();
 #ifdef ACE_TE_STAMPS
     const unsigned long long te1 = __builtin_amdgcn_s_memrealtime();
@@ -756,7 +690,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
             // other; the loads of a block of TE_PF rows are issued together ahead of the block's dependent
             // chain (they depend on the row index only), so the chain waits for one memory round trip per
             // block instead of one per row.  Same operations in the same order as the row-by-row form.
-            constexpr int TE_PF = 8;
+            constexpr int TE_PF = ACE_TE_PF;
             for (int sweep = 0; sweep < TE_SWEEPS; ++sweep) {
                 double cur = at(5, 0);
                 for (int i0 = 0; i0 + 1 < mt; i0 += TE_PF) {  // dgttrs, L

@@ -864,6 +864,17 @@ def bench_phaselift(args, dev, rank, world):
              "apply_A": "A(z) GEMM", "ystep": "x update, backtracking", "final": "final eig + map"}
     if roof:
         roof["kernel"] = names.get(roof["kernel"], roof["kernel"])
+        if roof.get("traffic") and roof.get("traffic_kernel") == "hetrd":
+            # the traffic is the blocked tridiagonalisation's (PMC per launch of bsz matrices of order d): against
+            # its compulsory bytes (read C, write the reflectors) and against the one-stage reduction's floor,
+            # which reads the trailing matrix once per column (d^3 / 3 entries) besides
+            d = min(m, tx * tx)
+            comp = bsz * 2 * 16 * d * d
+            lvl2 = bsz * 16 * (d ** 3 / 3 + 2 * d * d)
+            roof["traffic_algorithmic"] = comp
+            roof["traffic_per_algorithmic"] = round(roof["traffic"] / comp, 3)
+            roof["traffic_level2_floor"] = round(lvl2)
+            roof["traffic_per_level2_floor"] = round(roof["traffic"] / lvl2, 3)
     line = {
         "metric": PL_METRIC, "value": round(world * bsz * args.steps / elapsed, 3), "unit": "recoveries/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

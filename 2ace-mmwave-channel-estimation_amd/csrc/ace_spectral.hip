@@ -293,6 +293,9 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_NB
 #define ACE_HB_NB 4   // (r05: 4 against 8 at 1024 threads: PhaseLift 64.6 -> 67.5 rec/s; 2, and 512 / 256 threads, slower)
 #endif
+#ifndef ACE_HB_ADAPT
+#define ACE_HB_ADAPT 0
+#endif
 #ifndef ACE_HB_THREADS
 #define ACE_HB_THREADS 1024
 #endif
@@ -400,24 +403,29 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
-            for (int i0 = 0; i0 < L; i0 += HB_COLS) {
-                const int i = i0 + col;
+#if ACE_HB_ADAPT   // the map follows the trailing order: L rounded up to 64 columns (<= HB_COLS), the rest rows
+            const int ncol = min(HB_COLS, (L + 63) & ~63), nrb = HB_THREADS / ncol, acol = t % ncol, arb = t / ncol;
+#else
+            const int ncol = HB_COLS, nrb = HB_RB, acol = col, arb = rb;
+#endif
+            d2* partf = &part[0][0];   // [nrb][ncol]
+            for (int i0 = 0; i0 < L; i0 += ncol) {
+                const int i = i0 + acol;
                 double ar = 0.0, ai = 0.0;
-                if (i < L) {
+                if (i < L && arb < nrb) {
                     const d2* cc = C + r0 + i;
 #pragma unroll 4
-                    for (int j = rb; j < L; j += HB_RB) {
+                    for (int j = arb; j < L; j += nrb) {
                         const d2 c = cc[(long long)j * mt], vj = v[j];
                         ar += c.x * vj.x + c.y * vj.y;
                         ai += c.x * vj.y - c.y * vj.x;
                     }
                 }
-                part[rb][col] = make_double2(ar, ai);
+                if (arb < nrb) partf[arb * ncol + acol] = make_double2(ar, ai);
                 __syncthreads();
-                if (rb == 0 && i < L) {
-                    d2 acc = part[0][col];
-#pragma unroll
-                    for (int q = 1; q < HB_RB; ++q) acc = cadd(acc, part[q][col]);
+                if (arb == 0 && i < L) {
+                    d2 acc = partf[acol];
+                    for (int q = 1; q < nrb; ++q) acc = cadd(acc, partf[q * ncol + acol]);
                     const int r = k + 1 + i;
                     for (int q = 0; q < p; ++q)
                         acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
@@ -442,9 +450,14 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
         }
         // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
         const int kn = k0 + nbp, L2 = mt - kn;
-        for (int i0 = 0; i0 < L2; i0 += HB_COLS) {
-            const int i = i0 + col;
-            if (i >= L2) continue;
+#if ACE_HB_ADAPT
+        const int ncol2 = min(HB_COLS, (L2 + 63) & ~63), nrb2 = HB_THREADS / ncol2, tcol = t % ncol2, trb = t / ncol2;
+#else
+        const int ncol2 = HB_COLS, nrb2 = HB_RB, tcol = col, trb = rb;
+#endif
+        for (int i0 = 0; i0 < L2; i0 += ncol2) {
+            const int i = i0 + tcol;
+            if (i >= L2 || trb >= nrb2) continue;
             const int ci = kn + i;
             d2 vq[HB_NB], wq[HB_NB];
 #pragma unroll
@@ -452,7 +465,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 vq[q] = cj(Vp[q * mt + ci]);
                 wq[q] = cj(Wp[q * mt + ci]);
             }
-            for (int j = rb; j < L2; j += HB_RB) {
+            for (int j = trb; j < L2; j += nrb2) {
                 const int rj = kn + j;
                 d2* cp = C + (long long)rj * mt + ci;
                 d2 c = *cp;
@@ -488,6 +501,10 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
 #ifndef ACE_TE_ABSTOL
 #define ACE_TE_ABSTOL 1
 #endif
+#ifndef ACE_TE_GRID
+#define ACE_TE_GRID 0   // (0: off; else the number of grid cells, a multiple of 2)
+#endif
+constexpr int TE_GRID = ACE_TE_GRID > 0 ? ACE_TE_GRID : 2;
 #ifndef ACE_TE_SWEEPS
 #define ACE_TE_SWEEPS 2
 #endif
@@ -593,9 +610,37 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
+#if ACE_TE_GRID
+    // one shared round first: Sturm counts at TE_GRID + 1 even points of [gl, gu] (two per thread), so that
+    // every eigenvalue starts from its grid cell instead of the whole interval (log3(TE_GRID) rounds fewer)
+    __shared__ int gcnt[TE_GRID + 1];
+    const double gh = (gu - gl) / TE_GRID;
+    for (int g = 1 + 2 * t; g <= TE_GRID; g += 512) {
+        int ca, cb;
+        sturm_count2(d, e2, mt, gl + g * gh, gl + min(g + 1, TE_GRID) * gh, pivmin, ca, cb);
+        gcnt[g] = ca;
+        if (g + 1 <= TE_GRID) gcnt[g + 1] = cb;
+    }
+    if (t == 0) gcnt[0] = 0;
+    __syncthreads();
+#endif
     for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
+#if ACE_TE_GRID
+        {   // the first grid point with more than j eigenvalues below it (counts are monotone in x)
+            int a0 = 0, a1 = TE_GRID;
+            while (a1 - a0 > 1) {
+                const int am = (a0 + a1) >> 1;
+                if (gcnt[am] > j) a1 = am;
+                else a0 = am;
+            }
+            if (gcnt[a1] > j) {
+                lo = gl + a0 * gh;
+                if (a1 < TE_GRID) hi = gl + a1 * gh;
+            }
+        }
+#endif
         for (int it = 0; it < 200; ++it) {
 #if ACE_TE_ABSTOL   // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
             if (hi - lo <= fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), fmax(eps * tn, pivmin))) break;

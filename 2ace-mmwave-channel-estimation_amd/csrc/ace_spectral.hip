@@ -293,8 +293,8 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_NB
 #define ACE_HB_NB 4   // (r05: 4 against 8 at 1024 threads: PhaseLift 64.6 -> 67.5 rec/s; 2, and 512 / 256 threads, slower)
 #endif
-#ifndef ACE_HB_ADAPT
-#define ACE_HB_ADAPT 0
+#ifndef ACE_HB_UNROLL
+#define ACE_HB_UNROLL 4   // rows of the Hermitian product in flight per thread
 #endif
 #ifndef ACE_HB_THREADS
 #define ACE_HB_THREADS 1024
@@ -303,7 +303,18 @@ constexpr int HB_NB = ACE_HB_NB;             // panel width
 constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
 constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
 constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
-size_t hetrd_blk_lds(int mt) { return (size_t)mt * 16 * (2 * HB_NB + 2); }
+// ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
+// the trailing matrix -- half the bytes of the full square (the kernel is bound by them)
+#ifndef ACE_HB_LOWER
+#define ACE_HB_LOWER 0
+#endif
+constexpr int HB_NW = HB_THREADS / 64;   // waves
+__host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
+size_t hetrd_blk_lds(int mt) {
+    size_t b = (size_t)mt * 16 * (2 * HB_NB + 2);
+    if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
+    return b;
+}
 __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
@@ -313,7 +324,12 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
     d2* v = Wp + HB_NB * mt;                // current reflector, entry i = row k + 1 + i
     d2* w = v + mt;
     __shared__ double red[16 * 4 * HB_NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
+#if ACE_HB_LOWER
+    d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
+    d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
+#else
     __shared__ d2 part[HB_RB][HB_COLS];
+#endif
     __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
@@ -332,10 +348,17 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             double s1[1] = {0.0};
             for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
+#if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
+                d2 a = C[(long long)c * mt + k];
+                for (int q = 0; q < p; ++q)
+                    a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
+                v[i] = a;   // x_i = A[k + 1 + i][k]
+#else
                 d2 a = C[(long long)k * mt + c];
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + c])), cmul(Wp[q * mt + k], cj(Vp[q * mt + c]))));
                 v[i] = cj(a);   // x_i = A[k + 1 + i][k]
+#endif
                 if (i > 0) s1[0] += cabs2(a);
             }
             block_sum<1>(s1, red);
@@ -403,18 +426,97 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
-#if ACE_HB_ADAPT   // the map follows the trailing order: L rounded up to 64 columns (<= HB_COLS), the rest rows
-            const int ncol = min(HB_COLS, (L + 63) & ~63), nrb = HB_THREADS / ncol, acol = t % ncol, arb = t / ncol;
+#if ACE_HB_LOWER
+            // From the lower triangle only: element (j, i), j >= i, adds conj(c) v_j to p_i (column sums) and,
+            // for j > i, c v_i to p_j (row sums).  Tasks are 4-row groups of 64-column strips (strip s: columns
+            // 64s.., rows 64s..L-1), dealt to the waves in contiguous runs; lane (jr, ic) reads row jr of the
+            // group at columns ic + 16q (four 256-B rows per load).  A row's sum over a strip is reduced over
+            // the 16 ic lanes; a wave's column sums over its run in a strip over the 4 jr lanes at the end of
+            // the run (slot wave + strip: unique, since the runs are contiguous).
+            {
+                const int ns = hb_strips(L), wv = t >> 6, jr = (t & 63) >> 4, ic = t & 15;
+                auto ngr = [&](int s) { return (L - 64 * s + 3) >> 2; };
+                int G = 0;
+                for (int s = 0; s < ns; ++s) G += ngr(s);
+                const int g0 = wv * G / HB_NW, g1 = (wv + 1) * G / HB_NW;
+                const d2* C22 = C + r0;
+                int s = 0, gb = 0;
+                while (s < ns && g0 >= gb + ngr(s)) gb += ngr(s++);
+                d2 ca[4];
+                auto strip_start = [&]() {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) ca[q] = make_double2(0.0, 0.0);
+                };
+                auto flush = [&]() {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        double x = ca[q].x, y = ca[q].y;
+#pragma unroll
+                        for (int o = 16; o < 64; o <<= 1) {
+                            x += __shfl_xor(x, o, 64);
+                            y += __shfl_xor(y, o, 64);
+                        }
+                        if (jr == 0) colp[(wv + s) * 64 + ic + 16 * q] = make_double2(x, y);
+                    }
+                };
+                if (g0 < g1) strip_start();
+                for (int g = g0; g < g1; ++g) {
+                    if (g - gb >= ngr(s)) {
+                        flush();
+                        gb += ngr(s++);
+                        strip_start();
+                    }
+                    const int j = 64 * s + 4 * (g - gb) + jr;
+                    const bool jv = j < L;
+                    const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
+                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s + ic;
+                    d2 c[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        c[q] = (jv && 64 * s + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
+                    double rx = 0.0, ry = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        ca[q].x += c[q].x * vj.x + c[q].y * vj.y;
+                        ca[q].y += c[q].x * vj.y - c[q].y * vj.x;
+                        if (64 * s + ic + 16 * q < j) {   // (then i < L: v[i] is live)
+                            const d2 vi = v[64 * s + ic + 16 * q];
+                            rx += c[q].x * vi.x - c[q].y * vi.y;
+                            ry += c[q].x * vi.y + c[q].y * vi.x;
+                        }
+                    }
+                    rx = bsum16(rx);   // over the 16 ic lanes: one DPP row
+                    ry = bsum16(ry);
+                    if (ic == 0 && jv) rowp[s * mt + j] = make_double2(rx, ry);
+                }
+                if (g0 < g1) flush();
+                __syncthreads();
+                for (int i = t; i < L; i += HB_THREADS) {
+                    const int si = i >> 6;
+                    int bs = 0;
+                    for (int q = 0; q < si; ++q) bs += ngr(q);
+                    const int be = bs + ngr(si);
+                    d2 acc = make_double2(0.0, 0.0);
+                    for (int ww = 0; ww < HB_NW; ++ww)   // the runs that cover strip si, in wave order
+                        if (ww * G / HB_NW < be && (ww + 1) * G / HB_NW > bs && ww * G / HB_NW < (ww + 1) * G / HB_NW)
+                            acc = cadd(acc, colp[(ww + si) * 64 + (i & 63)]);
+                    for (int q = 0; q <= si; ++q) acc = cadd(acc, rowp[q * mt + i]);
+                    const int r = k + 1 + i;
+                    for (int q = 0; q < p; ++q)
+                        acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
+                    w[i] = cmul(tau, acc);
+                }
+                __syncthreads();
+            }
 #else
             const int ncol = HB_COLS, nrb = HB_RB, acol = col, arb = rb;
-#endif
             d2* partf = &part[0][0];   // [nrb][ncol]
             for (int i0 = 0; i0 < L; i0 += ncol) {
                 const int i = i0 + acol;
                 double ar = 0.0, ai = 0.0;
                 if (i < L && arb < nrb) {
                     const d2* cc = C + r0 + i;
-#pragma unroll 4
+#pragma unroll ACE_HB_UNROLL
                     for (int j = arb; j < L; j += nrb) {
                         const d2 c = cc[(long long)j * mt], vj = v[j];
                         ar += c.x * vj.x + c.y * vj.y;
@@ -433,6 +535,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 }
                 __syncthreads();
             }
+#endif
             // w = p - (tau / 2) (p^H v) v
             double s2[2] = {0.0, 0.0};
             for (int i = t; i < L; i += HB_THREADS) {
@@ -450,11 +553,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
         }
         // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
         const int kn = k0 + nbp, L2 = mt - kn;
-#if ACE_HB_ADAPT
-        const int ncol2 = min(HB_COLS, (L2 + 63) & ~63), nrb2 = HB_THREADS / ncol2, tcol = t % ncol2, trb = t / ncol2;
-#else
         const int ncol2 = HB_COLS, nrb2 = HB_RB, tcol = col, trb = rb;
-#endif
         for (int i0 = 0; i0 < L2; i0 += ncol2) {
             const int i = i0 + tcol;
             if (i >= L2 || trb >= nrb2) continue;
@@ -465,7 +564,11 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 vq[q] = cj(Vp[q * mt + ci]);
                 wq[q] = cj(Wp[q * mt + ci]);
             }
+#if ACE_HB_LOWER
+            for (int j = i + (((trb - i) % nrb2) + nrb2) % nrb2; j < L2; j += nrb2) {   // rows j >= i
+#else
             for (int j = trb; j < L2; j += nrb2) {
+#endif
                 const int rj = kn + j;
                 d2* cp = C + (long long)rj * mt + ci;
                 d2 c = *cp;
@@ -502,7 +605,7 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
 #define ACE_TE_ABSTOL 1
 #endif
 #ifndef ACE_TE_GRID
-#define ACE_TE_GRID 0   // (0: off; else the number of grid cells, a multiple of 2)
+#define ACE_TE_GRID 512   // (0: off; else the number of grid cells, even; r05: PhaseLift 69.4 -> 69.9 rec/s)
 #endif
 constexpr int TE_GRID = ACE_TE_GRID > 0 ? ACE_TE_GRID : 2;
 #ifndef ACE_TE_SWEEPS

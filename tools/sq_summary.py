@@ -9,7 +9,7 @@ def main(*paths):
             k = k.split("(int")[0].split("(ace::")[0][:40]
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     for k, d in sorted(agg.items()):
-        if not any(s in k for s in ("zgemm", "zstep", "pre_", "ystep", "gemv", "inv_ipk", "gyk", "i8ah", "i8a_")):
+        if not any(s in k for s in ("zgemm", "zstep", "pre_", "ystep", "gemv", "inv_ipk", "gyk", "i8ah", "i8a_", "hetrd", "trieig", "backxf", "wy_")):
             continue
         wc = d.get("SQ_WAVE_CYCLES", 0) or 1
         print(f"{k:40s} wave_cycles={wc:.3e}")

@@ -304,9 +304,9 @@ constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
 constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
 constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
 // ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
-// the trailing matrix -- half the bytes of the full square (the kernel is bound by them)
+// the trailing matrix: half the bytes of the full square (row sums reduced across each DPP row of 16 lanes)
 #ifndef ACE_HB_LOWER
-#define ACE_HB_LOWER 0
+#define ACE_HB_LOWER 1   // (r05: half the HBM bytes of the full square, 57.8 -> 28.5 GB per 512-matrix launch; 70.3 -> 71.4 rec/s)
 #endif
 constexpr int HB_NW = HB_THREADS / 64;   // waves
 __host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
@@ -608,6 +608,9 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
 #define ACE_TE_GRID 512   // (0: off; else the number of grid cells, even; r05: PhaseLift 69.4 -> 69.9 rec/s)
 #endif
 constexpr int TE_GRID = ACE_TE_GRID > 0 ? ACE_TE_GRID : 2;
+#ifndef ACE_TE_FUSE
+#define ACE_TE_FUSE 1
+#endif
 #ifndef ACE_TE_SWEEPS
 #define ACE_TE_SWEEPS 2
 #endif
@@ -839,14 +842,17 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
             // chain (they depend on the row index only), so the chain waits for one memory round trip per
             // block instead of one per row.  Same operations in the same order as the row-by-row form.
             constexpr int TE_PF = ACE_TE_PF;
+            // the normalisation of a solve's result is applied as the next solve loads it (sc): the same
+            // products fl(y inv) as a separate scaling pass, without its round trips
+            double sc = 1.0;
             for (int sweep = 0; sweep < TE_SWEEPS; ++sweep) {
-                double cur = at(5, 0);
+                double cur = ACE_TE_FUSE ? at(5, 0) * sc : at(5, 0);
                 for (int i0 = 0; i0 + 1 < mt; i0 += TE_PF) {  // dgttrs, L
                     double nx[TE_PF], fv[TE_PF], pv[TE_PF];
 #pragma unroll
                     for (int u = 0; u < TE_PF; ++u) {
                         const int i = min(i0 + u, mt - 2);
-                        nx[u] = at(5, i + 1);
+                        nx[u] = ACE_TE_FUSE ? at(5, i + 1) * sc : at(5, i + 1);
                         fv[u] = at(0, i);
                         pv[u] = at(4, i);
                     }
@@ -904,10 +910,26 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                     for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
                 }
                 const double inv = 1.0 / sqrt(nrm);
+#if ACE_TE_FUSE
+                if (sweep < TE_SWEEPS - 1) {
+                    sc = inv;
+                } else {   // the vector out, 32 rows per round trip
+                    constexpr int TE_CP = 32;
+                    for (int i0 = 0; i0 < mt; i0 += TE_CP) {
+                        double tv[TE_CP];
+#pragma unroll
+                        for (int u = 0; u < TE_CP; ++u) tv[u] = at(5, min(i0 + u, mt - 1));
+#pragma unroll
+                        for (int u = 0; u < TE_CP; ++u)
+                            if (i0 + u < mt) zq[i0 + u] = tv[u] * inv;
+                    }
+                }
+#else
                 if (sweep < TE_SWEEPS - 1)
                     for (int i = 0; i < mt; ++i) at(5, i) *= inv;
                 else
                     for (int i = 0; i < mt; ++i) zq[i] = at(5, i) * inv;
+#endif
             }
         }
     }

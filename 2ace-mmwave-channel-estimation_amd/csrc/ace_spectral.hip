@@ -306,7 +306,7 @@ constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
 // ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
 // the trailing matrix: half the bytes of the full square (row sums reduced across each DPP row of 16 lanes)
 #ifndef ACE_HB_LOWER
-#define ACE_HB_LOWER 1   // (r05: half the HBM bytes of the full square, 57.8 -> 28.5 GB per 512-matrix launch; 70.3 -> 71.4 rec/s)
+#define ACE_HB_LOWER 1   // (r05: half the HBM bytes of the full square, 60.6 -> 29.8 GB per 512-matrix launch; 70.3 -> 71.4 rec/s)
 #endif
 constexpr int HB_NW = HB_THREADS / 64;   // waves
 __host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }

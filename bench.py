@@ -867,10 +867,10 @@ def bench_phaselift(args, dev, rank, world):
         if roof.get("traffic") and roof.get("traffic_kernel") == "hetrd":
             # the traffic is the blocked tridiagonalisation's (PMC per launch of bsz matrices of order d): against
             # its compulsory bytes (read C, write the reflectors) and against the one-stage reduction's floor,
-            # which reads the trailing matrix once per column (d^3 / 3 entries) besides
+            # which reads the lower triangle of the trailing matrix once per column (d^3 / 6 entries) besides
             d = min(m, tx * tx)
             comp = bsz * 2 * 16 * d * d
-            lvl2 = bsz * 16 * (d ** 3 / 3 + 2 * d * d)
+            lvl2 = bsz * 16 * (d ** 3 / 6 + 2 * d * d)
             roof["traffic_algorithmic"] = comp
             roof["traffic_per_algorithmic"] = round(roof["traffic"] / comp, 3)
             roof["traffic_level2_floor"] = round(lvl2)

@@ -293,6 +293,16 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_NB
 #define ACE_HB_NB 4   // (r05: 4 against 8 at 1024 threads: PhaseLift 64.6 -> 67.5 rec/s; 2, and 512 / 256 threads, slower)
 #endif
+#ifndef ACE_HB_MPF
+#define ACE_HB_MPF 0   // lower-triangle product: one task's loads ahead
+#endif
+#ifndef ACE_HB_TPAIR
+#define ACE_HB_TPAIR 0   // trailing update by column pairs (balanced lower triangle)
+#endif
+#ifndef ACE_HB_TB
+#define ACE_HB_TB 1   // trailing-update rows per memory round trip
+#endif
+constexpr int HB_TB = ACE_HB_TB;
 #ifndef ACE_HB_UNROLL
 #define ACE_HB_UNROLL 4   // rows of the Hermitian product in flight per thread
 #endif
@@ -460,6 +470,18 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     }
                 };
                 if (g0 < g1) strip_start();
+                auto load_task = [&](int g, int s_, int gb_, d2 (&cc)[4]) {
+                    const int j = 64 * s_ + 4 * (g - gb_) + jr;
+                    const bool jv = j < L;
+                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s_ + ic;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        cc[q] = (jv && 64 * s_ + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
+                };
+#if ACE_HB_MPF   // the next task's loads issued before this task's sums
+                d2 cn[4];
+                if (g0 < g1) load_task(g0, s, gb, cn);
+#endif
                 for (int g = g0; g < g1; ++g) {
                     if (g - gb >= ngr(s)) {
                         flush();
@@ -469,11 +491,18 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     const int j = 64 * s + 4 * (g - gb) + jr;
                     const bool jv = j < L;
                     const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
-                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s + ic;
                     d2 c[4];
+#if ACE_HB_MPF
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        c[q] = (jv && 64 * s + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
+                    for (int q = 0; q < 4; ++q) c[q] = cn[q];
+                    if (g + 1 < g1) {
+                        int s2 = s, gb2 = gb;
+                        if (g + 1 - gb2 >= ngr(s2)) gb2 += ngr(s2++);
+                        load_task(g + 1, s2, gb2, cn);
+                    }
+#else
+                    load_task(g, s, gb, c);
+#endif
                     double rx = 0.0, ry = 0.0;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -553,6 +582,52 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
         }
         // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
         const int kn = k0 + nbp, L2 = mt - kn;
+#if ACE_HB_LOWER && ACE_HB_TPAIR
+        // the lower triangle's columns in pairs (i, L2 - 1 - i): every thread of a pair's HB_THREADS / 128 row groups
+        // updates L2 + 1 entries over the two columns (one column from 0 would do L2 alone)
+        {
+            constexpr int PRB = HB_THREADS / 128;
+            const int np = (L2 + 1) >> 1, pp = t % 128, prb = t / 128;
+            for (int p0 = 0; p0 < np; p0 += 128) {
+                const int pi = p0 + pp;
+                if (pi >= np) continue;
+#pragma unroll 1
+                for (int side = 0; side < 2; ++side) {
+                    const int i = side ? L2 - 1 - pi : pi;
+                    if (side && i == pi) break;   // the middle column of an odd order
+                    const int ci = kn + i;
+                    d2 vq[HB_NB], wq[HB_NB];
+#pragma unroll
+                    for (int q = 0; q < HB_NB; ++q) {
+                        vq[q] = cj(Vp[q * mt + ci]);
+                        wq[q] = cj(Wp[q * mt + ci]);
+                    }
+                    const int js = i + (((prb - i) % PRB) + PRB) % PRB;
+                    for (int j0 = js; j0 < L2; j0 += HB_TB * PRB) {
+                        d2 cb[HB_TB];
+#pragma unroll
+                        for (int u = 0; u < HB_TB; ++u) {
+                            const int j = j0 + u * PRB;
+                            cb[u] = j < L2 ? C[(long long)(kn + j) * mt + ci] : make_double2(0.0, 0.0);
+                        }
+#pragma unroll
+                        for (int u = 0; u < HB_TB; ++u) {
+                            const int j = j0 + u * PRB;
+                            if (j >= L2) break;
+                            const int rj = kn + j;
+                            d2 c = cb[u];
+#pragma unroll
+                            for (int q = 0; q < HB_NB; ++q)
+                                c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
+                            C[(long long)rj * mt + ci] = c;
+                        }
+                    }
+                }
+            }
+        }
+        if (0)
+#endif
+        {
         const int ncol2 = HB_COLS, nrb2 = HB_RB, tcol = col, trb = rb;
         for (int i0 = 0; i0 < L2; i0 += ncol2) {
             const int i = i0 + tcol;
@@ -565,18 +640,31 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 wq[q] = cj(Wp[q * mt + ci]);
             }
 #if ACE_HB_LOWER
-            for (int j = i + (((trb - i) % nrb2) + nrb2) % nrb2; j < L2; j += nrb2) {   // rows j >= i
+            const int js = i + (((trb - i) % nrb2) + nrb2) % nrb2;   // rows j >= i
 #else
-            for (int j = trb; j < L2; j += nrb2) {
+            const int js = trb;
 #endif
-                const int rj = kn + j;
-                d2* cp = C + (long long)rj * mt + ci;
-                d2 c = *cp;
+            // HB_TB rows per memory round trip: their loads issued together ahead of the updates and stores
+            for (int j0 = js; j0 < L2; j0 += HB_TB * nrb2) {
+                d2 cb[HB_TB];
 #pragma unroll
-                for (int q = 0; q < HB_NB; ++q)
-                    c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
-                *cp = c;
+                for (int u = 0; u < HB_TB; ++u) {
+                    const int j = j0 + u * nrb2;
+                    cb[u] = j < L2 ? C[(long long)(kn + j) * mt + ci] : make_double2(0.0, 0.0);
+                }
+#pragma unroll
+                for (int u = 0; u < HB_TB; ++u) {
+                    const int j = j0 + u * nrb2;
+                    if (j >= L2) break;
+                    const int rj = kn + j;
+                    d2 c = cb[u];
+#pragma unroll
+                    for (int q = 0; q < HB_NB; ++q)
+                        c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
+                    C[(long long)rj * mt + ci] = c;
+                }
             }
+        }
         }
         __syncthreads();
     }

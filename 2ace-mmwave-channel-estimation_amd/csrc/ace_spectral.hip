@@ -291,19 +291,13 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 // the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
 // d, e, tau and reflector k in row k of C.
 #ifndef ACE_HB_NB
-#define ACE_HB_NB 4   // (r05: 4 against 8 at 1024 threads: PhaseLift 64.6 -> 67.5 rec/s; 2, and 512 / 256 threads, slower)
-#endif
-#ifndef ACE_HB_MPF
-#define ACE_HB_MPF 0   // lower-triangle product: one task's loads ahead
-#endif
-#ifndef ACE_HB_PCOL
-#define ACE_HB_PCOL 0   // (with HB_TPAIR) the next panel's columns kept in LDS by the trailing update
+#define ACE_HB_NB 2   // (r05: full square 4 against 8: PhaseLift 64.6 -> 67.5; lower triangle + pair trailing update 2 against 4: +1.5 %)
 #endif
 #ifndef ACE_HB_TPAIR
-#define ACE_HB_TPAIR 0   // trailing update by column pairs (balanced lower triangle)
+#define ACE_HB_TPAIR 1   // trailing update by column pairs (balanced lower triangle; r05: +3 %)
 #endif
 #ifndef ACE_HB_TB
-#define ACE_HB_TB 1   // trailing-update rows per memory round trip
+#define ACE_HB_TB 4   // trailing-update rows per memory round trip
 #endif
 constexpr int HB_TB = ACE_HB_TB;
 #ifndef ACE_HB_UNROLL
@@ -326,7 +320,6 @@ __host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
 size_t hetrd_blk_lds(int mt) {
     size_t b = (size_t)mt * 16 * (2 * HB_NB + 2);
     if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
-    if (ACE_HB_LOWER && ACE_HB_TPAIR && ACE_HB_PCOL) b += (size_t)HB_NB * mt * 16;
     return b;
 }
 __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
@@ -341,9 +334,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
 #if ACE_HB_LOWER
     d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
     d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
-    // [HB_NB][mt]: the next panel's columns as the trailing update leaves them (row relative to the panel start)
-    d2* pcolb = colp + (HB_NW + hb_strips(mt)) * 64;
-    (void)pcolb;
 #else
     __shared__ d2 part[HB_RB][HB_COLS];
 #endif
@@ -366,11 +356,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
 #if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
-#if ACE_HB_TPAIR && ACE_HB_PCOL   // from LDS after the first panel (no strided read of column k)
-                d2 a = k0 > 0 ? pcolb[p * mt + (c - k0)] : C[(long long)c * mt + k];
-#else
                 d2 a = C[(long long)c * mt + k];
-#endif
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
                 v[i] = a;   // x_i = A[k + 1 + i][k]
@@ -398,11 +384,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 s_tau = tau;
                 s_scal = scal;
                 ee[k] = beta;
-#if ACE_HB_LOWER && ACE_HB_TPAIR && ACE_HB_PCOL
-                d2 ckk = k0 > 0 ? pcolb[p * mt + p] : C[(long long)k * mt + k];
-#else
                 d2 ckk = C[(long long)k * mt + k];
-#endif
                 for (int q = 0; q < p; ++q)
                     ckk = csub(ckk, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + k])), cmul(Wp[q * mt + k], cj(Vp[q * mt + k]))));
                 dd[k] = ckk.x;
@@ -493,10 +475,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     for (int q = 0; q < 4; ++q)
                         cc[q] = (jv && 64 * s_ + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
                 };
-#if ACE_HB_MPF   // the next task's loads issued before this task's sums
-                d2 cn[4];
-                if (g0 < g1) load_task(g0, s, gb, cn);
-#endif
                 for (int g = g0; g < g1; ++g) {
                     if (g - gb >= ngr(s)) {
                         flush();
@@ -507,17 +485,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     const bool jv = j < L;
                     const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
                     d2 c[4];
-#if ACE_HB_MPF
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) c[q] = cn[q];
-                    if (g + 1 < g1) {
-                        int s2 = s, gb2 = gb;
-                        if (g + 1 - gb2 >= ngr(s2)) gb2 += ngr(s2++);
-                        load_task(g + 1, s2, gb2, cn);
-                    }
-#else
                     load_task(g, s, gb, c);
-#endif
                     double rx = 0.0, ry = 0.0;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -635,9 +603,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                             for (int q = 0; q < HB_NB; ++q)
                                 c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
                             C[(long long)rj * mt + ci] = c;
-#if ACE_HB_PCOL
-                            if (i < HB_NB) pcolb[i * mt + j] = c;
-#endif
                         }
                     }
                 }

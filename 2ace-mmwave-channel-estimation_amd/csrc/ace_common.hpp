@@ -168,6 +168,34 @@ struct VMax {
     }
 };
 
+// wave64 sum with DPP inside the 16-lane rows, one swizzle across the rows of each half, one exchange between the
+// halves (VALU latency for 4 of the 6 steps); another association than wave_sum, every lane gets the same value
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v = bsum16(v);
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x401F), hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x401F);
+    v += __hiloint2double(hi, lo);
+    return v + __shfl_xor(v, 32, 64);
+}
+// block_sum with wave_sum_dpp
+template <int NV>
+__device__ __forceinline__ void block_sum_dpp(double (&v)[NV], double* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_sum_dpp(v[i]);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[w * NV + i] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < nw; ++k) s += sh[k * NV + i];
+        v[i] = s;
+    }
+    __syncthreads();
+}
+
 // block reduction of up to NV doubles; all threads get the result. `sh` >= 16*NV doubles.
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {

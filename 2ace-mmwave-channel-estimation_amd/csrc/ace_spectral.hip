@@ -293,6 +293,16 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_NB
 #define ACE_HB_NB 2   // (r05: full square 4 against 8: PhaseLift 64.6 -> 67.5; lower triangle + pair trailing update 2 against 4: +1.5 %)
 #endif
+#ifndef ACE_HB_DPP
+#define ACE_HB_DPP 0   // hetrd_blk's reductions on DPP (wave_sum_dpp)
+#endif
+#if ACE_HB_DPP
+#define ACE_HB_BSUM block_sum_dpp
+#define ACE_HB_WSUM wave_sum_dpp
+#else
+#define ACE_HB_BSUM block_sum
+#define ACE_HB_WSUM wave_sum
+#endif
 #ifndef ACE_HB_TPAIR
 #define ACE_HB_TPAIR 1   // trailing update by column pairs (balanced lower triangle; r05: +3 %)
 #endif
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
 #endif
                 if (i > 0) s1[0] += cabs2(a);
             }
-            block_sum<1>(s1, red);
+            ACE_HB_BSUM<1>(s1, red);
             if (t == 0) {   // zlarfg
                 const d2 alpha = v[0];
                 const double xn2 = s1[0];
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     a = cadd(a, cmulc(Wp[q * mt + r], v[i]));
                     c2 = cadd(c2, cmulc(Vp[q * mt + r], v[i]));
                 }
-                const double a0 = wave_sum(a.x), a1 = wave_sum(a.y), c0 = wave_sum(c2.x), c1 = wave_sum(c2.y);
+                const double a0 = ACE_HB_WSUM(a.x), a1 = ACE_HB_WSUM(a.y), c0 = ACE_HB_WSUM(c2.x), c1 = ACE_HB_WSUM(c2.y);
                 if ((t & 63) == 0) {
                     red[(q * 16 + (t >> 6)) * 4 + 0] = a0;
                     red[(q * 16 + (t >> 6)) * 4 + 1] = a1;
@@ -555,7 +565,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 s2[0] += q.x;
                 s2[1] += q.y;
             }
-            block_sum<2>(s2, red);
+            ACE_HB_BSUM<2>(s2, red);
             const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
             for (int i = t; i < L; i += HB_THREADS) {
                 const d2 wi = cadd(w[i], cmul(alpha2, v[i]));

@@ -196,6 +196,25 @@ __device__ __forceinline__ void block_sum_dpp(double (&v)[NV], double* sh) {
     __syncthreads();
 }
 
+// block_sum_dpp with one barrier: the caller keeps `sh` barrier-separated from its previous readers and its next
+// writers (no barrier before the partials are stored or after they are read)
+template <int NV>
+__device__ __forceinline__ void block_sum_dpp1(double (&v)[NV], double* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_sum_dpp(v[i]);
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[w * NV + i] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        double s = 0.0;
+        for (int k = 0; k < nw; ++k) s += sh[k * NV + i];
+        v[i] = s;
+    }
+}
+
 // block reduction of up to NV doubles; all threads get the result. `sh` >= 16*NV doubles.
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {

@@ -294,9 +294,15 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #define ACE_HB_NB 2   // (r05: full square 4 against 8: PhaseLift 64.6 -> 67.5; lower triangle + pair trailing update 2 against 4: +1.5 %)
 #endif
 #ifndef ACE_HB_DPP
-#define ACE_HB_DPP 0   // hetrd_blk's reductions on DPP (wave_sum_dpp)
+#define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
 #endif
-#if ACE_HB_DPP
+#ifndef ACE_HB_SYNC1
+#define ACE_HB_SYNC1 0   // hetrd_blk's block sums with one barrier (block_sum_dpp1)
+#endif
+#if ACE_HB_DPP && ACE_HB_SYNC1
+#define ACE_HB_BSUM block_sum_dpp1
+#define ACE_HB_WSUM wave_sum_dpp
+#elif ACE_HB_DPP
 #define ACE_HB_BSUM block_sum_dpp
 #define ACE_HB_WSUM wave_sum_dpp
 #else

@@ -296,9 +296,6 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_DPP
 #define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
 #endif
-#ifndef ACE_HB_LEAN
-#define ACE_HB_LEAN 0   // hetrd_blk: zlarfg in every thread (no barrier for thread 0), no correction barriers at p = 0
-#endif
 #ifndef ACE_HB_SYNC1
 #define ACE_HB_SYNC1 1   // hetrd_blk's block sums with one barrier (block_sum_dpp1; r05: +0.5 %)
 #endif
@@ -356,7 +353,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
 #else
     __shared__ d2 part[HB_RB][HB_COLS];
 #endif
-    __shared__ d2 s_tau, s_scal, s_alpha, s_cw[HB_NB], s_cv[HB_NB];
+    __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
     double* dd = base + lay.dd;
@@ -372,9 +369,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             const int k = k0 + p, L = mt - k - 1;
             // row k of the current matrix: the panel-start C minus the panel's earlier rank-2 updates
             double s1[1] = {0.0};
-#if ACE_HB_LEAN
-            const d2 ckk0 = t == 0 ? C[(long long)k * mt + k] : make_double2(0.0, 0.0);   // (with the column's loads)
-#endif
             for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
 #if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
@@ -382,9 +376,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
                 v[i] = a;   // x_i = A[k + 1 + i][k]
-#if ACE_HB_LEAN
-                if (i == 0) s_alpha = a;   // (v[0] is rewritten below while other threads may still need alpha)
-#endif
 #else
                 d2 a = C[(long long)k * mt + c];
                 for (int q = 0; q < p; ++q)
@@ -394,35 +385,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 if (i > 0) s1[0] += cabs2(a);
             }
             ACE_HB_BSUM<1>(s1, red);
-#if ACE_HB_LEAN
-            // zlarfg in every thread (the same operations on the same block sum: the same tau, scal, beta in all of
-            // them), so that no barrier waits for thread 0
-            d2 tau = make_double2(0.0, 0.0), scal = make_double2(0.0, 0.0);
-            {
-                const d2 alpha = s_alpha;
-                const double xn2 = s1[0];
-                double beta = alpha.x;
-                if (!(xn2 == 0.0 && alpha.y == 0.0)) {
-                    beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn2), alpha.x);
-                    tau = make_double2((beta - alpha.x) / beta, -alpha.y / beta);
-                    const d2 den = make_double2(alpha.x - beta, alpha.y);
-                    const double dn = 1.0 / cabs2(den);
-                    scal = make_double2(den.x * dn, -den.y * dn);
-                }
-                if (t == 0) {
-                    ee[k] = beta;
-                    d2 ckk = ckk0;
-                    for (int q = 0; q < p; ++q)
-                        ckk = csub(ckk, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + k])), cmul(Wp[q * mt + k], cj(Vp[q * mt + k]))));
-                    dd[k] = ckk.x;
-                    taus[k] = tau;
-                }
-            }
-            if (tau.x == 0.0 && tau.y == 0.0) {   // H = I (uniform): V, W of this column stay 0
-                __syncthreads();   // (s_alpha is read above before the next column's extraction rewrites it)
-                continue;
-            }
-#else
             if (t == 0) {   // zlarfg
                 const d2 alpha = v[0];
                 const double xn2 = s1[0];
@@ -448,7 +410,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             const d2 tau = s_tau;
             if (tau.x == 0.0 && tau.y == 0.0) continue;   // H = I (uniform): V, W of this column stay 0
             const d2 scal = s_scal;
-#endif
             for (int i = t; i < L; i += HB_THREADS) {
                 const d2 vi = i == 0 ? make_double2(1.0, 0.0) : cmul(v[i], scal);
                 v[i] = vi;
@@ -457,7 +418,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             }
             // the panel's corrections to C22 v: s_q = W_q^H v, t_q = V_q^H v (L < 1024: one entry per thread)
             __syncthreads();
-            if (!ACE_HB_LEAN || p > 0) {   // (the panel's first column has none)
             for (int q = 0; q < p; ++q) {
                 d2 a = make_double2(0.0, 0.0), c2 = a;
                 for (int i = t; i < L; i += HB_THREADS) {
@@ -487,7 +447,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 s_cv[t] = make_double2(sv0, sv1);
             }
             __syncthreads();
-            }
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
 #if ACE_HB_LOWER

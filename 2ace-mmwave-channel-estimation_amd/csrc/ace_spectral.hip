@@ -296,6 +296,9 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_DPP
 #define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
 #endif
+#ifndef ACE_HB_CPAR
+#define ACE_HB_CPAR 0   // hetrd_blk: the panel corrections' wave sums for all q side by side
+#endif
 #ifndef ACE_HB_SYNC1
 #define ACE_HB_SYNC1 1   // hetrd_blk's block sums with one barrier (block_sum_dpp1; r05: +0.5 %)
 #endif
@@ -418,6 +421,35 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             }
             // the panel's corrections to C22 v: s_q = W_q^H v, t_q = V_q^H v (L < 1024: one entry per thread)
             __syncthreads();
+#if ACE_HB_CPAR   // every q's dot products first, then their wave sums side by side (independent chains)
+            if (p > 0) {
+                d2 a[HB_NB], c2[HB_NB];
+#pragma unroll
+                for (int q = 0; q < HB_NB; ++q) a[q] = c2[q] = make_double2(0.0, 0.0);
+                for (int i = t; i < L; i += HB_THREADS) {
+                    const int r = k + 1 + i;
+                    const d2 vi = v[i];
+#pragma unroll
+                    for (int q = 0; q < HB_NB; ++q)
+                        if (q < p) {
+                            a[q] = cadd(a[q], cmulc(Wp[q * mt + r], vi));
+                            c2[q] = cadd(c2[q], cmulc(Vp[q * mt + r], vi));
+                        }
+                }
+#pragma unroll
+                for (int q = 0; q < HB_NB; ++q) {
+                    if (q >= p) break;
+                    const double a0 = ACE_HB_WSUM(a[q].x), a1 = ACE_HB_WSUM(a[q].y), c0 = ACE_HB_WSUM(c2[q].x),
+                                 c1 = ACE_HB_WSUM(c2[q].y);
+                    if ((t & 63) == 0) {
+                        red[(q * 16 + (t >> 6)) * 4 + 0] = a0;
+                        red[(q * 16 + (t >> 6)) * 4 + 1] = a1;
+                        red[(q * 16 + (t >> 6)) * 4 + 2] = c0;
+                        red[(q * 16 + (t >> 6)) * 4 + 3] = c1;
+                    }
+                }
+            }
+#else
             for (int q = 0; q < p; ++q) {
                 d2 a = make_double2(0.0, 0.0), c2 = a;
                 for (int i = t; i < L; i += HB_THREADS) {
@@ -433,6 +465,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     red[(q * 16 + (t >> 6)) * 4 + 3] = c1;
                 }
             }
+#endif
             __syncthreads();
             if (t < p) {   // fixed order over the 16 waves
                 double sw0 = 0.0, sw1 = 0.0, sv0 = 0.0, sv1 = 0.0;

@@ -291,13 +291,13 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 // the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
 // d, e, tau and reflector k in row k of C.
 #ifndef ACE_HB_NB
-#define ACE_HB_NB 2   // (r05: full square 4 against 8: PhaseLift 64.6 -> 67.5; lower triangle + pair trailing update 2 against 4: +1.5 %)
+#define ACE_HB_NB 4   // (r05: full square 4 against 8 +4.5 %; lower + pairs 2 against 4 +1.5 %; with the DPP sums 4 against 2 +2 %)
 #endif
 #ifndef ACE_HB_DPP
 #define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
 #endif
 #ifndef ACE_HB_CPAR
-#define ACE_HB_CPAR 0   // hetrd_blk: the panel corrections' wave sums for all q side by side
+#define ACE_HB_CPAR 1   // hetrd_blk: the panel corrections' wave sums for all q side by side
 #endif
 #ifndef ACE_HB_SYNC1
 #define ACE_HB_SYNC1 1   // hetrd_blk's block sums with one barrier (block_sum_dpp1; r05: +0.5 %)

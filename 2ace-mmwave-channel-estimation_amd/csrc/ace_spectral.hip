@@ -296,6 +296,9 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 #ifndef ACE_HB_DPP
 #define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
 #endif
+#ifndef ACE_HB_TR
+#define ACE_HB_TR 1   // lower-triangle product: rows per lane and task
+#endif
 #ifndef ACE_HB_CPAR
 #define ACE_HB_CPAR 1   // hetrd_blk: the panel corrections' wave sums for all q side by side
 #endif
@@ -491,7 +494,8 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             // the run (slot wave + strip: unique, since the runs are contiguous).
             {
                 const int ns = hb_strips(L), wv = t >> 6, jr = (t & 63) >> 4, ic = t & 15;
-                auto ngr = [&](int s) { return (L - 64 * s + 3) >> 2; };
+                constexpr int TR = ACE_HB_TR;   // rows per lane and task (a task: 4 TR rows of a strip)
+                auto ngr = [&](int s) { return (L - 64 * s + 4 * TR - 1) / (4 * TR); };
                 int G = 0;
                 for (int s = 0; s < ns; ++s) G += ngr(s);
                 const int g0 = wv * G / HB_NW, g1 = (wv + 1) * G / HB_NW;
@@ -516,39 +520,42 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     }
                 };
                 if (g0 < g1) strip_start();
-                auto load_task = [&](int g, int s_, int gb_, d2 (&cc)[4]) {
-                    const int j = 64 * s_ + 4 * (g - gb_) + jr;
-                    const bool jv = j < L;
-                    const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s_ + ic;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        cc[q] = (jv && 64 * s_ + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
-                };
                 for (int g = g0; g < g1; ++g) {
                     if (g - gb >= ngr(s)) {
                         flush();
                         gb += ngr(s++);
                         strip_start();
                     }
-                    const int j = 64 * s + 4 * (g - gb) + jr;
-                    const bool jv = j < L;
-                    const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
-                    d2 c[4];
-                    load_task(g, s, gb, c);
-                    double rx = 0.0, ry = 0.0;
+                    d2 c[TR][4];   // the task's loads, all issued before its sums
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        ca[q].x += c[q].x * vj.x + c[q].y * vj.y;
-                        ca[q].y += c[q].x * vj.y - c[q].y * vj.x;
-                        if (64 * s + ic + 16 * q < j) {   // (then i < L: v[i] is live)
-                            const d2 vi = v[64 * s + ic + 16 * q];
-                            rx += c[q].x * vi.x - c[q].y * vi.y;
-                            ry += c[q].x * vi.y + c[q].y * vi.x;
-                        }
+                    for (int h = 0; h < TR; ++h) {
+                        const int j = 64 * s + 4 * TR * (g - gb) + jr + 4 * h;
+                        const bool jv = j < L;
+                        const d2* crow = C22 + (long long)(jv ? j : 0) * mt + 64 * s + ic;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            c[h][q] = (jv && 64 * s + ic + 16 * q <= j) ? crow[16 * q] : make_double2(0.0, 0.0);
                     }
-                    rx = bsum16(rx);   // over the 16 ic lanes: one DPP row
-                    ry = bsum16(ry);
-                    if (ic == 0 && jv) rowp[s * mt + j] = make_double2(rx, ry);
+#pragma unroll
+                    for (int h = 0; h < TR; ++h) {
+                        const int j = 64 * s + 4 * TR * (g - gb) + jr + 4 * h;
+                        const bool jv = j < L;
+                        const d2 vj = jv ? v[j] : make_double2(0.0, 0.0);
+                        double rx = 0.0, ry = 0.0;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            ca[q].x += c[h][q].x * vj.x + c[h][q].y * vj.y;
+                            ca[q].y += c[h][q].x * vj.y - c[h][q].y * vj.x;
+                            if (64 * s + ic + 16 * q < j) {   // (then i < L: v[i] is live)
+                                const d2 vi = v[64 * s + ic + 16 * q];
+                                rx += c[h][q].x * vi.x - c[h][q].y * vi.y;
+                                ry += c[h][q].x * vi.y + c[h][q].y * vi.x;
+                            }
+                        }
+                        rx = bsum16(rx);   // over the 16 ic lanes: one DPP row
+                        ry = bsum16(ry);
+                        if (ic == 0 && jv) rowp[s * mt + j] = make_double2(rx, ry);
+                    }
                 }
                 if (g0 < g1) flush();
                 __syncthreads();

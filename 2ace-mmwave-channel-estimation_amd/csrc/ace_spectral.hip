@@ -328,7 +328,11 @@ constexpr int HB_TB = ACE_HB_TB;
 #ifndef ACE_HB_THREADS
 #define ACE_HB_THREADS 1024
 #endif
-constexpr int HB_NB = ACE_HB_NB;             // panel width
+constexpr int HB_NB = ACE_HB_NB;             // panel width (PhaseLift's prox)
+#ifndef ACE_HB_NB_SPEC
+#define ACE_HB_NB_SPEC 2   // panel width of the spectral initialisation (one matrix per realisation, latency-bound batches)
+#endif
+constexpr int HB_NB_SPEC = ACE_HB_NB_SPEC;
 constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
 constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
 constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
@@ -339,27 +343,28 @@ constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
 #endif
 constexpr int HB_NW = HB_THREADS / 64;   // waves
 __host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
-size_t hetrd_blk_lds(int mt) {
-    size_t b = (size_t)mt * 16 * (2 * HB_NB + 2);
+size_t hetrd_blk_lds(int mt, int nb = HB_NB) {
+    size_t b = (size_t)mt * 16 * (2 * nb + 2);
     if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
     return b;
 }
+template <int NB>
 __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (active && !active[b]) return;
     extern __shared__ double smem[];
-    d2* Vp = reinterpret_cast<d2*>(smem);   // [HB_NB][mt]: the panel's reflectors by absolute row (0 elsewhere)
-    d2* Wp = Vp + HB_NB * mt;               // [HB_NB][mt]: their w
-    d2* v = Wp + HB_NB * mt;                // current reflector, entry i = row k + 1 + i
+    d2* Vp = reinterpret_cast<d2*>(smem);   // [NB][mt]: the panel's reflectors by absolute row (0 elsewhere)
+    d2* Wp = Vp + NB * mt;               // [NB][mt]: their w
+    d2* v = Wp + NB * mt;                // current reflector, entry i = row k + 1 + i
     d2* w = v + mt;
-    __shared__ double red[16 * 4 * HB_NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
+    __shared__ double red[16 * 4 * NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
 #if ACE_HB_LOWER
     d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
     d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
 #else
     __shared__ d2 part[HB_RB][HB_COLS];
 #endif
-    __shared__ d2 s_tau, s_scal, s_cw[HB_NB], s_cv[HB_NB];
+    __shared__ d2 s_tau, s_scal, s_cw[NB], s_cv[NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
     double* dd = base + lay.dd;
@@ -367,9 +372,9 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
     d2* taus = reinterpret_cast<d2*>(base + lay.tau);
     const int col = t % HB_COLS, rb = t / HB_COLS;
     auto cj = [](d2 a) { return make_double2(a.x, -a.y); };
-    for (int k0 = 0; k0 + 1 < mt; k0 += HB_NB) {
-        const int nbp = min(HB_NB, mt - 1 - k0);
-        for (int e = t; e < 2 * HB_NB * mt; e += HB_THREADS) Vp[e] = make_double2(0.0, 0.0);
+    for (int k0 = 0; k0 + 1 < mt; k0 += NB) {
+        const int nbp = min(NB, mt - 1 - k0);
+        for (int e = t; e < 2 * NB * mt; e += HB_THREADS) Vp[e] = make_double2(0.0, 0.0);
         __syncthreads();
         for (int p = 0; p < nbp; ++p) {
             const int k = k0 + p, L = mt - k - 1;
@@ -426,21 +431,21 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
 #if ACE_HB_CPAR   // every q's dot products first, then their wave sums side by side (independent chains)
             if (p > 0) {
-                d2 a[HB_NB], c2[HB_NB];
+                d2 a[NB], c2[NB];
 #pragma unroll
-                for (int q = 0; q < HB_NB; ++q) a[q] = c2[q] = make_double2(0.0, 0.0);
+                for (int q = 0; q < NB; ++q) a[q] = c2[q] = make_double2(0.0, 0.0);
                 for (int i = t; i < L; i += HB_THREADS) {
                     const int r = k + 1 + i;
                     const d2 vi = v[i];
 #pragma unroll
-                    for (int q = 0; q < HB_NB; ++q)
+                    for (int q = 0; q < NB; ++q)
                         if (q < p) {
                             a[q] = cadd(a[q], cmulc(Wp[q * mt + r], vi));
                             c2[q] = cadd(c2[q], cmulc(Vp[q * mt + r], vi));
                         }
                 }
 #pragma unroll
-                for (int q = 0; q < HB_NB; ++q) {
+                for (int q = 0; q < NB; ++q) {
                     if (q >= p) break;
                     const double a0 = ACE_HB_WSUM(a[q].x), a1 = ACE_HB_WSUM(a[q].y), c0 = ACE_HB_WSUM(c2[q].x),
                                  c1 = ACE_HB_WSUM(c2[q].y);
@@ -635,9 +640,9 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     const int i = side ? L2 - 1 - pi : pi;
                     if (side && i == pi) break;   // the middle column of an odd order
                     const int ci = kn + i;
-                    d2 vq[HB_NB], wq[HB_NB];
+                    d2 vq[NB], wq[NB];
 #pragma unroll
-                    for (int q = 0; q < HB_NB; ++q) {
+                    for (int q = 0; q < NB; ++q) {
                         vq[q] = cj(Vp[q * mt + ci]);
                         wq[q] = cj(Wp[q * mt + ci]);
                     }
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                             const int rj = kn + j;
                             d2 c = cb[u];
 #pragma unroll
-                            for (int q = 0; q < HB_NB; ++q)
+                            for (int q = 0; q < NB; ++q)
                                 c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
                             C[(long long)rj * mt + ci] = c;
                         }
@@ -672,9 +677,9 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             const int i = i0 + tcol;
             if (i >= L2 || trb >= nrb2) continue;
             const int ci = kn + i;
-            d2 vq[HB_NB], wq[HB_NB];
+            d2 vq[NB], wq[NB];
 #pragma unroll
-            for (int q = 0; q < HB_NB; ++q) {
+            for (int q = 0; q < NB; ++q) {
                 vq[q] = cj(Vp[q * mt + ci]);
                 wq[q] = cj(Wp[q * mt + ci]);
             }
@@ -698,7 +703,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     const int rj = kn + j;
                     d2 c = cb[u];
 #pragma unroll
-                    for (int q = 0; q < HB_NB; ++q)
+                    for (int q = 0; q < NB; ++q)
                         c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
                     C[(long long)rj * mt + ci] = c;
                 }
@@ -1191,7 +1196,9 @@ int backxf_chunk(int mt) {
 }
 }  // namespace
 // dynamic LDS of hetrd_kernel / hetrd_blk_kernel at order d (ace_lds_request)
-size_t hetrd_request_bytes(int d, int blk) { return blk ? hetrd_blk_lds(d) : hetrd_lds(d); }
+size_t hetrd_request_bytes(int d, int blk) {   // (blk: the larger of the prox's and the spectral panel widths)
+    return blk ? std::max(hetrd_blk_lds(d, HB_NB), hetrd_blk_lds(d, HB_NB_SPEC)) : hetrd_lds(d);
+}
 
 namespace {
 // ---- primal form for m_t > n: the n x n Gram As^H As itself (a smaller eigenproblem)
@@ -1269,7 +1276,8 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
     const SpecLayout lay(n, r);
     const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 24;
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
-    const bool blk = spectral_blk() && hetrd_blk_lds(n) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
+    const bool blk = spectral_blk() &&
+                     hetrd_blk_lds(n, HB_NB_SPEC) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>));
     const int chunk = primal_chunk(mt, n, batch);
     double* Ast = scratch + (((size_t)lay.stride * chunk + 31) & ~(size_t)31);
     for (int b0 = 0; b0 < batch; b0 += chunk) {
@@ -1283,7 +1291,8 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
                      lay.stride / 2, nb, st);
         hipLaunchKernelGGL(spec_herm_kernel, dim3((n + 15) / 16, nb, (n + 15) / 16), dim3(256), 0, st, n, scratch, lay);
         if (blk)
-            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(n), st, n, scratch, lay, nullptr);
+            hipLaunchKernelGGL(hetrd_blk_kernel<HB_NB_SPEC>, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(n, HB_NB_SPEC), st, n,
+                               scratch, lay, nullptr);
         else
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
                                nullptr, nullptr, 0);
@@ -1302,7 +1311,8 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
     const SpecLayout lay(mt, r);
     const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 24;
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
-    const bool blk = spectral_blk() && hetrd_blk_lds(mt) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel));
+    const bool blk = spectral_blk() &&
+                     hetrd_blk_lds(mt, HB_NB_SPEC) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>));
     const int ldb = pr ? pr->m : mt;   // per-realisation partitions: the full K and B, rows per realisation
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
@@ -1310,7 +1320,8 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
             hipLaunchKernelGGL(spec_form_c_kernel, dim3(nb), dim3(256), (size_t)mt * sizeof(double), st, mt, K,
                                Bt + (long long)b0 * ldb, scratch, lay, pr ? pr->rows + (long long)b0 * pr->m : nullptr,
                                pr ? pr->m : 0);
-            hipLaunchKernelGGL(hetrd_blk_kernel, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(mt), st, mt, scratch, lay, nullptr);
+            hipLaunchKernelGGL(hetrd_blk_kernel<HB_NB_SPEC>, dim3(nb), dim3(HB_THREADS), hetrd_blk_lds(mt, HB_NB_SPEC), st, mt,
+                               scratch, lay, nullptr);
         } else {
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
                                lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
@@ -1452,12 +1463,12 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
     // the blocked reduction (hetrd_blk_kernel): blk = 1 (the caller reads ACE_HETRD_BLK once per solve)
-    if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel), "hetrd_blk_kernel", hetrd_blk_lds(d)))
+    if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB>), "hetrd_blk_kernel", hetrd_blk_lds(d)))
         blk = 0;   // (the unblocked reduction takes any d hetrd_lds_ok admits)
     if (blk) {
         // (all matrices in one launch: launches of 128 / 256 matrices, whose working set would stay in the MALL,
         // measured 37.8 / 54.1 against 60.4 rec/s -- the reduction is bound by its work-groups' latency, not HBM)
-        hipLaunchKernelGGL(hetrd_blk_kernel, dim3(batch), dim3(HB_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
+        hipLaunchKernelGGL(hetrd_blk_kernel<HB_NB>, dim3(batch), dim3(HB_THREADS), hetrd_blk_lds(d), st, d, scratch, lay, active);
     } else {
         hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
                            nullptr, 0);

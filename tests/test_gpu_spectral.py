@@ -30,7 +30,12 @@ def _case(seed, tx, m, count, zero_row=False):
                                               (4, 16, 640, 20, True),      # primal: m > n
                                               (5, 32, 256, 20, False),     # config-2 geometry (dual)
                                               (6, 32, 1216, 12, False),    # primal, n = 1024
-                                              (7, 8, 64, 20, True)])       # dual, m = n
+                                              (7, 8, 64, 20, True),        # dual, m = n
+                                              # orders that are not multiples of the product's 64-column strips
+                                              # or of the panel width (hetrd_blk's lower-triangle tasks, odd
+                                              # trailing orders in its column-pair update)
+                                              (10, 8, 17, 12, False), (11, 16, 130, 20, False),
+                                              (12, 16, 255, 20, True)])
 def test_spectral_initialize_matches_oracle(gpu, seed, tx, m, r, zero):
     from ace_amd import SpectralInitialize
     A, B = _case(seed, tx, m, 3, zero)

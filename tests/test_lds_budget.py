@@ -38,7 +38,8 @@ CASES = [
     ("msr", "ace_i8gemm.hip", [r"msr_kernelILi2E", r"msr_kernelILi4E"], [256]),
     ("nms", "ace_nucmsp.hip", [r"nms_kernelILb0E", r"nms_kernelILb1E"], [64, 256]),
     ("hetrd", "ace_spectral.hip", [r"12hetrd_kernel"], [256, 1024]),
-    ("hetrd_blk", "ace_spectral.hip", [r"16hetrd_blk_kernel"], [128, 256]),   # (the prox order d = m, §4)
+    ("hetrd_blk", "ace_spectral.hip", [r"16hetrd_blk_kernelILi4E", r"16hetrd_blk_kernelILi2E"],
+     [128, 256]),   # (the prox order d = m, §4; panels of 4 in the prox, 2 in the spectral initialisation)
 ]
 
 _REMARK = re.compile(r"remark: Function Name: (\S+)|remark:\s+LDS Size \[bytes/block\]: (\d+)")

@@ -65,10 +65,23 @@ __global__ __launch_bounds__(256) void pl_outer_begin_kernel(PlArgs a) {
     const int b = blockIdx.x, t = threadIdx.x;
     PlState& p = a.st[b];
     if (p.done) return;
-    const long long dd = 2LL * a.d * a.d, o = b * dd;
-    for (long long e = t; e < dd; e += 256) {
-        a.xo[o + e] = a.x[o + e];
-        a.zo[o + e] = a.z[o + e];
+    // x_old = x, z_old = z: 16-B accesses, four in flight per thread
+    const long long n2 = (long long)a.d * a.d, o = b * n2;
+    const d2* xs = reinterpret_cast<const d2*>(a.x) + o;
+    const d2* zs = reinterpret_cast<const d2*>(a.z) + o;
+    d2* xd = reinterpret_cast<d2*>(a.xo) + o;
+    d2* zd = reinterpret_cast<d2*>(a.zo) + o;
+    long long e = t;
+    for (; e + 256 < n2; e += 512) {
+        const d2 x0 = xs[e], x1 = xs[e + 256], z0 = zs[e], z1 = zs[e + 256];
+        xd[e] = x0;
+        xd[e + 256] = x1;
+        zd[e] = z0;
+        zd[e + 256] = z1;
+    }
+    for (; e < n2; e += 256) {
+        xd[e] = xs[e];
+        zd[e] = zs[e];
     }
     for (int i = t; i < a.m; i += 256) {
         a.Axo[(long long)b * a.m + i] = a.Ax[(long long)b * a.m + i];
@@ -232,17 +245,31 @@ __global__ __launch_bounds__(256) void pl_assemble_kernel(PlArgs a) {
     const d2* V = reinterpret_cast<const d2*>(a.V) + o;
     d2* P = reinterpret_cast<d2*>(a.P) + o;
     d2* VT = reinterpret_cast<d2*>(a.VT) + o;
-    for (long long e = t; e < (long long)d * d; e += 256) {
-        const int i = (int)(e / d), q = (int)(e % d);
-        d2 v = make_double2(0.0, 0.0);
-        double s = 0.0;
-        if (q < k) {
-            v = V[(long long)q * d + i];
-            s = lam[q] - tau;
+    // VT[i][q] = V[q][i] (q < k, else 0) and P[i][q] = VT[i][q] (lam_q - tau), by 32 x 32 tiles through LDS: V read
+    // along its rows (the element-wise form read V[q][i] down a column), the same values
+    __shared__ d2 tv[32][33];
+    const int nt = (d + 31) / 32, cc = t & 31, r0 = t >> 5;
+    for (int I = 0; I < nt; ++I)
+        for (int Q = 0; Q < nt; ++Q) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int rr = r0 + 8 * u, q = 32 * Q + rr, i = 32 * I + cc;
+                if (q < d && i < d) tv[rr][cc] = q < k ? V[(long long)q * d + i] : make_double2(0.0, 0.0);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int rr = r0 + 8 * u, i = 32 * I + rr, q = 32 * Q + cc;
+                if (i < d && q < d) {
+                    const d2 v = tv[cc][rr];
+                    const double s = q < k ? lam[q] - tau : 0.0;
+                    const long long e = (long long)i * d + q;
+                    VT[e] = v;
+                    P[e] = cscale(v, s);
+                }
+            }
+            __syncthreads();
         }
-        VT[e] = v;
-        P[e] = cscale(v, s);
-    }
     if (t == 0) a.st[b].C_z = a.lambda * base[a.hl.misc + 1];
 }
 
@@ -254,11 +281,36 @@ __global__ __launch_bounds__(256) void pl_take_z_kernel(PlArgs a) {
     const long long o = (long long)b * d * d;
     const d2* Zn = reinterpret_cast<const d2*>(a.Znew) + o;
     d2* z = reinterpret_cast<d2*>(a.z) + o;
-    for (long long e = t; e < (long long)d * d; e += 256) {
-        const int i = (int)(e / d), j = (int)(e % d);
-        const d2 u = Zn[e], l = Zn[(long long)j * d + i];
-        z[e] = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
-    }
+    // by 32 x 32 tile pairs (I, J), (J, I) staged in LDS (as pl_prox_in_kernel): every entry read once, row-coalesced
+    // (the element-wise form read Zn[j][i] down a column); the same expression per entry
+    __shared__ d2 tu[32][33], tl[32][33];
+    const int nt = (d + 31) / 32, cc = t & 31, r0 = t >> 5;
+    for (int I = 0; I < nt; ++I)
+        for (int J = I; J < nt; ++J) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = r0 + 8 * q;
+                const int i1 = 32 * I + rr, j1 = 32 * J + cc, i2 = 32 * J + rr, j2 = 32 * I + cc;
+                if (i1 < d && j1 < d) tu[rr][cc] = Zn[(long long)i1 * d + j1];
+                if (i2 < d && j2 < d) tl[rr][cc] = Zn[(long long)i2 * d + j2];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = r0 + 8 * q;
+                const int i1 = 32 * I + rr, j1 = 32 * J + cc;
+                if (i1 < d && j1 < d) {   // z[i1][j1] from u = Zn[i1][j1], l = Zn[j1][i1]
+                    const d2 u = tu[rr][cc], l = tl[cc][rr];
+                    z[(long long)i1 * d + j1] = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                }
+                const int i2 = 32 * J + rr, j2 = 32 * I + cc;
+                if (I != J && i2 < d && j2 < d) {
+                    const d2 u = tl[rr][cc], l = tu[cc][rr];
+                    z[(long long)i2 * d + j2] = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                }
+            }
+            __syncthreads();
+        }
 }
 
 // A(X) = diag(R^H X R) given T = X R: a_i = Re sum_r conj(R[r][i]) T[r][i]  (the imaginary part

@@ -1401,10 +1401,16 @@ __global__ __launch_bounds__(64) void wy_larft_kernel(int d, const double* scrat
     d2* Tg = reinterpret_cast<d2*>(wy + b * wl.stride + wl.Tm) + (long long)j * WY_NB * WY_NB;
     const int j0 = j * WY_NB, nbj = min(WY_NB, d - 1 - j0);
     for (int c = 0; c < WY_NB; ++c) T[a][c] = make_double2(0.0, 0.0);
+    // step i's G row and tau are loaded during step i - 1 (the loads do not depend on the recurrence)
+    d2 gn = G[a], tn = taus[j0];
     __syncthreads();
     for (int i = 0; i < nbj; ++i) {
-        const d2 ti = taus[j0 + i];
-        if (a < i) y[a] = cscale(cmul(ti, G[(long long)i * WY_NB + a]), -1.0);
+        const d2 ti = tn, gi = gn;
+        if (i + 1 < nbj) {
+            gn = G[(long long)(i + 1) * WY_NB + a];
+            tn = taus[j0 + i + 1];
+        }
+        if (a < i) y[a] = cscale(cmul(ti, gi), -1.0);
         __syncthreads();
         if (a < i) {
             d2 acc = make_double2(0.0, 0.0);

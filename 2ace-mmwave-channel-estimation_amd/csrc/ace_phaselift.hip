@@ -131,8 +131,14 @@ __global__ __launch_bounds__(256) void pl_make_y_kernel(PlArgs a) {
     const PlState& p = a.st[b];
     if (!a.act[b] || !p.ycomp) return;
     const double th = p.theta, om = 1.0 - th;
-    const long long dd = 2LL * a.d * a.d, o = b * dd;
-    for (long long e = t; e < dd; e += 256) a.y[o + e] = om * a.xo[o + e] + th * a.zo[o + e];
+    const long long n2 = (long long)a.d * a.d, o = b * n2;   // (16-B accesses, the same expression per double)
+    const d2* xo = reinterpret_cast<const d2*>(a.xo) + o;
+    const d2* zo = reinterpret_cast<const d2*>(a.zo) + o;
+    d2* y = reinterpret_cast<d2*>(a.y) + o;
+    for (long long e = t; e < n2; e += 256) {
+        const d2 u = xo[e], w = zo[e];
+        y[e] = make_double2(om * u.x + th * w.x, om * u.y + th * w.y);
+    }
 }
 
 // A_y = A(y) when the counter fired, else (1 - theta) A_x_old + theta A_z_old (tfocs_AT.m:39-44)

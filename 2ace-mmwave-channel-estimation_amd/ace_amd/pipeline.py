@@ -205,9 +205,21 @@ def infer_low_rank_pipeline_batch(A, B, tx, rx, train_idx, *, variant="A2only", 
     tr, layout = _layout(train_idx, batch)
     grp = _groups(tr, m)
     if grp is not None and len(grp) > 1:   # (m - m_t > PART_MAXTE: one shared-layout call per group)
+        cur = torch.cuda.current_stream(B.device)
+        if stream is not None and stream != cur:
+            # the whole grouped path (the B subsets, the group solves, the scatter of their outputs) runs on
+            # `stream` after what the caller queued on its current stream; A and B stay reserved for `stream`
+            stream.wait_stream(cur)
+            A.record_stream(stream)
+            B.record_stream(stream)
+            with torch.cuda.stream(stream):
+                return infer_low_rank_pipeline_batch(
+                    A, B, tx, rx, train_idx, variant=variant, restarts=restarts, r=r, mu0=mu0, rho=rho,
+                    cc_frac=cc_frac, tol_rel=tol_rel, tol_abs=tol_abs, maxiter=maxiter, eig_warm=eig_warm,
+                    stop_before_refine=stop_before_refine, workspace=workspace, stream=None)
         kw = dict(variant=variant, restarts=restarts, r=r, mu0=mu0, rho=rho, cc_frac=cc_frac, tol_rel=tol_rel,
                   tol_abs=tol_abs, maxiter=maxiter, eig_warm=eig_warm, stop_before_refine=stop_before_refine,
-                  workspace=workspace, stream=stream)
+                  workspace=workspace, stream=None)
         outs = []
         for g in grp:
             gi = torch.as_tensor(g, device=B.device)

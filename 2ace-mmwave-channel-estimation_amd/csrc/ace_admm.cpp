@@ -144,8 +144,11 @@ static bool msr_trace() {
     return v;
 }
 // eligibility of the fused kernels: their dynamic LDS within the kernel's derived budget (lds_dyn_budget)
-static bool fuse_ok(const Knobs& k, int m) { return k.fuse && i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes() <= i8ah_budget(1); }
-static bool gyf_ok(const Knobs& k, int m) { return k.gyf && gyf_lds_bytes(m) <= gyf_budget(); }
+// (the launchers' own rule, lds_ok_budget: a shape within the 64 KiB default needs no attribute)
+static bool fuse_ok(const Knobs& k, int m) {
+    return k.fuse && lds_ok_budget(i8ah_budget(1), i8ah_lds_bytes(m) + i8ah_fuse_lds_bytes());
+}
+static bool gyf_ok(const Knobs& k, int m) { return k.gyf && lds_ok_budget(gyf_budget(), gyf_lds_bytes(m)); }
 
 // ACE_NO_I8=1 keeps the f64 matrix-core applies for phase-code codebooks too (A/B comparisons).
 static bool i8_disabled() {
@@ -171,8 +174,8 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     ACE_HIP(read_back(c, L.c8, sizeof(double), st));
     // apply_AH and K Y both hold the digit planes of an m-long operand in LDS
-    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && i8ah_lds_bytes(m) <= i8ah_budget(0) &&
-             i8ah_lds_bytes(m) <= i8ah_budget(2);
+    L.i8ok = flag == 0 && c[0] > 0.0 && std::isfinite(c[0]) && lds_ok_budget(i8ah_budget(0), i8ah_lds_bytes(m)) &&
+             lds_ok_budget(i8ah_budget(2), i8ah_lds_bytes(m));
     if (!L.i8ok) return ACE_OK;
     c[1] = c[0] * c[0];
     ACE_HIP(upload(L.c8 + 1, c + 1, sizeof(double), st));
@@ -180,7 +183,7 @@ static int i8_setup(LinOps& L, hipStream_t st) {
     launch_i8k_expand(m, L.K, L.c8, L.LK8, L.i8flag, st);
     ACE_HIP(read_back(&flag, L.i8flag, sizeof(int), st));
     L.i8ok = flag == 0;
-    L.gyk_ok = L.i8ok && L.Gf && gyk_lds_bytes(m) <= gyk_budget();
+    L.gyk_ok = L.i8ok && L.Gf && lds_ok_budget(gyk_budget(), gyk_lds_bytes(m));
     return ACE_OK;
 }
 
@@ -461,6 +464,19 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
     }();
     hipEvent_t evs = nullptr;
     if (stg > 0 && nsplit > 1) ACE_HIP(hipEventCreateWithFlags(&evs, hipEventDisableTiming));
+    // a refused or failed launch inside the sub-batch loops: the caller's stream still waits for every
+    // sub-stream (work already queued there uses the caller's workspace) before the error is returned
+    auto split_fail = [&](int lc) -> int {
+        for (int h = 1; h < nsplit; ++h)
+            if (hipEventRecord(ev[h], ss[h]) == hipSuccess) (void)hipStreamWaitEvent(st, ev[h], 0);
+        if (evs) (void)hipEventDestroy(evs);
+        return lc;
+    };
+#define SPLIT_LAUNCHED(stage)                                           \
+    do {                                                                \
+        const int lc_ = ::ace::launch_check(stage, __FILE__, __LINE__); \
+        if (lc_) return split_fail(lc_);                                \
+    } while (0)
     auto stagger_mark = [&](int h, int it, int k) -> hipError_t {
         return (evs && h == 0 && it == 1 && k == stg) ? hipEventRecord(evs, ss[0]) : hipSuccess;
     };
@@ -524,7 +540,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
                 ProfScope ps(ACE_K_MSR, ss[h]);
                 pidx[h] = ps.idx;
                 launch_msr(ma, za, kn.msr_waves, ss[h]);
-                ACE_LAUNCHED("m-space run (msr_kernel)");
+                SPLIT_LAUNCHED("m-space run (msr_kernel)");
             }
             for (int h = 1; h < nsplit; ++h) {   // (the caller's stream waits for the sub-batches)
                 ACE_HIP(hipEventRecord(cev[h], ss[h]));
@@ -603,24 +619,24 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
             } else if (gyf) {
                 ProfScope ps(ACE_K_APPLY_G, sh);
                 launch_gyf(nb[h], m, n, ga, L.LAH8, wh.X, za, kn.gyf_ctl, sh);
-                ACE_LAUNCHED("g / Y-step / apply_AH (gyf_kernel)");
+                SPLIT_LAUNCHED("g / Y-step / apply_AH (gyf_kernel)");
             } else {
                 {
                     ProfScope ps(ACE_K_APPLY_G, sh);
                     launch_gyk(nb[h], m, ga, sh);
                 }
-                ACE_LAUNCHED("g / Y-step (gyk_kernel)");
+                SPLIT_LAUNCHED("g / Y-step (gyk_kernel)");
                 ACE_HIP(stagger_mark(h, it, 2));
                 ProfScope ps(ACE_K_APPLY_AH, sh);
                 launch_i8_apply_AH(nb[h], m, n, L.LAH8, wh.g, wh.X, L.c8, wh.st, sh, za.xfuse ? &za : nullptr);
-                ACE_LAUNCHED("apply_AH (i8ah_kernel)");
+                SPLIT_LAUNCHED("apply_AH (i8ah_kernel)");
             }
             ACE_HIP(stagger_mark(h, it, 3));
             if (pmask & 2) {
                 ProfScope ps(ACE_K_ZSTEP, sh);
                 if (lean && !za.xfuse) launch_zlean(za, nb[h], sh);
                 launch_zstep(p.variant, false, za, nb[h], sh);
-                ACE_LAUNCHED("Z-step");
+                SPLIT_LAUNCHED("Z-step");
             }
         }
         if (csync) ACE_TRY(barrier());
@@ -641,6 +657,7 @@ static int admm_iterate_split(const LinOps& L, const AdmmParams& p, const AdmmSt
         ACE_HIP(hipStreamWaitEvent(st, ev[h], 0));
     }
     ACE_LAUNCHED("split iterations");
+#undef SPLIT_LAUNCHED
     {
         ProfScope ps(ACE_K_FINAL, st);
         // best iterates still in m-space form (RealState::optsrc 3): opt_X = Z0 + A^H opt_S

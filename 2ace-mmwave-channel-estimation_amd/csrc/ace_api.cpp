@@ -62,11 +62,13 @@ void launch_refused(const char* kernel, size_t need, size_t budget) {
     t_refused = buf;
 }
 
+bool lds_ok_budget(size_t budget, size_t need) { return need <= 64 * 1024 || need <= budget; }
+bool lds_ok(const void* kernel, size_t need) {
+    return need <= 64 * 1024 || need <= lds_dyn_budget(kernel);   // (the default limit needs no attribute)
+}
 bool lds_fits(const void* kernel, const char* name, size_t need) {
-    if (need <= 64 * 1024) return true;   // (the default limit; no attribute needed)
-    const size_t b = lds_dyn_budget(kernel);
-    if (need <= b) return true;
-    launch_refused(name, need, b);
+    if (lds_ok(kernel, need)) return true;
+    launch_refused(name, need, lds_dyn_budget(kernel));
     return false;
 }
 

@@ -268,6 +268,10 @@ int launch_check(const char* stage, const char* file, int line);
     } while (0)
 // true (launch) when need fits the kernel's budget, else records the refusal
 bool lds_fits(const void* kernel, const char* name, size_t need);
+// the same rule (the 64 KiB default, or the derived budget) without recording anything: for path
+// eligibility tests and launchers that have a fallback
+bool lds_ok(const void* kernel, size_t need);
+bool lds_ok_budget(size_t budget, size_t need);
 size_t msr_request_bytes();                  // dynamic LDS of msr_kernel
 size_t hetrd_request_bytes(int d, int blk);  // ... of hetrd_kernel (blk = 0) / hetrd_blk_kernel (blk = 1)
 

@@ -34,8 +34,8 @@
 namespace ace {
 
 namespace {
-constexpr int SPEC_CHUNK = 256;
-constexpr double kOrtol = 1e-5;   // cluster separation, relative to ||T|| (see trieig_kernel)   // realisations per launch (C = 0.9 MiB each at m_t = 243)
+constexpr int SPEC_CHUNK = 256;   // realisations per launch (C = 0.9 MiB each at m_t = 243)
+constexpr double kOrtol = 1e-5;   // cluster separation, relative to ||T|| (see trieig_kernel)
 
 // per-realisation scratch layout (units: doubles)
 struct SpecLayout {
@@ -290,63 +290,20 @@ __global__ __launch_bounds__(256) void spec_form_c_kernel(int mt, const double* 
 // HB_NB + 2 passes over the trailing matrix instead of hetrd_kernel's 2 HB_NB (read + write per step):
 // the kernel is bound by that traffic (the matrices live in the L2 / MALL).  The outputs are hetrd_kernel's:
 // d, e, tau and reflector k in row k of C.
-#ifndef ACE_HB_NB
-#define ACE_HB_NB 4   // (r05: full square 4 against 8 +4.5 %; lower + pairs 2 against 4 +1.5 %; with the DPP sums 4 against 2 +2 %)
-#endif
-#ifndef ACE_HB_DPP
-#define ACE_HB_DPP 1   // hetrd_blk's reductions on DPP (wave_sum_dpp; r05: PhaseLift 75.6 -> 77.6 rec/s)
-#endif
-#ifndef ACE_HB_TR
-#define ACE_HB_TR 1   // lower-triangle product: rows per lane and task
-#endif
-#ifndef ACE_HB_CPAR
-#define ACE_HB_CPAR 1   // hetrd_blk: the panel corrections' wave sums for all q side by side
-#endif
-#ifndef ACE_HB_SYNC1
-#define ACE_HB_SYNC1 1   // hetrd_blk's block sums with one barrier (block_sum_dpp1; r05: +0.5 %)
-#endif
-#if ACE_HB_DPP && ACE_HB_SYNC1
-#define ACE_HB_BSUM block_sum_dpp1
-#define ACE_HB_WSUM wave_sum_dpp
-#elif ACE_HB_DPP
-#define ACE_HB_BSUM block_sum_dpp
-#define ACE_HB_WSUM wave_sum_dpp
-#else
-#define ACE_HB_BSUM block_sum
-#define ACE_HB_WSUM wave_sum
-#endif
-#ifndef ACE_HB_TPAIR
-#define ACE_HB_TPAIR 1   // trailing update by column pairs (balanced lower triangle; r05: +3 %)
-#endif
-#ifndef ACE_HB_TB
-#define ACE_HB_TB 4   // trailing-update rows per memory round trip
-#endif
-constexpr int HB_TB = ACE_HB_TB;
-#ifndef ACE_HB_UNROLL
-#define ACE_HB_UNROLL 4   // rows of the Hermitian product in flight per thread
-#endif
-#ifndef ACE_HB_THREADS
-#define ACE_HB_THREADS 1024
-#endif
-constexpr int HB_NB = ACE_HB_NB;             // panel width (PhaseLift's prox)
-#ifndef ACE_HB_NB_SPEC
-#define ACE_HB_NB_SPEC 2   // panel width of the spectral initialisation (one matrix per realisation, latency-bound batches)
-#endif
-constexpr int HB_NB_SPEC = ACE_HB_NB_SPEC;
-constexpr int HB_THREADS = ACE_HB_THREADS;   // threads per matrix
-constexpr int HB_COLS = 256;                 // threads per row group of the Hermitian product
-constexpr int HB_RB = HB_THREADS / HB_COLS;  // row groups
-// ACE_HB_LOWER: the Hermitian product and the trailing update touch only the lower triangle (j >= i) of
-// the trailing matrix: half the bytes of the full square (row sums reduced across each DPP row of 16 lanes)
-#ifndef ACE_HB_LOWER
-#define ACE_HB_LOWER 1   // (r05: half the HBM bytes of the full square, 60.6 -> 29.8 GB per 512-matrix launch; 70.3 -> 71.4 rec/s)
-#endif
+// Fixed geometry (r05 A/B measurements; the variants measured and not kept were removed in r06):
+// panels of HB_NB = 4 columns in the prox (2 in the spectral initialisation, whose small batches are
+// latency-bound), 1024 threads per matrix, the lower triangle only (half the bytes of the full square; row sums
+// reduced across each DPP row of 16 lanes), the reductions on DPP with one barrier per block sum, the
+// corrections' wave sums for all q side by side, the trailing update by balanced column pairs with HB_TB rows
+// per memory round trip.
+constexpr int HB_NB = 4;        // panel width (PhaseLift's prox)
+constexpr int HB_NB_SPEC = 2;   // panel width of the spectral initialisation
+constexpr int HB_THREADS = 1024;   // threads per matrix
+constexpr int HB_TB = 4;        // trailing-update rows per memory round trip
 constexpr int HB_NW = HB_THREADS / 64;   // waves
 __host__ __device__ constexpr int hb_strips(int mt) { return (mt + 63) >> 6; }
 size_t hetrd_blk_lds(int mt, int nb = HB_NB) {
-    size_t b = (size_t)mt * 16 * (2 * nb + 2);
-    if (ACE_HB_LOWER) b += (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
-    return b;
+    return (size_t)mt * 16 * (2 * nb + 2) + (size_t)hb_strips(mt) * mt * 16 + (size_t)(HB_NW + hb_strips(mt)) * 64 * 16;
 }
 template <int NB>
 __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* scratch, SpecLayout lay, const int* active) {
@@ -358,19 +315,14 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
     d2* v = Wp + NB * mt;                // current reflector, entry i = row k + 1 + i
     d2* w = v + mt;
     __shared__ double red[16 * 4 * NB];   // (block_sum: 16 waves; the corrections: [q][wave][4])
-#if ACE_HB_LOWER
     d2* rowp = w + mt;                        // [strip][row]: row sums of the lower triangle, per 64-column strip
     d2* colp = rowp + hb_strips(mt) * mt;     // [wave + strip][64]: column sums, per wave and strip
-#else
-    __shared__ d2 part[HB_RB][HB_COLS];
-#endif
     __shared__ d2 s_tau, s_scal, s_cw[NB], s_cv[NB];
     double* base = scratch + b * lay.stride;
     d2* C = reinterpret_cast<d2*>(base + lay.C);
     double* dd = base + lay.dd;
     double* ee = base + lay.ee;
     d2* taus = reinterpret_cast<d2*>(base + lay.tau);
-    const int col = t % HB_COLS, rb = t / HB_COLS;
     auto cj = [](d2 a) { return make_double2(a.x, -a.y); };
     for (int k0 = 0; k0 + 1 < mt; k0 += NB) {
         const int nbp = min(NB, mt - 1 - k0);
@@ -382,20 +334,14 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             double s1[1] = {0.0};
             for (int i = t; i < L; i += HB_THREADS) {
                 const int c = k + 1 + i;
-#if ACE_HB_LOWER   // column k below the diagonal (the upper triangle is not kept)
+                // column k below the diagonal (the upper triangle is not kept)
                 d2 a = C[(long long)c * mt + k];
                 for (int q = 0; q < p; ++q)
                     a = csub(a, cadd(cmul(Vp[q * mt + c], cj(Wp[q * mt + k])), cmul(Wp[q * mt + c], cj(Vp[q * mt + k]))));
                 v[i] = a;   // x_i = A[k + 1 + i][k]
-#else
-                d2 a = C[(long long)k * mt + c];
-                for (int q = 0; q < p; ++q)
-                    a = csub(a, cadd(cmul(Vp[q * mt + k], cj(Wp[q * mt + c])), cmul(Wp[q * mt + k], cj(Vp[q * mt + c]))));
-                v[i] = cj(a);   // x_i = A[k + 1 + i][k]
-#endif
                 if (i > 0) s1[0] += cabs2(a);
             }
-            ACE_HB_BSUM<1>(s1, red);
+            block_sum_dpp1<1>(s1, red);
             if (t == 0) {   // zlarfg
                 const d2 alpha = v[0];
                 const double xn2 = s1[0];
@@ -429,7 +375,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             }
             // the panel's corrections to C22 v: s_q = W_q^H v, t_q = V_q^H v (L < 1024: one entry per thread)
             __syncthreads();
-#if ACE_HB_CPAR   // every q's dot products first, then their wave sums side by side (independent chains)
+            // every q's dot products first, then their wave sums side by side (independent chains)
             if (p > 0) {
                 d2 a[NB], c2[NB];
 #pragma unroll
@@ -447,8 +393,8 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {
                     if (q >= p) break;
-                    const double a0 = ACE_HB_WSUM(a[q].x), a1 = ACE_HB_WSUM(a[q].y), c0 = ACE_HB_WSUM(c2[q].x),
-                                 c1 = ACE_HB_WSUM(c2[q].y);
+                    const double a0 = wave_sum_dpp(a[q].x), a1 = wave_sum_dpp(a[q].y), c0 = wave_sum_dpp(c2[q].x),
+                                 c1 = wave_sum_dpp(c2[q].y);
                     if ((t & 63) == 0) {
                         red[(q * 16 + (t >> 6)) * 4 + 0] = a0;
                         red[(q * 16 + (t >> 6)) * 4 + 1] = a1;
@@ -457,23 +403,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                     }
                 }
             }
-#else
-            for (int q = 0; q < p; ++q) {
-                d2 a = make_double2(0.0, 0.0), c2 = a;
-                for (int i = t; i < L; i += HB_THREADS) {
-                    const int r = k + 1 + i;
-                    a = cadd(a, cmulc(Wp[q * mt + r], v[i]));
-                    c2 = cadd(c2, cmulc(Vp[q * mt + r], v[i]));
-                }
-                const double a0 = ACE_HB_WSUM(a.x), a1 = ACE_HB_WSUM(a.y), c0 = ACE_HB_WSUM(c2.x), c1 = ACE_HB_WSUM(c2.y);
-                if ((t & 63) == 0) {
-                    red[(q * 16 + (t >> 6)) * 4 + 0] = a0;
-                    red[(q * 16 + (t >> 6)) * 4 + 1] = a1;
-                    red[(q * 16 + (t >> 6)) * 4 + 2] = c0;
-                    red[(q * 16 + (t >> 6)) * 4 + 3] = c1;
-                }
-            }
-#endif
             __syncthreads();
             if (t < p) {   // fixed order over the 16 waves
                 double sw0 = 0.0, sw1 = 0.0, sv0 = 0.0, sv1 = 0.0;
@@ -490,7 +419,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             __syncthreads();
             // p = tau (C22 v - V s - W t): the sweep only reads C22 (thread (col, rb): rows rb, rb + 4, ...)
             const long long r0 = (long long)(k + 1) * mt + (k + 1);
-#if ACE_HB_LOWER
             // From the lower triangle only: element (j, i), j >= i, adds conj(c) v_j to p_i (column sums) and,
             // for j > i, c v_i to p_j (row sums).  Tasks are 4-row groups of 64-column strips (strip s: columns
             // 64s.., rows 64s..L-1), dealt to the waves in contiguous runs; lane (jr, ic) reads row jr of the
@@ -499,7 +427,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
             // the run (slot wave + strip: unique, since the runs are contiguous).
             {
                 const int ns = hb_strips(L), wv = t >> 6, jr = (t & 63) >> 4, ic = t & 15;
-                constexpr int TR = ACE_HB_TR;   // rows per lane and task (a task: 4 TR rows of a strip)
+                constexpr int TR = 1;   // rows per lane and task (a task: 4 TR rows of a strip)
                 auto ngr = [&](int s) { return (L - 64 * s + 4 * TR - 1) / (4 * TR); };
                 int G = 0;
                 for (int s = 0; s < ns; ++s) G += ngr(s);
@@ -581,34 +509,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 }
                 __syncthreads();
             }
-#else
-            const int ncol = HB_COLS, nrb = HB_RB, acol = col, arb = rb;
-            d2* partf = &part[0][0];   // [nrb][ncol]
-            for (int i0 = 0; i0 < L; i0 += ncol) {
-                const int i = i0 + acol;
-                double ar = 0.0, ai = 0.0;
-                if (i < L && arb < nrb) {
-                    const d2* cc = C + r0 + i;
-#pragma unroll ACE_HB_UNROLL
-                    for (int j = arb; j < L; j += nrb) {
-                        const d2 c = cc[(long long)j * mt], vj = v[j];
-                        ar += c.x * vj.x + c.y * vj.y;
-                        ai += c.x * vj.y - c.y * vj.x;
-                    }
-                }
-                if (arb < nrb) partf[arb * ncol + acol] = make_double2(ar, ai);
-                __syncthreads();
-                if (arb == 0 && i < L) {
-                    d2 acc = partf[acol];
-                    for (int q = 1; q < nrb; ++q) acc = cadd(acc, partf[q * ncol + acol]);
-                    const int r = k + 1 + i;
-                    for (int q = 0; q < p; ++q)
-                        acc = csub(acc, cadd(cmul(Vp[q * mt + r], s_cw[q]), cmul(Wp[q * mt + r], s_cv[q])));
-                    w[i] = cmul(tau, acc);
-                }
-                __syncthreads();
-            }
-#endif
             // w = p - (tau / 2) (p^H v) v
             double s2[2] = {0.0, 0.0};
             for (int i = t; i < L; i += HB_THREADS) {
@@ -616,7 +516,7 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 s2[0] += q.x;
                 s2[1] += q.y;
             }
-            ACE_HB_BSUM<2>(s2, red);
+            block_sum_dpp1<2>(s2, red);
             const d2 alpha2 = cscale(cmul(tau, make_double2(s2[0], s2[1])), -0.5);
             for (int i = t; i < L; i += HB_THREADS) {
                 const d2 wi = cadd(w[i], cmul(alpha2, v[i]));
@@ -626,7 +526,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
         }
         // the trailing matrix past the panel: C -= sum_q (V_q W_q^H + W_q V_q^H), one read and write
         const int kn = k0 + nbp, L2 = mt - kn;
-#if ACE_HB_LOWER && ACE_HB_TPAIR
         // the lower triangle's columns in pairs (i, L2 - 1 - i): every thread of a pair's HB_THREADS / 128 row groups
         // updates L2 + 1 entries over the two columns (one column from 0 would do L2 alone)
         {
@@ -669,47 +568,6 @@ __global__ __launch_bounds__(HB_THREADS) void hetrd_blk_kernel(int mt, double* s
                 }
             }
         }
-        if (0)
-#endif
-        {
-        const int ncol2 = HB_COLS, nrb2 = HB_RB, tcol = col, trb = rb;
-        for (int i0 = 0; i0 < L2; i0 += ncol2) {
-            const int i = i0 + tcol;
-            if (i >= L2 || trb >= nrb2) continue;
-            const int ci = kn + i;
-            d2 vq[NB], wq[NB];
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                vq[q] = cj(Vp[q * mt + ci]);
-                wq[q] = cj(Wp[q * mt + ci]);
-            }
-#if ACE_HB_LOWER
-            const int js = i + (((trb - i) % nrb2) + nrb2) % nrb2;   // rows j >= i
-#else
-            const int js = trb;
-#endif
-            // HB_TB rows per memory round trip: their loads issued together ahead of the updates and stores
-            for (int j0 = js; j0 < L2; j0 += HB_TB * nrb2) {
-                d2 cb[HB_TB];
-#pragma unroll
-                for (int u = 0; u < HB_TB; ++u) {
-                    const int j = j0 + u * nrb2;
-                    cb[u] = j < L2 ? C[(long long)(kn + j) * mt + ci] : make_double2(0.0, 0.0);
-                }
-#pragma unroll
-                for (int u = 0; u < HB_TB; ++u) {
-                    const int j = j0 + u * nrb2;
-                    if (j >= L2) break;
-                    const int rj = kn + j;
-                    d2 c = cb[u];
-#pragma unroll
-                    for (int q = 0; q < NB; ++q)
-                        c = csub(c, cadd(cmul(Vp[q * mt + rj], wq[q]), cmul(Wp[q * mt + rj], vq[q])));
-                    C[(long long)rj * mt + ci] = c;
-                }
-            }
-        }
-        }
         __syncthreads();
     }
     if (t == 0) {
@@ -731,29 +589,16 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e, int
     }
     return cnt;
 }
-// Bisection stops at LAPACK dstebz's width max(2 ulp |lambda|, ulp ||T||, pivmin) (its default ABSTOL <= 0); the
-// relative-only test (ACE_TE_ABSTOL=0) refined eigenvalues far below ||T|| to their own ulp, ~20 rounds more
-#ifndef ACE_TE_ABSTOL
-#define ACE_TE_ABSTOL 1
-#endif
-#ifndef ACE_TE_GRID
-#define ACE_TE_GRID 512   // (0: off; else the number of grid cells, even; r05: PhaseLift 69.4 -> 69.9 rec/s)
-#endif
-constexpr int TE_GRID = ACE_TE_GRID > 0 ? ACE_TE_GRID : 2;
-#ifndef ACE_TE_FUSE
-#define ACE_TE_FUSE 1
-#endif
-#ifndef ACE_TE_SWEEPS
-#define ACE_TE_SWEEPS 2
-#endif
+// Bisection stops at LAPACK dstebz's width max(2 ulp |lambda|, ulp ||T||, pivmin) (its default ABSTOL <= 0); a
+// relative-only test refined eigenvalues far below ||T|| to their own ulp, ~20 rounds more (r05).
+// TE_GRID: one shared round of Sturm counts at TE_GRID + 1 even points first (r05: PhaseLift 69.4 -> 69.9 rec/s)
+constexpr int TE_GRID = 512;
 // inverse-iteration solves per eigenvector: with the eigenvalue to full precision, one solve leaves the other
 // eigenvectors at <= eps ||T|| / gap of the vector (gap >= kOrtol ||T||, closer ones are a cluster and projected
 // out), the second squares that (r05: 3 -> 2, PhaseLift 67.6 -> 69.3 rec/s; LAPACK dstein stops 2 solves after
 // its growth test passes)
-constexpr int TE_SWEEPS = ACE_TE_SWEEPS;
-#ifndef ACE_TE_PF
-#define ACE_TE_PF 8
-#endif
+constexpr int TE_SWEEPS = 2;
+constexpr int TE_PF = 8;   // rows of the LU solves' loads issued ahead of their dependent chain
 // 1 / x from the v_rcp_f64 seed and two Newton steps (~1 ulp; x finite and nonzero here)
 __device__ __forceinline__ double rcp_nr(double x) {
     double y = __builtin_amdgcn_rcp(x);
@@ -795,9 +640,6 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                                                      int* status, int status_off, const int* active) {
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (active && !active[b]) return;
-#ifdef ACE_TE_STAMPS   // phase times of work-groups 0..3 (10 ns units): bisection, clusters, inverse iteration
-    const unsigned long long te0 = __builtin_amdgcn_s_memrealtime();
-#endif
     extern __shared__ double smem[];
     double* d = smem;
     double* e = smem + mt;
@@ -848,7 +690,6 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     __syncthreads();
     const int k = s_k;
     double* lam = base + lay.lam;
-#if ACE_TE_GRID
     // one shared round first: Sturm counts at TE_GRID + 1 even points of [gl, gu] (two per thread), so that
     // every eigenvalue starts from its grid cell instead of the whole interval (log3(TE_GRID) rounds fewer)
     __shared__ int gcnt[TE_GRID + 1];
@@ -861,11 +702,9 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     }
     if (t == 0) gcnt[0] = 0;
     __syncthreads();
-#endif
     for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
         const int j = mt - 1 - q;
         double lo = gl, hi = gu;
-#if ACE_TE_GRID
         {   // the first grid point with more than j eigenvalues below it (counts are monotone in x)
             int a0 = 0, a1 = TE_GRID;
             while (a1 - a0 > 1) {
@@ -878,13 +717,9 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                 if (a1 < TE_GRID) hi = gl + a1 * gh;
             }
         }
-#endif
         for (int it = 0; it < 200; ++it) {
-#if ACE_TE_ABSTOL   // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
+            // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
             if (hi - lo <= fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), fmax(eps * tn, pivmin))) break;
-#else
-            if (hi - lo <= 2.0 * eps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
-#endif
             const double stp = (hi - lo) * (1.0 / 3.0);
             const double x0 = lo + stp, x1 = fmax(x0, hi - stp);
             int c0, c1;
@@ -902,9 +737,6 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         lam[q] = 0.5 * (lo + hi);
     }
     __syncthreads();
-#ifdef ACE_TE_STAMPS
-    const unsigned long long te1 = __builtin_amdgcn_s_memrealtime();
-#endif
     double* cl = base + lay.cl;
     if (t == 0) {
         int nc = 0;
@@ -973,18 +805,17 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
             // other; the loads of a block of TE_PF rows are issued together ahead of the block's dependent
             // chain (they depend on the row index only), so the chain waits for one memory round trip per
             // block instead of one per row.  Same operations in the same order as the row-by-row form.
-            constexpr int TE_PF = ACE_TE_PF;
             // the normalisation of a solve's result is applied as the next solve loads it (sc): the same
             // products fl(y inv) as a separate scaling pass, without its round trips
             double sc = 1.0;
             for (int sweep = 0; sweep < TE_SWEEPS; ++sweep) {
-                double cur = ACE_TE_FUSE ? at(5, 0) * sc : at(5, 0);
+                double cur = at(5, 0) * sc;
                 for (int i0 = 0; i0 + 1 < mt; i0 += TE_PF) {  // dgttrs, L
                     double nx[TE_PF], fv[TE_PF], pv[TE_PF];
 #pragma unroll
                     for (int u = 0; u < TE_PF; ++u) {
                         const int i = min(i0 + u, mt - 2);
-                        nx[u] = ACE_TE_FUSE ? at(5, i + 1) * sc : at(5, i + 1);
+                        nx[u] = at(5, i + 1) * sc;
                         fv[u] = at(0, i);
                         pv[u] = at(4, i);
                     }
@@ -1042,7 +873,6 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                     for (int i = 0; i < mt; ++i) nrm += at(5, i) * at(5, i);
                 }
                 const double inv = 1.0 / sqrt(nrm);
-#if ACE_TE_FUSE
                 if (sweep < TE_SWEEPS - 1) {
                     sc = inv;
                 } else {   // the vector out, 32 rows per round trip
@@ -1056,36 +886,10 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                             if (i0 + u < mt) zq[i0 + u] = tv[u] * inv;
                     }
                 }
-#else
-                if (sweep < TE_SWEEPS - 1)
-                    for (int i = 0; i < mt; ++i) at(5, i) *= inv;
-                else
-                    for (int i = 0; i < mt; ++i) zq[i] = at(5, i) * inv;
-#endif
             }
         }
     }
     if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
-#ifdef ACE_TE_STAMPS
-    __syncthreads();
-    if (t == 0 && b < 4) {
-        int mx = 0;
-        for (int c = 0; c < ncl; ++c) mx = max(mx, (int)(cl[c + 1] - cl[c]));
-        printf("trieig b %d mt %d k %d ncl %d maxcl %d lanes %d: bisect %llu invit %llu (x10ns)\n", b, mt, k, ncl, mx,
-               lay.lanes, te1 - te0, __builtin_amdgcn_s_memrealtime() - te1);
-    }
-#endif
-#ifdef ACE_DEBUG_SPEC
-    __syncthreads();
-    if (t == 0 && b < 2) {
-        int nl = 0, nz = 0;
-        for (int q = 0; q < k; ++q) {
-            if (!isfinite(lam[q])) ++nl;
-            for (int i = 0; i < mt; ++i) nz += !isfinite(Z[(long long)q * mt + i]);
-        }
-        printf("trieig b %d k %d ncl %d nan lam %d z %d lam0 %g lam_k-1 %g tn %g\n", b, k, ncl, nl, nz, lam[0], lam[k - 1], tn);
-    }
-#endif
 }
 
 // u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),
@@ -1277,7 +1081,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
     const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 24;
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() &&
-                     hetrd_blk_lds(n, HB_NB_SPEC) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>));
+                     lds_ok(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>), hetrd_blk_lds(n, HB_NB_SPEC));
     const int chunk = primal_chunk(mt, n, batch);
     double* Ast = scratch + (((size_t)lay.stride * chunk + 31) & ~(size_t)31);
     for (int b0 = 0; b0 < batch; b0 += chunk) {
@@ -1312,7 +1116,7 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
     const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 24;
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() &&
-                     hetrd_blk_lds(mt, HB_NB_SPEC) <= lds_dyn_budget(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>));
+                     lds_ok(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>), hetrd_blk_lds(mt, HB_NB_SPEC));
     const int ldb = pr ? pr->m : mt;   // per-realisation partitions: the full K and B, rows per realisation
     for (int b0 = 0; b0 < batch; b0 += SPEC_CHUNK) {
         const int nb = batch - b0 < SPEC_CHUNK ? batch - b0 : SPEC_CHUNK;
@@ -1469,8 +1273,9 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
     // the blocked reduction (hetrd_blk_kernel): blk = 1 (the caller reads ACE_HETRD_BLK once per solve)
-    if (blk && !lds_fits(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB>), "hetrd_blk_kernel", hetrd_blk_lds(d)))
-        blk = 0;   // (the unblocked reduction takes any d hetrd_lds_ok admits)
+    // (a check that records nothing: the unblocked reduction takes any d hetrd_lds_ok admits, so a blocked form
+    // that does not fit is a choice of path, not a refused launch)
+    if (blk && !lds_ok(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB>), hetrd_blk_lds(d))) blk = 0;
     if (blk) {
         // (all matrices in one launch: launches of 128 / 256 matrices, whose working set would stay in the MALL,
         // measured 37.8 / 54.1 against 60.4 rec/s -- the reduction is bound by its work-groups' latency, not HBM)

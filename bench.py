@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--no-default-profile", action="store_true",
                     help="refine_input: skip the comparison run with the default rank profile for every realisation")
     ap.add_argument("--cpu-recoveries", type=int, default=0, help="CPU sample size (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="time budget of a sampled CPU baseline")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="unit mode: skip the config 3 / 4 / 5 and pipeline objects of the default line")
     ap.add_argument("--no-prof", action="store_true", help="disable live per-kernel event timing")
     ap.add_argument("--mode", default="unit",
                     choices=["unit", "config5", "pipeline", "phaselift", "beamformer", "driver", "refine"])
@@ -415,6 +418,27 @@ def cpu_baseline(args, n_samples, private, variant=None, A_host=None):
 
 # ------------------------------------------------------------------ unit / config5
 
+def _work_accounting(per_gpu, variant, m, n, tx, iters, msp_frac):
+    """SURVEY.md §8(d) prices a recovery in the reference's U-form (X = U (A^H (Y - M/mu) + Z - N/mu) with
+    U = inv(A^H A + I) n x n: 8 (3mn + n^2 + 3 tx^3) flops per iteration for A2only, 8 (3mn + n^2) for
+    A2nuclear); the build executes the Woodbury / m-space form instead (g = G T with
+    G = (I + K)^-1 m x m, 8 m^2 f64 flops per iteration, the Aᴴ / A applies on the int8 digit planes for the
+    iterations outside the m-space form).  Both rates per GPU, so that a U-form rate above the FP64 peak
+    reads as what it is: less work done, not a faster chip."""
+    u = 8.0 * (3 * m * n + n * n + (3 * tx ** 3 if variant == "A2only" else 0)) * iters
+    ex64 = 8.0 * m * m * iters
+    ex8 = (1.0 - msp_frac) * iters * 2 * 2.0 * 8 * (2 * m) * (2 * n) if variant == "A2only" else None
+    d = {"u_form_flops_per_recovery": u, "u_form_tflops_per_gpu": round(per_gpu * u / 1e12, 2),
+         "u_form_frac_of_fp64_peak": round(per_gpu * u / 1e12 / PEAK_FP64_TFLOPS, 3),
+         "executed_f64_flops_per_recovery": ex64, "executed_f64_tflops_per_gpu": round(per_gpu * ex64 / 1e12, 2),
+         "executed_f64_frac_of_peak": round(per_gpu * ex64 / 1e12 / PEAK_FP64_TFLOPS, 3)}
+    if ex8 is not None:
+        d["executed_int8_ops_per_recovery"] = ex8
+        d["executed_int8_tops_per_gpu"] = round(per_gpu * ex8 / 1e12, 1)
+    d["note"] = _work_accounting.__doc__.split("\n\n")[0].replace("\n    ", " ")
+    return d
+
+
 def unit_bench(args, private, dev, rank, world, workload=None):
     """One unit-metric measurement (regime S or P, or a given workload); the JSON line dict on rank 0.
     workload: {"tag", "name", "variant", "A" (device codebook), "A_host", "bsz", "first", "counts",
@@ -644,6 +668,7 @@ def unit_bench(args, private, dev, rank, world, workload=None):
         "cpu_baseline": cpu,
         "kernels_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
         "msp_frac": round(msp_frac, 4),
+        "work_accounting": _work_accounting(total / elapsed / world, variant, m, n, tx, args.iters, msp_frac),
         "checks": {"all_iters_ran": it_ok, "finite": finite},
     }
 
@@ -769,7 +794,7 @@ def bench_pipeline(args, dev, rank, world):
             tag="pipeline", batch=bsz)
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
-        return
+        return None
     its = res.stage_iters.cpu().numpy()
     Xh = res.X.cpu().numpy()
     Hh = H.cpu().numpy()
@@ -796,7 +821,7 @@ def bench_pipeline(args, dev, rank, world):
     }
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline_pipeline(args, A[0].cpu().numpy(), B.cpu().numpy(), tr)
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def cpu_baseline_pipeline(args, A, B, tr):   # tr: [batch][restarts][m_t]
@@ -805,7 +830,7 @@ def cpu_baseline_pipeline(args, A, B, tr):   # tr: [batch][restarts][m_t]
     sys.path.insert(0, str(ROOT / "oracle"))
     import ace_oracle as O
     k, t0 = 0, time.perf_counter()
-    while k < min(len(B), args.cpu_recoveries or 8) and (k == 0 or time.perf_counter() - t0 < 20.0):
+    while k < min(len(B), args.cpu_recoveries or 8) and (k == 0 or time.perf_counter() - t0 < args.cpu_seconds):
         O.infer_low_rank_pipeline(A, B[k], args.tx, args.tx, list(tr[k]),
                                   variant=O.VARIANT_A2ONLY if args.variant == "A2only" else O.VARIANT_NUCLEAR)
         k += 1
@@ -857,7 +882,7 @@ def bench_phaselift(args, dev, rank, world):
             "eig with vectors), A*(g) 8 d^2 m, assembly 8 d^3, A(z) 8 m d^2", tag="phaselift", batch=bsz)
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
-        return
+        return None
     its = res.iters.cpu().numpy()
     names = {"setup": "setup (reduction)", "pre": "y, A_y, gradient", "apply_AH": "A*(g) GEMM",
              "zstep": "prox eig (tridiag+bisect+invit+backxf)", "apply_G": "prox assembly GEMM",
@@ -890,7 +915,7 @@ def bench_phaselift(args, dev, rank, world):
     }
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline_phaselift(args, Phi.cpu().numpy(), b[:4].cpu().numpy())
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def cpu_baseline_phaselift(args, Phi, b):
@@ -900,7 +925,7 @@ def cpu_baseline_phaselift(args, Phi, b):
     sys.path.insert(0, str(ROOT / "oracle"))
     import tfocs_oracle as T
     k, t0 = 0, time.perf_counter()
-    while k < len(b) and (k == 0 or time.perf_counter() - t0 < 20.0):
+    while k < len(b) and (k == 0 or time.perf_counter() - t0 < args.cpu_seconds):
         T.my_phaselift_reduced(b[k], Phi, maxIts=args.iters)
         k += 1
     dt = time.perf_counter() - t0
@@ -944,7 +969,7 @@ def bench_beamformer(args, dev, rank, world):
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     elapsed = _max_over_ranks(elapsed, dev, world)
     if rank != 0:
-        return
+        return None
     st = res.status.cpu().numpy()
     per_unit = 16.0 * tx * tx + 2 * tx + 8 + 8 + 4        # read H; write codes, idx, rss, status
     achieved = per_unit * bsz / (kern_ms * 1e-3) / 1e9
@@ -962,7 +987,7 @@ def bench_beamformer(args, dev, rank, world):
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_beamformer(tx, H[: 2000].cpu().numpy())
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def cpu_baseline_beamformer(tx, Hs):
@@ -1007,7 +1032,7 @@ def bench_driver(args, dev, rank, world):
     laptop): the only published timing of the path, a qualitative upper bound."""
     from ace_amd import engine
     if rank != 0:
-        return
+        return None
     tx = 16
     amp, ang, rss = driver_trace(tx, 17)
     eng = engine.start_matlab()
@@ -1049,7 +1074,7 @@ def bench_driver(args, dev, rank, world):
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_driver(tx, amp, ang, rss)
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def cpu_baseline_driver(tx, amp, ang, rss):
@@ -1075,6 +1100,56 @@ def cpu_baseline_driver(tx, amp, ang, rss):
                       f"{_cpu_model()}"}
 
 
+# ------------------------------------------------------------------ the other configs on the default line
+
+def _sub(args, **kw):
+    a = argparse.Namespace(**vars(args))
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def _leg_summary(ln, keep=()):
+    """A config's own line reduced to what the default line carries for it."""
+    if ln is None:
+        return None
+    d = {k: ln[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "scaling", "config",
+                            "roofline", "cpu_baseline") if k in ln}
+    for k in keep:
+        if k in ln:
+            d[k] = ln[k]
+    return d
+
+
+def config_legs(args, dev, rank, world):
+    """BASELINE.json configs[2..4] and the pipeline, each measured with its own steps inside the default run
+    (every config driver-observed): (key, thunk returning the object on rank 0).  Steps are
+    fewer for the slow workloads so that the whole default line stays within a few minutes; each object
+    carries its own ms_per_step x steps, roofline (live HIP events + the newest PMC traffic of its tag) and
+    CPU baseline (a shorter sample budget than the modes' own lines)."""
+    cpu_s = min(args.cpu_seconds, 8.0)
+
+    def config3():
+        a = _sub(args, variant="A2nuclear", cpu_seconds=cpu_s)
+        ln = unit_bench(a, False, dev, rank, world)
+        return _leg_summary(ln, ("kernels_ms", "checks", "roofline_msr")) if rank == 0 else None
+
+    def config5():
+        a = _sub(args, cpu_seconds=cpu_s, global_batch=CONFIG5_GLOBAL)
+        ln = unit_bench(a, False, dev, rank, world, config5_workload(a, rank, world, dev))
+        return _leg_summary(ln, ("kernels_ms", "checks")) if rank == 0 else None
+
+    def config4():
+        a = _sub(args, batch=512, steps=1, warmup=1, cpu_seconds=cpu_s)
+        return _leg_summary(bench_phaselift(a, dev, rank, world), ("iters_all", "device_time_shares"))
+
+    def pipeline():
+        a = _sub(args, batch=4096, steps=1, warmup=1, cpu_seconds=cpu_s, cpu_recoveries=2)
+        return _leg_summary(bench_pipeline(a, dev, rank, world), ("stage_iters_mean", "device_time_shares"))
+
+    return [("config3", config3), ("config5_shard", config5), ("config4", config4), ("pipeline", pipeline)]
+
+
 # ------------------------------------------------------------------ main
 
 def main():
@@ -1093,8 +1168,10 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     if args.mode in ("pipeline", "phaselift", "beamformer", "driver"):
-        {"pipeline": bench_pipeline, "phaselift": bench_phaselift, "beamformer": bench_beamformer,
-         "driver": bench_driver}[args.mode](args, dev, rank, world)
+        line = {"pipeline": bench_pipeline, "phaselift": bench_phaselift, "beamformer": bench_beamformer,
+                "driver": bench_driver}[args.mode](args, dev, rank, world)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
     elif args.mode == "refine":   # the unit on the reference's own refinement alone (refine_input of the unit line)
         ri = refine_input_bench(args, dev, rank, world)
         if rank == 0:
@@ -1135,6 +1212,11 @@ def main():
                 ri = leg(lambda: refine_input_bench(args, dev, rank, world))
                 if rank == 0:
                     line["refine_input"] = ri
+            if not args.no_configs and args.tx == 32:
+                for key, fn in config_legs(args, dev, rank, world):
+                    r = leg(fn)
+                    if rank == 0:
+                        line[key] = r
         if rank == 0:
             print(json.dumps(line), flush=True)
     if world > 1:

@@ -135,3 +135,16 @@ def test_phaselift_blocked_tridiagonalisation(gpu, monkeypatch):
         assert O.phase_aligned_rel_err(blk.sig[r], unb.sig[r]) <= 1e-9, r
     sig, _ = T.my_phaselift_reduced(b[0], Phi, maxIts=60)
     assert O.phase_aligned_rel_err(blk.sig[0], sig) <= 1e-8
+
+
+def test_phaselift_order_512_takes_the_unblocked_fallback(gpu):
+    """at d = m = 512 (32 antennas, 512 measurements; the reference's 32-antenna sweep reaches
+    d = 841 and 1024) the blocked reduction's LDS exceeds the CU, and the solver must take the unblocked
+    reduction instead of failing the solve with a refused launch (it used to record the refusal)."""
+    from ace_amd import phaselift_host
+    Phi, b = _problem(23, 32, 512, 2)
+    res = phaselift_host(Phi, b, maxIts=8)
+    assert (res.iters == 8).all() and np.isfinite(res.sig).all()
+    for r in range(2):
+        sig, ref = T.my_phaselift_reduced(b[r], Phi, maxIts=8)
+        assert O.phase_aligned_rel_err(res.sig[r], sig) <= 1e-8, r

@@ -39,7 +39,7 @@ CASES = [
     ("nms", "ace_nucmsp.hip", [r"nms_kernelILb0E", r"nms_kernelILb1E"], [64, 256]),
     ("hetrd", "ace_spectral.hip", [r"12hetrd_kernel"], [256, 1024]),
     ("hetrd_blk", "ace_spectral.hip", [r"16hetrd_blk_kernelILi4E", r"16hetrd_blk_kernelILi2E"],
-     [128, 256]),   # (the prox order d = m, §4; panels of 4 in the prox, 2 in the spectral initialisation)
+     [128, 243, 256]),   # (the prox order d = m, §4; the spectral order m_t = 243; panels of 4 / 2)
 ]
 
 _REMARK = re.compile(r"remark: Function Name: (\S+)|remark:\s+LDS Size \[bytes/block\]: (\d+)")
@@ -97,3 +97,18 @@ def test_unknown_kernel_is_an_error():
     from ace_amd import _lib
     with pytest.raises(_lib.AceError):
         _lib.lds_request("nope", 256)
+
+
+def test_prox_reduction_has_a_fitting_path_at_every_order(static_lds):
+    """the prox's blocked reduction does not fit the CU above d of about 470; the launcher
+    then takes hetrd_kernel (a choice of path, not a refusal).  At every order the PhaseLift host accepts
+    up to the reference's 32-antenna sweep (d = 841, 1024) one of the two must fit."""
+    from ace_amd import _lib
+    kernels = static_lds["ace_spectral.hip"]
+    st_blk = max(v for k, v in kernels.items() if re.search(r"16hetrd_blk_kernelILi4E", k))
+    st_unb = max(v for k, v in kernels.items() if re.search(r"12hetrd_kernel", k))
+    for d in (243, 256, 470, 512, 560, 841, 1024):
+        blk_fits = st_blk + _lib.lds_request("hetrd_blk", d) <= LDS_CU
+        unb_fits = st_unb + _lib.lds_request("hetrd", d) <= LDS_CU
+        assert blk_fits or unb_fits, d
+    assert st_blk + _lib.lds_request("hetrd_blk", 512) > LDS_CU   # (so the fallback is what d = 512 exercises)

@@ -9,7 +9,7 @@ tail -2 $O/tests.log
 echo "== smoke $(date +%T)"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -2 $O/smoke.log
-B="--no-cpu-baseline --no-regime-p --no-refine-input --no-prof"
+B="--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --no-prof"
 pmc() { local tag=$1 cnt=$2; shift 2; echo "== pmc $tag $cnt $(date +%T)"; timeout -k 10 -s KILL 300 rocprofv3 --pmc $cnt -d $O/${tag}_$cnt -o run --output-format csv -- python3 bench.py $B "$@" > $O/${tag}_$cnt.log 2>&1 || { tail -20 $O/${tag}_$cnt.log; exit 1; }; }
 pmc pipeline FETCH_SIZE --mode pipeline --steps 1 --warmup 0
 pmc pipeline WRITE_SIZE --mode pipeline --steps 1 --warmup 0

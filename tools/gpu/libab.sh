@@ -2,9 +2,9 @@
 # passes of each (FETCH_SIZE, WRITE_SIZE, separate runs):  bash tools/gpu/libab.sh <tag> <alt.so> ["bench args"]
 set -o pipefail
 export TMPDIR=/tmp
-TAG=$1; ALT=$2; ARGS=${3:-"--no-cpu-baseline --no-regime-p --no-refine-input --steps 5"}
+TAG=$1; ALT=$2; ARGS=${3:-"--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --steps 5"}
 O=gpurun_out/$TAG; mkdir -p $O
-B="--no-cpu-baseline --no-regime-p --no-refine-input --no-prof --steps 1 --warmup 1"
+B="--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --no-prof --steps 1 --warmup 1"
 for rep in 1 2; do
   for v in base alt; do
     L=2ace-mmwave-channel-estimation_amd/ace_amd/libace.so; [ $v = alt ] && L=$ALT

@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/${1:-prof}; R=${2:-r05_v1}; shift 2
 mkdir -p $O
 export TMPDIR=/tmp
-B="--no-cpu-baseline --no-regime-p --no-refine-input --no-prof"
+B="--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --no-prof"
 args() {
   case $1 in
     unit) echo "--steps 1 --warmup 1";;

@@ -5,7 +5,7 @@
 set -o pipefail
 O=gpurun_out/${1:-prof}; mkdir -p $O
 export TMPDIR=/tmp
-B="--no-cpu-baseline --no-regime-p --no-refine-input --no-prof"
+B="--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --no-prof"
 st() { local tag=$1; shift; echo "== stats $tag $(date +%T)"; timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/$tag -o run --output-format csv -- python3 bench.py $B "$@" > $O/$tag.log 2>&1 || { tail -20 $O/$tag.log; exit 1; }; }
 pmc() { local tag=$1 cnt=$2; shift 2; echo "== pmc $tag $cnt $(date +%T)"; timeout -k 10 -s KILL 300 rocprofv3 --pmc $cnt -d $O/${tag}_$cnt -o run --output-format csv -- python3 bench.py $B "$@" > $O/${tag}_$cnt.log 2>&1 || { tail -20 $O/${tag}_$cnt.log; exit 1; }; }
 st unit --steps 1 --warmup 1

@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/${1:-punit}; mkdir -p $O
 R=${2:-r03_v13}
 export TMPDIR=/tmp
-B="--no-cpu-baseline --no-regime-p --no-refine-input --no-prof"
+B="--no-cpu-baseline --no-regime-p --no-refine-input --no-configs --no-prof"
 echo "== stats $(date +%T)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 bench.py $B --steps 1 --warmup 1 > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do

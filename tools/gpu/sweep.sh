@@ -5,7 +5,7 @@ set -o pipefail
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
-B="--steps 10 --warmup 3 --no-cpu-baseline --no-regime-p --no-refine-input"
+B="--steps 10 --warmup 3 --no-cpu-baseline --no-regime-p --no-refine-input --no-configs"
 i=0
 for s in "$@"; do
   i=$((i+1))

@@ -12,7 +12,7 @@ from ._lib import path_counts  # noqa: F401
 from .pipeline import (inferLowRankV4_multi, inferLowRankV4, inferLowRank_Nuclear,  # noqa: F401
                        infer_low_rank_pipeline_host, infer_low_rank_pipeline_batch, draw_partitions,
                        PipelineResult, SpectralInitialize)
-from .phaselift import MyPhaseLift, phaselift_host, phaselift_batch, PhaseLiftResult  # noqa: F401
+from .phaselift import MyPhaseLift, phaselift_host, phaselift_batch, PhaseLiftResult, prox_eig_host  # noqa: F401
 from .beamformer import (svd_beamformer, svd_beamformer_compensation, codebook_beams,  # noqa: F401
                          svd_beamformer_host, svd_beamformer_batch, BeamResult)
 from . import synth, engine  # noqa: F401

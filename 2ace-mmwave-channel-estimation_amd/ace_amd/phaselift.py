@@ -42,6 +42,26 @@ LIB.ace_phaselift_solve_host.argtypes = [_cfgp, C.c_int, C.c_int, C.c_int, _dp, 
 LIB.ace_phaselift_solve_host.restype = C.c_int
 
 
+LIB.ace_prox_eig_host.argtypes = [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.POINTER(C.c_int32)]
+LIB.ace_prox_eig_host.restype = C.c_int
+
+
+def prox_eig_host(A, tau, path=2):
+    """The prox's eigensolver on host arrays (TFOCS/prox_trace.m:88-92): every eigenpair of the Hermitian A[b]
+    above tau[b], descending.  path 0 / 1 / 2: unblocked one-stage / blocked one-stage / two-stage reduction.
+    Returns (lam [batch][d], V [batch][d][d] with eigenvector q as row q, k [batch])."""
+    A = np.ascontiguousarray(np.asarray(A, dtype=np.complex128).reshape((-1,) + np.shape(A)[-2:]))
+    batch, d = A.shape[0], A.shape[1]
+    tau = np.ascontiguousarray(np.broadcast_to(np.asarray(tau, dtype=np.float64), (batch,)))
+    lam = np.zeros((batch, d))
+    V = np.zeros((batch, d, d), np.complex128)
+    k = np.zeros(batch, np.int32)
+    check(LIB.ace_prox_eig_host(batch, d, int(path), A.view(np.float64).ctypes.data_as(_dp), tau.ctypes.data_as(_dp),
+                                lam.ctypes.data_as(_dp), V.view(np.float64).ctypes.data_as(_dp),
+                                k.ctypes.data_as(C.POINTER(C.c_int32))))
+    return lam, V, k
+
+
 def phaselift_cfg(maxIts=4000, tol=1e-10, restart=200, lam=5e-2, **kw) -> PhaseLiftCfg:
     cfg = PhaseLiftCfg()
     LIB.ace_phaselift_cfg_default(C.byref(cfg))

@@ -102,6 +102,9 @@ int ace_lds_request(const char* kernel, int m, size_t* bytes) {
     else if (k == "nms") *bytes = nms_lds_bytes(m);
     else if (k == "hetrd") *bytes = hetrd_request_bytes(m, 0);
     else if (k == "hetrd_blk") *bytes = hetrd_request_bytes(m, 1);
+    else if (k == "he2hb") *bytes = heev2_request_bytes(m, 0);
+    else if (k == "hb2st") *bytes = heev2_request_bytes(m, 1);
+    else if (k == "bt2") *bytes = heev2_request_bytes(m, 2);
     else return fail(ACE_ERR_ARG, "unknown kernel '%s'", kernel);
     return ACE_OK;
 }

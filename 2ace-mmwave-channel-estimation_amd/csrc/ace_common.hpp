@@ -274,6 +274,7 @@ bool lds_ok(const void* kernel, size_t need);
 bool lds_ok_budget(size_t budget, size_t need);
 size_t msr_request_bytes();                  // dynamic LDS of msr_kernel
 size_t hetrd_request_bytes(int d, int blk);  // ... of hetrd_kernel (blk = 0) / hetrd_blk_kernel (blk = 1)
+size_t heev2_request_bytes(int d, int which);   // ... of he2hb_kernel (0), hb2st_kernel (1), bt2_kernel (2)
 
 // ------------------------------------------------------------------ launchers
 // GEMM (MFMA f64) with a shared complex LHS over a batch of realisation vectors:

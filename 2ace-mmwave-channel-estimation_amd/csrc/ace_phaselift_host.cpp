@@ -153,11 +153,12 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
         launch_zgemm(0, false, m, d, batch * d, w.RT, d, 0, X, d, 0, w.T, nullptr, m, 0, 1, st);
         launch_pl_diagform(d, m, batch, a.R, w.T, out, a.act, st);
     };
-    // the prox's panel-blocked tridiagonalisation (hetrd_blk_kernel; r05: 53.8 -> 60.4 rec/s at config 4,
-    // identical iterations to the unblocked hetrd_kernel); ACE_HETRD_BLK=0 for the unblocked one (A/B),
-    // read once per solve
+    // the prox's reduction (launch_heev's path): the two-stage one (ace_heev2.hip, r06) where it applies, else the
+    // panel-blocked one-stage hetrd_blk_kernel; ACE_HETRD_BLK=0 / 1 / 2 selects the unblocked / blocked one-stage /
+    // two-stage reduction (A/B and the GPU tests that pin the paths against each other), read once per solve
     const char* hb = getenv("ACE_HETRD_BLK");
-    const int blk = !(hb && hb[0] == '0');
+    const int path = hb && hb[0] == '0' ? 0 : (hb && hb[0] == '1' ? 1 : 2);
+    const int blk = path == 0 ? 0 : 1;   // (the final top-1 eig: one-stage)
     int h[8];
     for (int outer = 0; outer < cfg->maxIts + 1; ++outer) {
         launch_pl_outer_begin(a, st);
@@ -184,7 +185,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             {
                 ProfScope ps(ACE_K_ZSTEP, st, 17.3 * dd3 * act);   // prox_trace: eig of z_old - step g_y, shrink
                 launch_pl_prox_in(a, st);
-                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st, blk));
+                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st, path));
                 launch_pl_assemble(a, st);
             }
             {
@@ -261,6 +262,45 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
             (iters && (e = hipMemcpy(iters, di, 4 * (size_t)batch, hipMemcpyDeviceToHost))) ||
             (status && (e = hipMemcpy(status, dst, 4 * (size_t)batch, hipMemcpyDeviceToHost))))
             rc = fail(ACE_ERR_HIP, "phaselift: %s", hipGetErrorString(e));
+    }
+    const std::string keep = g_err;
+    cleanup();
+    g_err = keep;
+    return rc;
+}
+
+int ace_prox_eig_host(int batch, int d, int path, const double* A, const double* tau, double* lam, double* V,
+                      int32_t* k) {
+    g_err.clear();
+    if (batch < 1 || d < 2 || d > 1600 || !A || !tau || !lam || !V || !k) return fail(ACE_ERR_ARG, "bad ace_prox_eig_host arguments");
+    const HeevLayout hl = heev_layout(d, d);
+    const size_t dd = 16 * (size_t)d * d, sb = heev_scratch_bytes(d, d, batch);
+    void *ds = nullptr, *dt = nullptr, *dv = nullptr;
+    auto cleanup = [&]() {
+        for (void* q : {ds, dt, dv}) (void)hipFree(q);
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&ds, sb)) || (e = hipMalloc(&dt, 8 * (size_t)batch)) || (e = hipMalloc(&dv, dd * batch))) {
+        cleanup();
+        return fail(ACE_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
+    }
+    double* sc = (double*)ds;
+    int rc = ACE_OK;
+    for (int b = 0; b < batch && !rc; ++b)
+        if ((e = hipMemcpy(sc + (size_t)b * hl.stride + hl.C, A + 2 * (size_t)b * d * d, dd, hipMemcpyHostToDevice)))
+            rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
+    if (!rc && (e = hipMemcpy(dt, tau, 8 * (size_t)batch, hipMemcpyHostToDevice)))
+        rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
+    if (!rc) rc = launch_heev(d, d, batch, (const double*)dt, sc, (double*)dv, nullptr, nullptr, nullptr, path);
+    if (!rc) rc = launch_check("prox eig", __FILE__, __LINE__);
+    if (!rc && (e = hipDeviceSynchronize())) rc = fail(ACE_ERR_HIP, "prox eig: %s", hipGetErrorString(e));
+    if (!rc && (e = hipMemcpy(V, dv, dd * batch, hipMemcpyDeviceToHost))) rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
+    for (int b = 0; b < batch && !rc; ++b) {
+        double misc = 0.0;
+        if ((e = hipMemcpy(&misc, sc + (size_t)b * hl.stride + hl.misc, 8, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(lam + (size_t)b * d, sc + (size_t)b * hl.stride + hl.lam, 8 * (size_t)d, hipMemcpyDeviceToHost)))
+            rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
+        k[b] = (int32_t)misc;
     }
     const std::string keep = g_err;
     cleanup();

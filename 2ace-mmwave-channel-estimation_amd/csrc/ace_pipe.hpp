@@ -68,12 +68,23 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
 // eigenvector q as row q; the scratch's `misc` slot holds {k_b, sum(lam - tau)}, `lam` the
 // eigenvalues.  The matrix is destroyed; realisations with active[b] == 0 are skipped.
 struct HeevLayout {
-    long long stride, C, misc, lam;
+    long long stride, C, misc, lam, dd, ee, z;
 };
 HeevLayout heev_layout(int d, int kmax);
 size_t heev_scratch_bytes(int d, int kmax, int batch);
-// blk = 1: the panel-blocked reduction (hetrd_blk_kernel) instead of hetrd_kernel
+// path: 0 the unblocked one-stage reduction (hetrd_kernel), 1 the panel-blocked one (hetrd_blk_kernel), 2 the
+// two-stage reduction (ace_heev2.hip: dense -> band on the f64 matrix cores, band -> tridiagonal by bulge
+// chasing) where heev2_eligible, else 1
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st, int blk = 0);
+                const int* active, hipStream_t st, int path = 0);
+// the tridiagonal eigenpairs of the reduction's (dd, ee) into z / lam / misc (trieig_kernel, ace_spectral.hip)
+void launch_trieig(int d, int kmax, int batch, const double* tau, double* scratch, int* status, const int* active,
+                   hipStream_t st);
+
+// ---- two-stage prox eigensolver (ace_heev2.hip): all eigenpairs above tau (kmax = d), 32 <= d <= 256
+bool heev2_eligible(int d, int kmax);
+size_t heev2_extra_bytes(int d, int batch);   // beyond the one-stage layout's batch * stride
+int launch_heev2(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
+                 const int* active, hipStream_t st);
 
 }  // namespace ace

@@ -1259,16 +1259,25 @@ __global__ __launch_bounds__(256) void wy_kmax_kernel(int batch, const double* s
 // ---- thresholded / top-k Hermitian eigen (PhaseLift prox_trace and its final eig): see ace_pipe.hpp
 HeevLayout heev_layout(int d, int kmax) {
     const SpecLayout lay(d, kmax);
-    return HeevLayout{lay.stride, lay.C, lay.misc, lay.lam};
+    return HeevLayout{lay.stride, lay.C, lay.misc, lay.lam, lay.dd, lay.ee, lay.z};
 }
 size_t heev_scratch_bytes(int d, int kmax, int batch) {
-    size_t b = sizeof(double) * (size_t)SpecLayout(d, kmax).stride * batch;
-    if (wy_path(d, kmax)) b += sizeof(double) * (size_t)WyLayout(d, kmax).stride * batch + 256;
-    return b;
+    size_t b = sizeof(double) * (size_t)SpecLayout(d, kmax).stride * batch, x = 0;
+    if (wy_path(d, kmax)) x = sizeof(double) * (size_t)WyLayout(d, kmax).stride * batch + 256;
+    if (heev2_eligible(d, kmax)) x = std::max(x, heev2_extra_bytes(d, batch));
+    return b + x;
+}
+
+void launch_trieig(int d, int kmax, int batch, const double* tau, double* scratch, int* status, const int* active,
+                   hipStream_t st) {
+    const SpecLayout lay(d, kmax);
+    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), (size_t)d * 24, st, d, tau, scratch, lay, status, 0, active);
 }
 
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st, int blk) {
+                const int* active, hipStream_t st, int path) {
+    if (path == 2 && heev2_eligible(d, kmax)) return launch_heev2(d, kmax, batch, tau, scratch, V, status, active, st);
+    int blk = path != 0;
     const SpecLayout lay(d, kmax);
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;

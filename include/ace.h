@@ -231,6 +231,13 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
                               void* workspace, size_t workspace_bytes, void* stream);
 int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
                              const double* b, double* sig, int32_t* iters, uint32_t* status);
+/* The prox's eigensolver alone (prox_trace.m:88-92: all eigenpairs of a Hermitian d x d matrix above tau),
+ * for parity tests of its paths: A [batch][d][d] c128 (HOST, Hermitian; the lower triangle is read), tau [batch];
+ * lam [batch][d] (descending; entries >= k[b] undefined), V [batch][d][d] c128 (eigenvector q as row q),
+ * k [batch].  path: 0 unblocked one-stage, 1 blocked one-stage, 2 two-stage (where it applies, else 1).
+ * Synchronous; allocates its own device memory. */
+int ace_prox_eig_host(int batch, int d, int path, const double* A, const double* tau, double* lam, double* V,
+                      int32_t* k);
 
 /* ---- driver-level boundary (MATLAB Engine calls of main/main.py:308, :427-437) ------------
  *   [H_amp,H_angle] = channel_recovery_ADMM_v2_simulation_<A2only|A2nuclear|multiresolution|phaselift>(

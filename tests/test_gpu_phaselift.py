@@ -119,22 +119,24 @@ def test_phaselift_config4_batch512_invariance(gpu):
 
 
 
-def test_phaselift_blocked_tridiagonalisation(gpu, monkeypatch):
-    """The prox eig's blocked Householder reduction (hetrd_blk_kernel, panels of 8 columns, zlatrd;
-    ACE_HETRD_BLK=1) against the unblocked one at config 4's geometry: the same iterations and
-    solutions within 1e-9 at 60 TFOCS iterations (the oracle's own stable horizon), and the blocked
-    path against the oracle (test_phaselift_config4_geometry holds the default path to 1e-8)."""
+def test_phaselift_reduction_paths(gpu, monkeypatch):
+    """The prox eig's reductions against each other at config 4's geometry: the unblocked and panel-blocked
+    one-stage Householder reductions (hetrd_kernel, hetrd_blk_kernel; ACE_HETRD_BLK=0 / 1) and the two-stage
+    one (ace_heev2.hip, the default; ACE_HETRD_BLK=2): the same iterations and solutions within 1e-9 at 60 TFOCS
+    iterations (the oracle's own stable horizon), and each against the oracle (1e-8)."""
     from ace_amd import phaselift_host
     Phi, b = _problem(19, 32, 256, 4)
-    monkeypatch.setenv("ACE_HETRD_BLK", "0")
-    unb = phaselift_host(Phi, b, maxIts=60)
-    monkeypatch.setenv("ACE_HETRD_BLK", "1")
-    blk = phaselift_host(Phi, b, maxIts=60)
-    assert np.array_equal(blk.iters, unb.iters)
-    for r in range(4):
-        assert O.phase_aligned_rel_err(blk.sig[r], unb.sig[r]) <= 1e-9, r
+    res = {}
+    for path in ("0", "1", "2"):
+        monkeypatch.setenv("ACE_HETRD_BLK", path)
+        res[path] = phaselift_host(Phi, b, maxIts=60)
+    for path in ("1", "2"):
+        assert np.array_equal(res[path].iters, res["0"].iters)
+        for r in range(4):
+            assert O.phase_aligned_rel_err(res[path].sig[r], res["0"].sig[r]) <= 1e-9, (path, r)
     sig, _ = T.my_phaselift_reduced(b[0], Phi, maxIts=60)
-    assert O.phase_aligned_rel_err(blk.sig[0], sig) <= 1e-8
+    for path in ("0", "1", "2"):
+        assert O.phase_aligned_rel_err(res[path].sig[0], sig) <= 1e-8, path
 
 
 def test_phaselift_order_512_takes_the_unblocked_fallback(gpu):

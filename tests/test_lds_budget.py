@@ -40,6 +40,10 @@ CASES = [
     ("hetrd", "ace_spectral.hip", [r"12hetrd_kernel"], [256, 1024]),
     ("hetrd_blk", "ace_spectral.hip", [r"16hetrd_blk_kernelILi4E", r"16hetrd_blk_kernelILi2E"],
      [128, 243, 256]),   # (the prox order d = m, §4; the spectral order m_t = 243; panels of 4 / 2)
+    # the two-stage prox eigensolver (r06): every order it takes (32 <= d <= 256)
+    ("he2hb", "ace_heev2.hip", [r"12he2hb_kernel"], [32, 40, 121, 200, 256]),
+    ("hb2st", "ace_heev2.hip", [r"12hb2st_kernel"], [32, 40, 121, 200, 256]),
+    ("bt2", "ace_heev2.hip", [r"10bt2_kernel"], [32, 40, 121, 200, 256]),
 ]
 
 _REMARK = re.compile(r"remark: Function Name: (\S+)|remark:\s+LDS Size \[bytes/block\]: (\d+)")

@@ -40,6 +40,9 @@ LIB.ace_phaselift_solve_batch.restype = C.c_int
 LIB.ace_phaselift_solve_host.argtypes = [_cfgp, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]
 LIB.ace_phaselift_solve_host.restype = C.c_int
+LIB.ace_phaselift_solve_host_x.argtypes = [_cfgp, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp,
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_uint32), _dp]
+LIB.ace_phaselift_solve_host_x.restype = C.c_int
 
 
 LIB.ace_prox_eig_host.argtypes = [C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.POINTER(C.c_int32)]
@@ -48,7 +51,8 @@ LIB.ace_prox_eig_host.restype = C.c_int
 
 def prox_eig_host(A, tau, path=2):
     """The prox's eigensolver on host arrays (TFOCS/prox_trace.m:88-92): every eigenpair of the Hermitian A[b]
-    above tau[b], descending.  path 0 / 1 / 2: unblocked one-stage / blocked one-stage / two-stage reduction.
+    above tau[b], descending.  path 0 / 1 / 2: unblocked one-stage / blocked one-stage / two-stage reduction; + 4:
+    the smaller side of tau (k[b] < 0: V holds the -k[b] eigenpairs at or below tau, ascending).
     Returns (lam [batch][d], V [batch][d][d] with eigenvector q as row q, k [batch])."""
     A = np.ascontiguousarray(np.asarray(A, dtype=np.complex128).reshape((-1,) + np.shape(A)[-2:]))
     batch, d = A.shape[0], A.shape[1]
@@ -78,10 +82,13 @@ class PhaseLiftResult:
     sig: object      # [batch][n] complex128
     iters: object    # [batch] int32 (TFOCS iterations)
     status: object   # [batch] uint32 (ACE_ST_CONVERGED: step tolerance reached before maxIts)
+    X: object = None  # [batch][d][d] complex128: the final TFOCS iterate, reduced coordinates (with_x=True)
 
 
-def phaselift_host(Phi, b, **kw) -> PhaseLiftResult:
-    """Batch of MyPhaseLift solves on host arrays: Phi [m][n] (shared), b [batch][m]."""
+def phaselift_host(Phi, b, with_x=False, **kw) -> PhaseLiftResult:
+    """Batch of MyPhaseLift solves on host arrays: Phi [m][n] (shared), b [batch][m].  with_x: also return
+    solver_TraceLS's iterate (MyPhaseLift.m:98 recoveredMat) in the coordinates of range(Phi^H)
+    (ace_phaselift_solve_host_x; recoveredMat = Q X Q^H, Phi^H = Q R, R = chol(Phi Phi^H))."""
     Phi = np.ascontiguousarray(Phi, dtype=np.complex128)
     b = np.ascontiguousarray(np.atleast_2d(np.asarray(b, dtype=np.float64)))
     m, n = Phi.shape
@@ -92,11 +99,16 @@ def phaselift_host(Phi, b, **kw) -> PhaseLiftResult:
     sig = np.empty((batch, n), np.complex128)
     it = np.empty(batch, np.int32)
     stt = np.empty(batch, np.uint32)
-    check(LIB.ace_phaselift_solve_host(C.byref(cfg), batch, m, n, Phi.view(np.float64).ctypes.data_as(_dp),
-                                       b.ctypes.data_as(_dp), sig.view(np.float64).ctypes.data_as(_dp),
-                                       it.ctypes.data_as(C.POINTER(C.c_int32)),
-                                       stt.ctypes.data_as(C.POINTER(C.c_uint32))))
-    return PhaseLiftResult(sig, it, stt)
+    args = (C.byref(cfg), batch, m, n, Phi.view(np.float64).ctypes.data_as(_dp), b.ctypes.data_as(_dp),
+            sig.view(np.float64).ctypes.data_as(_dp), it.ctypes.data_as(C.POINTER(C.c_int32)),
+            stt.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if not with_x:
+        check(LIB.ace_phaselift_solve_host(*args))
+        return PhaseLiftResult(sig, it, stt)
+    d = min(m, n)
+    X = np.empty((batch, d, d), np.complex128)
+    check(LIB.ace_phaselift_solve_host_x(*args, X.view(np.float64).ctypes.data_as(_dp)))
+    return PhaseLiftResult(sig, it, stt, X)
 
 
 def MyPhaseLift(measurements, measurementMat, **kw):

@@ -36,7 +36,9 @@ namespace ace {
 namespace {
 
 constexpr int H2_MAXD = 256;
-constexpr int S1_THREADS = 512, S1_NW = S1_THREADS / 64;
+// stage 1: 4 waves per matrix, two matrices per CU (LDS 77 KB, <= 256 VGPRs each): one matrix's serial panel QR
+// overlaps the other's MFMA phases; wave w owns the trailing matrix's block rows w + 4 h (h < S1_NH)
+constexpr int S1_THREADS = 256, S1_NW = S1_THREADS / 64, S1_NH = (H2_MAXD / 16 + S1_NW - 1) / S1_NW;
 constexpr int S2_THREADS = 512, S2_NW = S2_THREADS / 64;
 // super-steps between consecutive sweeps: step j of sweep i touches rows [s_j, s_j + 16) x columns [s_j - 16, s_j + 16)
 // (s_j = i + 1 + 16 j); step j - 2 of sweep i + 1 touches rows [s_j - 31, s_j - 15), disjoint from it, and needs only
@@ -80,6 +82,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// a work-group barrier that orders LDS only (an MMRA-restricted fence: waits for the LDS operations, not for the
+// wave's global stores, which no other wave of the kernel reads)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // LAPACK zlarfg from (alpha, ||x(2:n)||^2): H^H (alpha; x) = (beta; 0), H = I - tau v v^H, v = (1; x * scal)
@@ -137,119 +146,157 @@ __device__ __forceinline__ d2 quad_sum(d2 v) {   // over the 4 lanes of a quad (
 
 // ---------------------------------------------------------------- stage 1: dense -> band (width 16)
 // Per panel p (columns 16 p .., trailing matrix A22 from row / column r0 = 16 p + 16, tt tiles of 16):
-//   X = A22 V T    all waves; wave w owns block rows w, w + 8 (row tiles J <= I of A22 and the conjugate transposes
+//   QR             zgeqr2 of the panel below the band block by all waves, one panel row per thread in registers
+//                  (the column loop unrolled; per column two work-group barriers: the norm, the 15 dot products),
+//                  then V (unit diagonal) to global scratch, the Gram V^H V on the matrix cores and T (zlarft)
+//   X = A22 V T    all waves; wave w owns block rows w + 4 h (row tiles J <= I of A22 and the conjugate transposes
 //                  of the column tiles J > I; the diagonal tile made Hermitian), the next tile's operands loaded
 //                  while the current one multiplies
 //   W = X - V (T^H (V^H X)) / 2
-//   A22 -= V W^H + W V^H on the lower tiles: first block column 0 (the next panel), then, while wave 0 factors the
-//                  next panel (look-ahead: zgeqr2 with the panel in LDS and wave-level reductions only, then the Gram
-//                  V^H V and zlarft), waves 1..7 update the rest
-// V lives in a double-buffered global scratch (written by the factoring wave, read by all), W in global scratch.
-constexpr int PN_MAX = H2_MAXD - 16;   // rows of a panel below its band block
-constexpr int PNS = 17;                // LDS row stride of the panel (consecutive rows on distinct banks)
+//   A22 -= V W^H + W V^H on the lower tiles
+// Two matrices per CU (LDS 46 KB, <= 256 VGPRs per work-group): one's barrier-bound QR overlaps the other's
+// matrix-core phases.
+constexpr int TBS = 9;   // LDS row stride of a wave's transposed partial sums (8 columns)
 
-// zgeqr2 of the panel A[r0 .. dp)[k .. k + 16) by one wave (the panel in LDS pn [L][PNS]), then V (unit diagonal,
-// zeros above) into Vg, the panel (R, beta, reflectors) back into C, the Gram V^H V on the matrix cores and T (zlarft)
-// into sT and T1
-__device__ void panel_qr_wave(int d, int k, int r0, int dp, d2* C, d2* pn, d2* Vg, d2* T1p, d2* sT, d2* sG, d2* s_tau,
-                              d2* tb, d2* tw) {
-    const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
-    const int L = dp - r0, tt = L >> 4;
-    for (int e = lane; e < L * 16; e += 64) {
-        const int rr = e >> 4, c = e & 15, r = r0 + rr, cc = k + c;
-        pn[rr * PNS + c] = (r < d && cc < d) ? C[(long long)r * d + cc] : czero();
-    }
-    wave_sync();
-    // lane rows rr = lane + 64 m (m < 4), all 16 columns; the 16 column dot products w_c are summed over the lanes by a
-    // transposition through LDS (lane (part, c) sums 16 lanes' partials of column c, two shuffles add the 4 parts),
-    // not by 30 wave-wide reductions
-    for (int j = 0; j < 16; ++j) {
-        double s = 0.0;
+struct QrLds {
+    d2 tb[S1_NW][64 * TBS];   // per wave: the column dot products' partials, transposed (aliased by the X / M slots)
+    d2 wpart[S1_NW][16];      // per wave: its sums of the dot products
+    d2 twv[S1_NW][16];        // per wave: its copy of conj(tau) w
+    d2 sG[256], s_tau[16], s_alpha;
+    double red[S1_NW];
+};
+static_assert(64 * TBS >= 256, "a wave's X / M slot must fit its tb");
+
+// zgeqr2 of the panel A[r0 .. dp)[k .. k + 16) (thread t holds row r0 + t), V (unit diagonal, zeros above) into Vg,
+// the panel (R, beta, reflectors) back into C, T (zlarft from the Gram) into sT and T1p.  Ends with a barrier.
+__device__ __forceinline__ void panel_qr(int d, int k, int r0, int dp, d2* C, d2* Vg, d2* T1p, d2* sT, QrLds& q) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, lr = lane >> 4, lc = lane & 15;
+    const int L = dp - r0, tt = L >> 4, rr = t, r = r0 + rr;
+    d2 P[16];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int rr = lane + 64 * m;
-            if (rr < L && rr > j) s += cabs2(pn[rr * PNS + j]);
-        }
-        s = wave_sum_dpp(s);
-        const Refl R = zlarfg_dev(pn[j * PNS + j], s);
-        d2 v[4];
+    for (int c = 0; c < 16; ++c) P[c] = (rr < L && r < d && k + c < d) ? C[(long long)r * d + k + c] : czero();
+    d2* tbw = q.tb[w];
+    // (one call per column with j a compile-time constant: the register array P is indexed by constants only)
+    auto col_step = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        double s = wave_sum_dpp(rr > j ? cabs2(P[j]) : 0.0);   // (rows >= L hold zeros)
+        if (lane == 0) q.red[w] = s;
+        if (t == j) q.s_alpha = P[j];
+        lds_barrier();
+        s = 0.0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int rr = lane + 64 * m;
-            v[m] = (rr < L && rr > j) ? cmul(pn[rr * PNS + j], R.scal) : make_double2(rr == j ? 1.0 : 0.0, 0.0);
+        for (int ww = 0; ww < S1_NW; ++ww) s += q.red[ww];
+        const Refl R = zlarfg_dev(q.s_alpha, s);
+        const d2 v = rr > j ? cmul(P[j], R.scal) : make_double2(rr == j ? 1.0 : 0.0, 0.0);
+        // w_c = v^H P[.][c] (c > j): the wave's partials transposed through LDS in halves of 8 columns (lane
+        // (part, c8) adds 8 lanes' partials of column c8, three shuffles the 8 parts), then the waves' sums
+        if (j < 15) {
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                if (8 * hf + 7 <= j) continue;
+#pragma unroll
+                for (int c8 = 0; c8 < 8; ++c8) {
+                    const int c = 8 * hf + c8;
+                    tbw[lane * TBS + c8] = c > j ? cmulc(v, P[c]) : czero();
+                }
+                wave_sync();
+                const int part = lane >> 3, c8 = lane & 7;
+                d2 a = czero();
+#pragma unroll
+                for (int l = 0; l < 8; ++l) a = cadd(a, tbw[(8 * part + l) * TBS + c8]);
+#pragma unroll
+                for (int o = 8; o < 64; o <<= 1) {
+                    a.x += __shfl_xor(a.x, o, 64);
+                    a.y += __shfl_xor(a.y, o, 64);
+                }
+                if (part == 0) q.wpart[w][8 * hf + c8] = a;
+                wave_sync();
+            }
+            lds_barrier();
+            if (lane < 16) {   // (lane c of every wave: conj(tau) w_c into the wave's copy)
+                d2 a = czero();
+#pragma unroll
+                for (int ww = 0; ww < S1_NW; ++ww) a = cadd(a, q.wpart[ww][lane]);
+                q.twv[w][lane] = cmul(cconj(R.tau), a);
+            }
+            wave_sync();
+#pragma unroll
+            for (int c = j + 1; c < 16; ++c) P[c] = csub(P[c], cmul(v, q.twv[w][c]));   // (I - conj(tau) v v^H)
         }
+        P[j] = rr == j ? make_double2(R.beta, 0.0) : (rr > j ? v : P[j]);   // rows < j: R
+        if (t == 0) q.s_tau[j] = R.tau;
+    };
+    using std::integral_constant;
+    col_step(integral_constant<int, 0>{});
+    col_step(integral_constant<int, 1>{});
+    col_step(integral_constant<int, 2>{});
+    col_step(integral_constant<int, 3>{});
+    col_step(integral_constant<int, 4>{});
+    col_step(integral_constant<int, 5>{});
+    col_step(integral_constant<int, 6>{});
+    col_step(integral_constant<int, 7>{});
+    col_step(integral_constant<int, 8>{});
+    col_step(integral_constant<int, 9>{});
+    col_step(integral_constant<int, 10>{});
+    col_step(integral_constant<int, 11>{});
+    col_step(integral_constant<int, 12>{});
+    col_step(integral_constant<int, 13>{});
+    col_step(integral_constant<int, 14>{});
+    col_step(integral_constant<int, 15>{});
+    // the panel back into C, V into Vg (rows < L)
+    if (rr < L) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-            d2 a = czero();
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int rr = lane + 64 * m;
-                if (c > j && rr < L && rr >= j) a = cadd(a, cmulc(v[m], pn[rr * PNS + c]));
-            }
-            tb[lane * 17 + c] = a;
+            if (r < d && k + c < d) C[(long long)r * d + k + c] = P[c];
+            Vg[rr * 16 + c] = rr > c ? P[c] : make_double2(rr == c ? 1.0 : 0.0, 0.0);
         }
-        wave_sync();
-        {
-            const int part = lane >> 4, cc = lane & 15;
-            d2 a = czero();
-#pragma unroll
-            for (int l = 0; l < 16; ++l) a = cadd(a, tb[(16 * part + l) * 17 + cc]);
-            a.x += __shfl_xor(a.x, 16, 64);
-            a.y += __shfl_xor(a.y, 16, 64);
-            a.x += __shfl_xor(a.x, 32, 64);
-            a.y += __shfl_xor(a.y, 32, 64);
-            if (part == 0) tw[cc] = cmul(cconj(R.tau), a);   // conj(tau) w_c
-        }
-        wave_sync();
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int rr = lane + 64 * m;
-            if (rr >= L || rr < j) continue;
-#pragma unroll
-            for (int c = 0; c < 16; ++c)
-                if (c > j) pn[rr * PNS + c] = csub(pn[rr * PNS + c], cmul(v[m], tw[c]));
-            pn[rr * PNS + j] = rr == j ? make_double2(R.beta, 0.0) : v[m];
-        }
-        if (lane == 0) s_tau[j] = R.tau;
-        wave_sync();
     }
-    // V, the panel, the Gram (rows of tile I: lane (lr + 4 q, lc))
+    __syncthreads();   // (Vg: global stores read by the other waves)
+    // the Gram V^H V: wave w's tiles I = w (mod S1_NW), partials summed through LDS (rows of tile I: lane (lr + 4 q, lc))
     Cacc G = cacc0();
-    for (int I = 0; I < tt; ++I) {
+    for (int I = w; I < tt; I += S1_NW) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = 16 * I + lr + 4 * q;
-            const d2 pv = pn[rr * PNS + lc];
-            const d2 vv = rr > lc ? pv : make_double2(rr == lc ? 1.0 : 0.0, 0.0);
-            Vg[rr * 16 + lc] = vv;
-            if (r0 + rr < d && k + lc < d) C[(long long)(r0 + rr) * d + k + lc] = pv;
+        for (int qq = 0; qq < 4; ++qq) {
+            const d2 vv = Vg[(16 * I + lr + 4 * qq) * 16 + lc];
             cmma(G, cconj(vv), vv);
         }
     }
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) sG[(lr + 4 * j4) * 16 + lc] = cget(G, j4);
-    wave_sync();
-    if (lane < 16) {   // zlarft (forward, columnwise): lane a computes row a of T
-        const int a = lane;
-        d2 Tr[16];
+    for (int j4 = 0; j4 < 4; ++j4) tbw[(lr + 4 * j4) * 16 + lc] = cget(G, j4);
+    lds_barrier();
+    if (w == 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const d2 ti = s_tau[i];
-            d2 acc = czero();
+        for (int j4 = 0; j4 < 4; ++j4) {
+            const int e = (lr + 4 * j4) * 16 + lc;
+            d2 a = czero();
 #pragma unroll
-            for (int c = 0; c < 16; ++c)
-                if (c < i && c >= a) acc = cadd(acc, cmul(Tr[c], cneg(cmul(ti, sG[c * 16 + i]))));
-            Tr[i] = i == a ? ti : (i > a ? acc : czero());
+            for (int ww = 0; ww < S1_NW; ++ww) a = cadd(a, q.tb[ww][e]);
+            q.sG[e] = a;
         }
+        wave_sync();
+        if (lane < 16) {   // zlarft (forward, columnwise): lane a computes row a of T
+            const int a = lane;
+            d2 Tr[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            sT[a * 16 + i] = Tr[i];
-            T1p[a * 16 + i] = Tr[i];
+            for (int i = 0; i < 16; ++i) {
+                const d2 ti = q.s_tau[i];
+                d2 acc = czero();
+#pragma unroll
+                for (int c = 0; c < 16; ++c)
+                    if (c < i && c >= a) acc = cadd(acc, cmul(Tr[c], cneg(cmul(ti, q.sG[c * 16 + i]))));
+                Tr[i] = i == a ? ti : (i > a ? acc : czero());
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sT[a * 16 + i] = Tr[i];
+                T1p[a * 16 + i] = Tr[i];
+            }
         }
     }
+    lds_barrier();
 }
 
-__global__ __launch_bounds__(S1_THREADS) void he2hb_kernel(int d, double* scratch, HeevLayout hl, double* xs, H2Lay xl,
+__global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2))) void he2hb_kernel(int d, double* scratch, HeevLayout hl, double* xs, H2Lay xl,
                                                            const int* active) {
     const int b = blockIdx.x;
     if (active && !active[b]) return;
@@ -260,16 +307,15 @@ __global__ __launch_bounds__(S1_THREADS) void he2hb_kernel(int d, double* scratc
     d2* Wg = reinterpret_cast<d2*>(xb + xl.W);
     d2* Vg2 = reinterpret_cast<d2*>(xb + xl.V);
     const int dp = xl.dp;
-    __shared__ d2 pn[PN_MAX * PNS];
-    __shared__ d2 sl[S1_NW][256];
-    __shared__ d2 sT[256], sG[256], s_tau[16], tb[64 * 17], tw[16];
-    d2* slw = sl[w];
+    __shared__ QrLds q;
+    __shared__ d2 sT[256];
+    d2* slw = q.tb[w];   // the wave's X / M slot (its QR partials' space)
     auto ldC = [&](int r, int c) -> d2 { return (r < d && c < d) ? C[(long long)r * d + c] : czero(); };
     auto stC = [&](int r, int c, d2 v) {
         if (r < d && c < d) C[(long long)r * d + c] = v;
     };
 #ifdef ACE_H2_STAMPS
-    unsigned long long st_ph[5] = {0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_ph[4] = {0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
     auto stamp = [&](int ph) {
         const unsigned long long n = __builtin_amdgcn_s_memrealtime();
         st_ph[ph] += n - st_t;
@@ -278,17 +324,15 @@ __global__ __launch_bounds__(S1_THREADS) void he2hb_kernel(int d, double* scratc
 #else
     auto stamp = [](int) {};
 #endif
-    if (xl.np > 0 && w == 0) panel_qr_wave(d, 0, 16, dp, C, pn, Vg2, T1, sT, sG, s_tau, tb, tw);
-    __syncthreads();
-    stamp(0);
     for (int p = 0; p < xl.np; ++p) {
         const int r0 = 16 * p + 16, tt = (dp - r0) >> 4;
-        const d2* Vg = Vg2 + (p & 1) * dp * 16;
+        const d2* Vg = Vg2;
+        panel_qr(d, 16 * p, r0, dp, C, Vg2, T1 + p * 256, sT, q);
+        stamp(0);
         // ---- X = A22 V T for the wave's block rows I
-        Cacc X[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            X[h] = cacc0();
+        // (X goes to Wg tile by tile, W is formed in place; M = V^H X accumulates as the tiles come)
+        Cacc Mp = cacc0();
+        for (int h = 0; h < S1_NH; ++h) {
             const int I = w + S1_NW * h;
             if (I >= tt) continue;
             const int ri = r0 + 16 * I;
@@ -328,45 +372,41 @@ __global__ __launch_bounds__(S1_THREADS) void he2hb_kernel(int d, double* scratc
 #pragma unroll
             for (int s = 0; s < 4; ++s) cmma(Xh, slw[lc * 16 + 4 * s + lr], sT[(4 * s + lr) * 16 + lc]);
             wave_sync();
-            X[h] = Xh;
+#pragma unroll
+            for (int j4 = 0; j4 < 4; ++j4) Wg[(16 * I + lr + 4 * j4) * 16 + lc] = cget(Xh, j4);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) cmma(Mp, cconj(Vg[(16 * I + 4 * s + lr) * 16 + lc]), cget(Xh, s));
         }
         stamp(1);
         // ---- M = V^H X (partials per wave, summed in wave order), S = T^H M, W = X - V S / 2
-        Cacc Mp = cacc0();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int I = w + S1_NW * h;
-            if (I >= tt) continue;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) cmma(Mp, cconj(Vg[(16 * I + 4 * s + lr) * 16 + lc]), cget(X[h], s));
-        }
 #pragma unroll
         for (int j4 = 0; j4 < 4; ++j4) slw[(lr + 4 * j4) * 16 + lc] = cget(Mp, j4);
-        __syncthreads();
+        lds_barrier();
         Cacc S = cacc0();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = 4 * s + lr;
             d2 m = czero();
 #pragma unroll
-            for (int ww = 0; ww < S1_NW; ++ww) m = cadd(m, sl[ww][kk * 16 + lc]);
+            for (int ww = 0; ww < S1_NW; ++ww) m = cadd(m, q.tb[ww][kk * 16 + lc]);
             cmma(S, cconj(sT[kk * 16 + lc]), m);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < S1_NH; ++h) {
             const int I = w + S1_NW * h;
             if (I >= tt) continue;
             Cacc U = cacc0();
 #pragma unroll
             for (int s = 0; s < 4; ++s) cmma(U, Vg[(16 * I + lc) * 16 + 4 * s + lr], cget(S, s));
 #pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4)
-                Wg[(16 * I + lr + 4 * j4) * 16 + lc] = csub(cget(X[h], j4), cscale(cget(U, j4), 0.5));
+            for (int j4 = 0; j4 < 4; ++j4) {   // (the thread's own X entries)
+                d2& x = Wg[(16 * I + lr + 4 * j4) * 16 + lc];
+                x = csub(x, cscale(cget(U, j4), 0.5));
+            }
         }
         __syncthreads();
         stamp(2);
-        // ---- A22 -= V W^H + W V^H on the lower tiles: block column 0 first, then the rest while wave 0 factors
-        // the next panel (block column 0's tiles below its diagonal one)
+        // ---- A22 -= V W^H + W V^H on the lower tiles
         auto upd = [&](int I, int J) {
             const int ri = r0 + 16 * I, rj = r0 + 16 * J;
             d2 vi[4], wi[4], wj[4], vj[4];
@@ -393,30 +433,18 @@ __global__ __launch_bounds__(S1_THREADS) void he2hb_kernel(int d, double* scratc
 #pragma unroll
             for (int j4 = 0; j4 < 4; ++j4) stC(ri + lr + 4 * j4, rj + lc, cget(A, j4));
         };
-        const bool next = p + 1 < xl.np;
-        for (int I = w; I < tt; I += S1_NW) upd(I, 0);
-        __syncthreads();
-        stamp(3);
-        if (w == 0) {
-            if (next)
-                panel_qr_wave(d, r0, r0 + 16, dp, C, pn, Vg2 + ((p + 1) & 1) * dp * 16, T1 + (p + 1) * 256, sT, sG,
-                              s_tau, tb, tw);
-        } else {
-            const int nrest = tt * (tt + 1) / 2 - tt;   // tiles I >= J >= 1
-            for (int e = w - 1; e < nrest; e += S1_NW - 1) {
-                int I = 1;
-                while (I * (I + 1) / 2 <= e) ++I;   // e = I (I - 1) / 2 + (J - 1), 1 <= J <= I
-                const int J = e - I * (I - 1) / 2 + 1;
-                upd(I, J);
-            }
+        const int nt = tt * (tt + 1) / 2;   // tiles I >= J
+        for (int e = w; e < nt; e += S1_NW) {
+            int I = 0;
+            while ((I + 1) * (I + 2) / 2 <= e) ++I;   // e = I (I + 1) / 2 + J, 0 <= J <= I
+            upd(I, e - I * (I + 1) / 2);
         }
         __syncthreads();
-        stamp(4);
+        stamp(3);
     }
 #ifdef ACE_H2_STAMPS
     if (t == 0 && (b % 101) == 0)
-        printf("he2hb b %d: qr0 %llu X %llu W %llu upd0 %llu qr|upd %llu (x10ns)\n", b, st_ph[0], st_ph[1], st_ph[2],
-               st_ph[3], st_ph[4]);
+        printf("he2hb b %d: qr %llu X %llu W %llu upd %llu (x10ns)\n", b, st_ph[0], st_ph[1], st_ph[2], st_ph[3]);
 #endif
 }
 
@@ -572,7 +600,7 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                 two_sided(r0, len, tau);
             }
         }
-        __syncthreads();
+        lds_barrier();   // (the Q2 slots are global stores read only by bt2q2_kernel)
     }
 #ifdef ACE_H2_STAMPS
     if (t == 0 && (b % 101) == 0) printf("hb2st b %d: %d super-steps\n", b, nss);
@@ -640,7 +668,7 @@ __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int 
     fetch(0);
     stage(0);
     if (nblk > 1) fetch(1);
-    __syncthreads();
+    lds_barrier();
     const bool has_vec = q0 + qv < k;
     const double* zv = base + hl.z + (long long)(q0 + qv) * d;
     d2* vo = reinterpret_cast<d2*>(Vout) + ((long long)b * kmax + q0 + qv) * d;
@@ -707,10 +735,10 @@ __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int 
             __builtin_amdgcn_sched_barrier(0);   // (no hoisting of later steps' LDS reads: they would not fit)
         }
         if (blk + 1 < nblk) {
-            __syncthreads();   // (every wave is done with the buffer the next-but-one block goes to)
+            lds_barrier();   // (every wave is done with the buffer the next-but-one block goes to)
             stage((blk + 1) & 1);
             if (blk + 2 < nblk) fetch(blk + 2);
-            __syncthreads();
+            lds_barrier();   // (LDS only: a full barrier would wait for the prefetch just issued)
         }
     };
     for (int blk = 0; blk < nblk; blk += 2) {
@@ -795,7 +823,7 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
         for (int cv = 0; cv < 2; ++cv)
 #pragma unroll
             for (int j4 = 0; j4 < 4; ++j4) sl[w][cv][(lr + 4 * j4) * 16 + lc] = cget(W1[cv], j4);
-        __syncthreads();
+        lds_barrier();
         Cacc W2[2] = {cacc0(), cacc0()};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -823,7 +851,7 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
             }
         }
         load_v(p - 1, false, true);
-        __syncthreads();
+        lds_barrier();   // (LDS only: the next panel's operands stay in flight)
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -860,14 +888,14 @@ size_t heev2_request_bytes(int d, int which) {
 }
 
 int launch_heev2(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                 const int* active, hipStream_t st) {
+                 const int* active, hipStream_t st, int side_ok) {
     if (!heev2_eligible(d, kmax)) return fail(ACE_ERR_UNSUPPORTED, "two-stage eigensolver: d = %d not supported", d);
     const HeevLayout hl = heev_layout(d, kmax);
     const H2Lay xl = h2lay(d);
     double* xs = scratch + (((size_t)hl.stride * batch + 31) & ~(size_t)31);
     hipLaunchKernelGGL(he2hb_kernel, dim3(batch), dim3(S1_THREADS), s1_lds(xl), st, d, scratch, hl, xs, xl, active);
     hipLaunchKernelGGL(hb2st_kernel, dim3(batch), dim3(S2_THREADS), s2_lds(d), st, d, scratch, hl, xs, xl, active);
-    launch_trieig(d, kmax, batch, tau, scratch, status, active, st);
+    launch_trieig(d, kmax, batch, tau, scratch, status, active, st, side_ok);
     const int groups = (batch + 7) / 8, nc2 = (d + Q2_NV - 1) / Q2_NV, nc1 = (d + Q1_NV - 1) / Q1_NV;
     hipLaunchKernelGGL(bt2q2_kernel, dim3(groups * nc2 * 8), dim3(Q2_THREADS), 0, st, d, kmax, batch, nc2, scratch, hl,
                        xs, xl, V, active);

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(256) void pl_assemble_kernel(PlArgs a) {
     const double* base = a.scratch + (long long)b * a.hl.stride;
     const int k = (int)base[a.hl.misc];
     const double tau = a.tau[b];
+    const double sgn = base[a.hl.misc + 2] != 0.0 ? -1.0 : 1.0;   // (the complement side: s = tau - lam)
     const double* lam = base + a.hl.lam;
     const long long o = (long long)b * d * d;
     const d2* V = reinterpret_cast<const d2*>(a.V) + o;
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(256) void pl_assemble_kernel(PlArgs a) {
                 const int rr = r0 + 8 * u, i = 32 * I + rr, q = 32 * Q + cc;
                 if (i < d && q < d) {
                     const d2 v = tv[cc][rr];
-                    const double s = q < k ? lam[q] - tau : 0.0;
+                    const double s = q < k ? sgn * (lam[q] - tau) : 0.0;
                     const long long e = (long long)i * d + q;
                     VT[e] = v;
                     P[e] = cscale(v, s);
@@ -287,9 +288,16 @@ __global__ __launch_bounds__(256) void pl_take_z_kernel(PlArgs a) {
     const long long o = (long long)b * d * d;
     const d2* Zn = reinterpret_cast<const d2*>(a.Znew) + o;
     d2* z = reinterpret_cast<d2*>(a.z) + o;
+    // the prox's complement form (misc[2], trieig_kernel: more than half of the eigenvalues above tau): Zn holds
+    // sum_{lam <= tau} (tau - lam) v v^H and z = Zn + (W + W^H)/2 - tau I, W = z_old - step G as pl_prox_in built it
+    const double* mb = a.scratch + (long long)b * a.hl.stride + a.hl.misc;
+    const bool side = mb[2] != 0.0;
+    const double st = a.st[b].step, tau = a.tau[b];
+    const d2* zo = reinterpret_cast<const d2*>(a.zo) + o;
+    const d2* G = reinterpret_cast<const d2*>(a.G) + o;
     // by 32 x 32 tile pairs (I, J), (J, I) staged in LDS (as pl_prox_in_kernel): every entry read once, row-coalesced
     // (the element-wise form read Zn[j][i] down a column); the same expression per entry
-    __shared__ d2 tu[32][33], tl[32][33];
+    __shared__ d2 tu[32][33], tl[32][33], wu[32][33], wl[32][33];
     const int nt = (d + 31) / 32, cc = t & 31, r0 = t >> 5;
     for (int I = 0; I < nt; ++I)
         for (int J = I; J < nt; ++J) {
@@ -297,8 +305,16 @@ __global__ __launch_bounds__(256) void pl_take_z_kernel(PlArgs a) {
             for (int q = 0; q < 4; ++q) {
                 const int rr = r0 + 8 * q;
                 const int i1 = 32 * I + rr, j1 = 32 * J + cc, i2 = 32 * J + rr, j2 = 32 * I + cc;
-                if (i1 < d && j1 < d) tu[rr][cc] = Zn[(long long)i1 * d + j1];
-                if (i2 < d && j2 < d) tl[rr][cc] = Zn[(long long)i2 * d + j2];
+                if (i1 < d && j1 < d) {
+                    const long long e = (long long)i1 * d + j1;
+                    tu[rr][cc] = Zn[e];
+                    if (side) wu[rr][cc] = csub(zo[e], cscale(G[e], st));
+                }
+                if (i2 < d && j2 < d) {
+                    const long long e = (long long)i2 * d + j2;
+                    tl[rr][cc] = Zn[e];
+                    if (side) wl[rr][cc] = csub(zo[e], cscale(G[e], st));
+                }
             }
             __syncthreads();
 #pragma unroll
@@ -307,12 +323,22 @@ __global__ __launch_bounds__(256) void pl_take_z_kernel(PlArgs a) {
                 const int i1 = 32 * I + rr, j1 = 32 * J + cc;
                 if (i1 < d && j1 < d) {   // z[i1][j1] from u = Zn[i1][j1], l = Zn[j1][i1]
                     const d2 u = tu[rr][cc], l = tl[cc][rr];
-                    z[(long long)i1 * d + j1] = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                    d2 v = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                    if (side) {
+                        const d2 w1 = wu[rr][cc], w2 = wl[cc][rr];
+                        v = cadd(v, make_double2(0.5 * (w1.x + w2.x) - (i1 == j1 ? tau : 0.0), 0.5 * (w1.y - w2.y)));
+                    }
+                    z[(long long)i1 * d + j1] = v;
                 }
                 const int i2 = 32 * J + rr, j2 = 32 * I + cc;
                 if (I != J && i2 < d && j2 < d) {
                     const d2 u = tl[rr][cc], l = tu[cc][rr];
-                    z[(long long)i2 * d + j2] = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                    d2 v = make_double2(0.5 * (u.x + l.x), 0.5 * (u.y - l.y));
+                    if (side) {
+                        const d2 w1 = wl[rr][cc], w2 = wu[cc][rr];
+                        v = cadd(v, make_double2(0.5 * (w1.x + w2.x), 0.5 * (w1.y - w2.y)));
+                    }
+                    z[(long long)i2 * d + j2] = v;
                 }
             }
             __syncthreads();

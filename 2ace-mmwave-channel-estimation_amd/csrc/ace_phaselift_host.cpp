@@ -88,10 +88,13 @@ size_t ace_phaselift_workspace_size(const ace_phaselift_cfg* cfg, int batch, int
     return cv.off + 256;
 }
 
-int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
-                              const double* bvec, double* sig, int32_t* iters, uint32_t* status, void* workspace,
-                              size_t workspace_bytes, void* stream) {
-    g_err.clear();
+}  // extern "C"
+
+namespace {
+// ace_phaselift_solve_batch; Xout (device, may be NULL): the final TFOCS iterate [batch][d][d] (reduced coordinates)
+int solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi, const double* bvec,
+                double* sig, int32_t* iters, uint32_t* status, void* workspace, size_t workspace_bytes, void* stream,
+                double* Xout) {
     PlDims D;
     ACE_TRY(validate(cfg, batch, m, n, &D));
     if (!Phi || !bvec || !sig || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
@@ -158,6 +161,11 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
     // two-stage reduction (A/B and the GPU tests that pin the paths against each other), read once per solve
     const char* hb = getenv("ACE_HETRD_BLK");
     const int path = hb && hb[0] == '0' ? 0 : (hb && hb[0] == '1' ? 1 : 2);
+    // ACE_PROX_SIDE=1: the prox's eigenvectors from the smaller side of the threshold (trieig_kernel).  Off by
+    // default: at config 4 the pairs at or below the threshold form large near-zero clusters, and their
+    // orthogonalisation in trieig costs more than the back-transform saves (r06: 69.7 vs 81.1 rec/s)
+    const char* sd = getenv("ACE_PROX_SIDE");
+    const int side_ok = sd && sd[0] == '1';
     const int blk = path == 0 ? 0 : 1;   // (the final top-1 eig: one-stage)
     int h[8];
     for (int outer = 0; outer < cfg->maxIts + 1; ++outer) {
@@ -185,7 +193,7 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             {
                 ProfScope ps(ACE_K_ZSTEP, st, 17.3 * dd3 * act);   // prox_trace: eig of z_old - step g_y, shrink
                 launch_pl_prox_in(a, st);
-                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st, path));
+                ACE_TRY(launch_heev(d, d, batch, a.tau, a.scratch, a.V, (int*)status, a.act, st, path, side_ok));
                 launch_pl_assemble(a, st);
             }
             {
@@ -223,17 +231,18 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
             launch_zgemm(0, false, n, m, batch, w.AH, m, 0, w.wfin, m, 0, sig, nullptr, n, 0, 1, st);
         launch_pl_outputs(batch, a.st, iters, status, st);
     }
+    if (Xout) ACE_HIP(hipMemcpyAsync(Xout, a.x, 16 * (size_t)batch * d * d, hipMemcpyDeviceToDevice, st));
     ACE_LAUNCHED("PhaseLift final eigenvector");
     return ACE_OK;
 }
 
-int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
-                             const double* bvec, double* sig, int32_t* iters, uint32_t* status) {
+int solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi, const double* bvec,
+               double* sig, int32_t* iters, uint32_t* status, double* Xr) {
     g_err.clear();
     PlDims D;
     ACE_TRY(validate(cfg, batch, m, n, &D));
     const size_t nP = 16 * (size_t)m * n, nb = 8 * (size_t)batch * m, ns = 16 * (size_t)batch * n,
-                 ws = ace_phaselift_workspace_size(cfg, batch, m, n);
+                 nx = 16 * (size_t)batch * D.d * D.d, ws = ace_phaselift_workspace_size(cfg, batch, m, n);
     std::vector<void*> bufs;
     auto cleanup = [&]() {
         for (void* q : bufs) (void)hipFree(q);
@@ -244,10 +253,10 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
         if (e == hipSuccess) bufs.push_back(*q);
         return e;
     };
-    void *dP, *db, *ds, *di, *dst, *dw;
+    void *dP, *db, *ds, *di, *dst, *dw, *dx = nullptr;
     hipError_t e;
     if ((e = dalloc(nP, &dP)) || (e = dalloc(nb, &db)) || (e = dalloc(ns, &ds)) || (e = dalloc(4 * (size_t)batch, &di)) ||
-        (e = dalloc(4 * (size_t)batch, &dst)) || (e = dalloc(ws, &dw))) {
+        (e = dalloc(4 * (size_t)batch, &dst)) || (e = dalloc(ws, &dw)) || (Xr && (e = dalloc(nx, &dx)))) {
         cleanup();
         return fail(ACE_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
     }
@@ -255,18 +264,43 @@ int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int
         cleanup();
         return fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
     }
-    int rc = ace_phaselift_solve_batch(cfg, batch, m, n, (const double*)dP, (const double*)db, (double*)ds,
-                                       (int32_t*)di, (uint32_t*)dst, dw, ws, nullptr);
+    int rc = solve_batch(cfg, batch, m, n, (const double*)dP, (const double*)db, (double*)ds, (int32_t*)di,
+                         (uint32_t*)dst, dw, ws, nullptr, (double*)dx);
     if (rc == ACE_OK) {
         if ((e = hipDeviceSynchronize()) || (e = hipMemcpy(sig, ds, ns, hipMemcpyDeviceToHost)) ||
             (iters && (e = hipMemcpy(iters, di, 4 * (size_t)batch, hipMemcpyDeviceToHost))) ||
-            (status && (e = hipMemcpy(status, dst, 4 * (size_t)batch, hipMemcpyDeviceToHost))))
+            (status && (e = hipMemcpy(status, dst, 4 * (size_t)batch, hipMemcpyDeviceToHost))) ||
+            (Xr && (e = hipMemcpy(Xr, dx, nx, hipMemcpyDeviceToHost))))
             rc = fail(ACE_ERR_HIP, "phaselift: %s", hipGetErrorString(e));
     }
     const std::string keep = g_err;
     cleanup();
     g_err = keep;
     return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                              const double* bvec, double* sig, int32_t* iters, uint32_t* status, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+    g_err.clear();
+    return solve_batch(cfg, batch, m, n, Phi, bvec, sig, iters, status, workspace, workspace_bytes, stream, nullptr);
+}
+
+int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                             const double* bvec, double* sig, int32_t* iters, uint32_t* status) {
+    return solve_host(cfg, batch, m, n, Phi, bvec, sig, iters, status, nullptr);
+}
+
+int ace_phaselift_solve_host_x(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                               const double* bvec, double* sig, int32_t* iters, uint32_t* status, double* Xr) {
+    if (!Xr) {
+        g_err.clear();
+        return fail(ACE_ERR_ARG, "NULL buffer");
+    }
+    return solve_host(cfg, batch, m, n, Phi, bvec, sig, iters, status, Xr);
 }
 
 int ace_prox_eig_host(int batch, int d, int path, const double* A, const double* tau, double* lam, double* V,
@@ -291,16 +325,16 @@ int ace_prox_eig_host(int batch, int d, int path, const double* A, const double*
             rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
     if (!rc && (e = hipMemcpy(dt, tau, 8 * (size_t)batch, hipMemcpyHostToDevice)))
         rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
-    if (!rc) rc = launch_heev(d, d, batch, (const double*)dt, sc, (double*)dv, nullptr, nullptr, nullptr, path);
+    if (!rc) rc = launch_heev(d, d, batch, (const double*)dt, sc, (double*)dv, nullptr, nullptr, nullptr, path & 3, path >> 2);
     if (!rc) rc = launch_check("prox eig", __FILE__, __LINE__);
     if (!rc && (e = hipDeviceSynchronize())) rc = fail(ACE_ERR_HIP, "prox eig: %s", hipGetErrorString(e));
     if (!rc && (e = hipMemcpy(V, dv, dd * batch, hipMemcpyDeviceToHost))) rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
     for (int b = 0; b < batch && !rc; ++b) {
-        double misc = 0.0;
-        if ((e = hipMemcpy(&misc, sc + (size_t)b * hl.stride + hl.misc, 8, hipMemcpyDeviceToHost)) ||
+        double misc[3] = {0.0, 0.0, 0.0};
+        if ((e = hipMemcpy(misc, sc + (size_t)b * hl.stride + hl.misc, 24, hipMemcpyDeviceToHost)) ||
             (e = hipMemcpy(lam + (size_t)b * d, sc + (size_t)b * hl.stride + hl.lam, 8 * (size_t)d, hipMemcpyDeviceToHost)))
             rc = fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
-        k[b] = (int32_t)misc;
+        k[b] = misc[2] != 0.0 ? -(int32_t)misc[0] : (int32_t)misc[0];
     }
     const std::string keep = g_err;
     cleanup();

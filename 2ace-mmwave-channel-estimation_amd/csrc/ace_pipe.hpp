@@ -75,16 +75,18 @@ size_t heev_scratch_bytes(int d, int kmax, int batch);
 // path: 0 the unblocked one-stage reduction (hetrd_kernel), 1 the panel-blocked one (hetrd_blk_kernel), 2 the
 // two-stage reduction (ace_heev2.hip: dense -> band on the f64 matrix cores, band -> tridiagonal by bulge
 // chasing) where heev2_eligible, else 1
+// side_ok (tau given, kmax = d): the vectors of the smaller side of tau (misc[2] = 1: those at or below it, see
+// trieig_kernel); misc[1] is sum_{lam > tau} (lam - tau) either way
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st, int path = 0);
+                const int* active, hipStream_t st, int path = 0, int side_ok = 0);
 // the tridiagonal eigenpairs of the reduction's (dd, ee) into z / lam / misc (trieig_kernel, ace_spectral.hip)
 void launch_trieig(int d, int kmax, int batch, const double* tau, double* scratch, int* status, const int* active,
-                   hipStream_t st);
+                   hipStream_t st, int side_ok);
 
 // ---- two-stage prox eigensolver (ace_heev2.hip): all eigenpairs above tau (kmax = d), 32 <= d <= 256
 bool heev2_eligible(int d, int kmax);
 size_t heev2_extra_bytes(int d, int batch);   // beyond the one-stage layout's batch * stride
 int launch_heev2(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                 const int* active, hipStream_t st);
+                 const int* active, hipStream_t st, int side_ok);
 
 }  // namespace ace

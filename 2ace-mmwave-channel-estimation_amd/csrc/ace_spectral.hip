@@ -55,7 +55,7 @@ struct SpecLayout {
         z = take((long long)kmax * mt);
         lam = take(kmax);
         cl = take(kmax + 1);               // cluster starts (as doubles)
-        misc = take(8);                    // [0] k, [1] sum(lam - tau)
+        misc = take(8);                    // [0] k, [1] sum over lam > tau of (lam - tau), [2] side (trieig_kernel)
         stride = o;
     }
 };
@@ -636,10 +636,24 @@ __device__ __forceinline__ void sturm_count2(const double* d, const double* e2, 
 // that chains up to ~100 eigenvalues into one sequential cluster, while at 1e-5 the largest
 // cluster has two members.  Inverse-iteration vectors of eigenvalues separated by more than
 // kOrtol ||T|| are orthogonal to ~eps / kOrtol (2e-11) without projection.  Writes z[k][mt], lam[k], misc = {k, sum(lam - tau)}.
+// side_ok (the prox, kmax = mt): when more than half of the eigenvalues lie above tau, the vectors of the ones at
+// or below it are computed instead (ascending), misc[2] = 1: prox_trace's shrink is then
+// X = (W - tau I) + sum_{lam <= tau} (tau - lam) v v^H (the same matrix; PhaseLift's take_z adds W - tau I), and
+// misc[1] = sum_{lam > tau} (lam - tau) = (trace T - mt tau) - sum_{lam <= tau} (lam - tau).
 __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p, double* scratch, SpecLayout lay,
-                                                     int* status, int status_off, const int* active) {
+                                                     int* status, int status_off, const int* active, int side_ok) {
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (active && !active[b]) return;
+#ifdef ACE_H2_STAMPS
+    unsigned long long st_ph[4] = {0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&](int ph) {
+        const unsigned long long n = __builtin_amdgcn_s_memrealtime();
+        st_ph[ph] += n - st_t;
+        st_t = n;
+    };
+#else
+    auto stamp = [](int) {};
+#endif
     extern __shared__ double smem[];
     double* d = smem;
     double* e = smem + mt;
@@ -678,17 +692,23 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     gl -= 2.0 * tn * eps * mt;
     gu += 2.0 * tn * eps * mt;
     const double tau = tau_p ? tau_p[status_off + b] : 0.0;
+    __shared__ int s_side;
     if (t == 0) {
-        int k = lay.kmax < mt ? lay.kmax : mt;
+        int k = lay.kmax < mt ? lay.kmax : mt, side = 0;
         if (tau_p) {  // eigenvalues strictly above tau (prox_trace keeps s = lam - tau > 0)
             const int kk = mt - sturm_count(d, e, mt, tau, pivmin);
             if (kk > k && status) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
             k = kk < k ? kk : k;
+            if (side_ok && 2 * kk > mt) {
+                side = 1;
+                k = mt - kk;
+            }
         }
         s_k = k;
+        s_side = side;
     }
     __syncthreads();
-    const int k = s_k;
+    int k = s_k, side = s_side;
     double* lam = base + lay.lam;
     // one shared round first: Sturm counts at TE_GRID + 1 even points of [gl, gu] (two per thread), so that
     // every eigenvalue starts from its grid cell instead of the whole interval (log3(TE_GRID) rounds fewer)
@@ -702,55 +722,80 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     }
     if (t == 0) gcnt[0] = 0;
     __syncthreads();
-    for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue
-        const int j = mt - 1 - q;
-        double lo = gl, hi = gu;
-        {   // the first grid point with more than j eigenvalues below it (counts are monotone in x)
-            int a0 = 0, a1 = TE_GRID;
-            while (a1 - a0 > 1) {
-                const int am = (a0 + a1) >> 1;
-                if (gcnt[am] > j) a1 = am;
-                else a0 = am;
-            }
-            if (gcnt[a1] > j) {
-                lo = gl + a0 * gh;
-                if (a1 < TE_GRID) hi = gl + a1 * gh;
-            }
-        }
-        for (int it = 0; it < 200; ++it) {
-            // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
-            if (hi - lo <= fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), fmax(eps * tn, pivmin))) break;
-            const double stp = (hi - lo) * (1.0 / 3.0);
-            const double x0 = lo + stp, x1 = fmax(x0, hi - stp);
-            int c0, c1;
-            sturm_count2(d, e2, mt, x0, x1, pivmin, c0, c1);
-            // eigenvalue j lies below x iff more than j eigenvalues do
-            if (c0 > j) {
-                hi = x0;
-            } else if (c1 > j) {
-                lo = x0;
-                hi = x1;
-            } else {
-                lo = x1;
-            }
-        }
-        lam[q] = 0.5 * (lo + hi);
-    }
-    __syncthreads();
+    stamp(0);
     double* cl = base + lay.cl;
-    if (t == 0) {
-        int nc = 0;
-        double sum = 0.0;
-        for (int q = 0; q < k; ++q) {
-            if (q == 0 || lam[q - 1] - lam[q] >= kOrtol * tn) cl[nc++] = q;
-            sum += lam[q] - tau;
+    // (side: if the eigenvalues at or below tau come in a cluster of more than TE_SIDE_CL members -- the inverse
+    // iteration orthogonalises a cluster in one thread, serially -- the other side is taken after all)
+    constexpr int TE_SIDE_CL = 8;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int q = t; q < k; q += 256) {  // trisection for the (mt-1-q)-th ascending eigenvalue (side: the q-th)
+            const int j = side ? q : mt - 1 - q;
+            double lo = gl, hi = gu;
+            {   // the first grid point with more than j eigenvalues below it (counts are monotone in x)
+                int a0 = 0, a1 = TE_GRID;
+                while (a1 - a0 > 1) {
+                    const int am = (a0 + a1) >> 1;
+                    if (gcnt[am] > j) a1 = am;
+                    else a0 = am;
+                }
+                if (gcnt[a1] > j) {
+                    lo = gl + a0 * gh;
+                    if (a1 < TE_GRID) hi = gl + a1 * gh;
+                }
+            }
+            for (int it = 0; it < 200; ++it) {
+                // LAPACK dstebz's test with its default ABSTOL = ulp ||T||
+                if (hi - lo <= fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), fmax(eps * tn, pivmin))) break;
+                const double stp = (hi - lo) * (1.0 / 3.0);
+                const double x0 = lo + stp, x1 = fmax(x0, hi - stp);
+                int c0, c1;
+                sturm_count2(d, e2, mt, x0, x1, pivmin, c0, c1);
+                // eigenvalue j lies below x iff more than j eigenvalues do
+                if (c0 > j) {
+                    hi = x0;
+                } else if (c1 > j) {
+                    lo = x0;
+                    hi = x1;
+                } else {
+                    lo = x1;
+                }
+            }
+            lam[q] = 0.5 * (lo + hi);
         }
-        cl[nc] = k;
-        s_ncl = nc;
-        base[lay.misc] = k;
-        base[lay.misc + 1] = sum;
+        __syncthreads();
+        stamp(1);
+        if (t == 0) {
+            int nc = 0, mx = 0;
+            double sum = 0.0;
+            for (int q = 0; q < k; ++q) {
+                if (q == 0 || fabs(lam[q - 1] - lam[q]) >= kOrtol * tn) cl[nc++] = q;
+                if (nc > 0) mx = max(mx, q + 1 - (int)cl[nc - 1]);
+                sum += lam[q] - tau;
+            }
+            if (side && mx > TE_SIDE_CL) {   // the eigenvalues above tau instead
+                s_side = 0;
+                s_k = mt - k;
+            } else {
+                if (side) {
+                    double tr = 0.0;
+                    for (int i = 0; i < mt; ++i) tr += d[i];
+                    sum = (tr - mt * tau) - sum;
+                }
+                cl[nc] = k;
+                s_ncl = nc;
+                base[lay.misc] = k;
+                base[lay.misc + 1] = sum;
+                base[lay.misc + 2] = side;
+                s_side = -1;   // (done)
+            }
+        }
+        __syncthreads();
+        if (s_side < 0) break;
+        side = s_side;
+        k = s_k;
     }
     __syncthreads();
+    stamp(2);
     const int ncl = s_ncl;
     double* lu = base + lay.lu;
     double* Z = base + lay.z;
@@ -890,6 +935,12 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         }
     }
     if (t == 0 && status && !(tn >= 0.0)) atomicOr(&status[status_off + b], (int)ACE_ST_EIG_NOCONV);
+#ifdef ACE_H2_STAMPS
+    stamp(3);
+    if (t == 0 && (b % 101) == 0)
+        printf("trieig b %d k %d ncl %d: grid %llu bisect %llu clus %llu invit %llu (x10ns)\n", b, k, ncl, st_ph[0],
+               st_ph[1], st_ph[2], st_ph[3]);
+#endif
 }
 
 // u_k = H_0 H_1 ... H_{mt-2} z_k  (Q of zhetrd applied to the tridiagonal eigenvectors),
@@ -1100,7 +1151,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
         else
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, n, nullptr, nullptr, scratch, lay,
                                nullptr, nullptr, 0);
-        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, n, nullptr, scratch, lay, status, b0, nullptr);
+        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, n, nullptr, scratch, lay, status, b0, nullptr, 0);
         const int cv = backxf_chunk(n);
         double* Xb = X + 2LL * b0 * r * n;
         hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * n * 16, st, n, r, scratch, lay, Xb, 0,
@@ -1130,7 +1181,7 @@ int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt,
             hipLaunchKernelGGL(hetrd_kernel, dim3(nb), dim3(HT_THREADS), sm_h, st, mt, K, Bt + (long long)b0 * ldb, scratch,
                                lay, nullptr, pr ? pr->rows + (long long)b0 * pr->m : nullptr, pr ? pr->m : 0);
         }
-        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr);
+        hipLaunchKernelGGL(trieig_kernel, dim3(nb), dim3(256), sm_t, st, mt, nullptr, scratch, lay, status, b0, nullptr, 0);
         const int cv = backxf_chunk(mt);
         hipLaunchKernelGGL(backxf_kernel, dim3(nb), dim3(256), (size_t)cv * mt * 16, st, mt, r, scratch, lay,
                            W + 2LL * b0 * r * mt, 1, nullptr, cv);
@@ -1269,14 +1320,17 @@ size_t heev_scratch_bytes(int d, int kmax, int batch) {
 }
 
 void launch_trieig(int d, int kmax, int batch, const double* tau, double* scratch, int* status, const int* active,
-                   hipStream_t st) {
+                   hipStream_t st, int side_ok) {
     const SpecLayout lay(d, kmax);
-    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), (size_t)d * 24, st, d, tau, scratch, lay, status, 0, active);
+    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), (size_t)d * 24, st, d, tau, scratch, lay, status, 0, active,
+                       side_ok);
 }
 
 int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, double* V, int* status,
-                const int* active, hipStream_t st, int path) {
-    if (path == 2 && heev2_eligible(d, kmax)) return launch_heev2(d, kmax, batch, tau, scratch, V, status, active, st);
+                const int* active, hipStream_t st, int path, int side_ok) {
+    side_ok = side_ok && tau && kmax == d;
+    if (path == 2 && heev2_eligible(d, kmax))
+        return launch_heev2(d, kmax, batch, tau, scratch, V, status, active, st, side_ok);
     int blk = path != 0;
     const SpecLayout lay(d, kmax);
     const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
@@ -1293,7 +1347,7 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
         hipLaunchKernelGGL(hetrd_kernel, dim3(batch), dim3(HT_THREADS), sm_h, st, d, nullptr, nullptr, scratch, lay, active,
                            nullptr, 0);
     }
-    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active);
+    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), sm_t, st, d, tau, scratch, lay, status, 0, active, side_ok);
     if (!wy_path(d, kmax)) {
         const int cv = backxf_chunk(d);
         hipLaunchKernelGGL(backxf_kernel, dim3(batch), dim3(256), (size_t)cv * d * 16, st, d, kmax, scratch, lay, V, 0,

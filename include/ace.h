@@ -231,10 +231,18 @@ int ace_phaselift_solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, in
                               void* workspace, size_t workspace_bytes, void* stream);
 int ace_phaselift_solve_host(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
                              const double* b, double* sig, int32_t* iters, uint32_t* status);
+/* ace_phaselift_solve_host plus solver_TraceLS's result itself (MyPhaseLift.m:98 recoveredMat, the final
+ * tfocs_AT iterate): Xr [batch][d][d] c128 (HOST), d = min(m, n), in the coordinates of range(Phi^H)
+ * (recoveredMat = Q Xr Q^H, Phi^H = Q R with R = chol(Phi Phi^H); Q = I when m > n).  For parity tests of the
+ * iterate and of the TFOCS objective 0.5 ||A(X) - b||^2 + lambda tr X. */
+int ace_phaselift_solve_host_x(const ace_phaselift_cfg* cfg, int batch, int m, int n, const double* Phi,
+                               const double* b, double* sig, int32_t* iters, uint32_t* status, double* Xr);
 /* The prox's eigensolver alone (prox_trace.m:88-92: all eigenpairs of a Hermitian d x d matrix above tau),
  * for parity tests of its paths: A [batch][d][d] c128 (HOST, Hermitian; the lower triangle is read), tau [batch];
  * lam [batch][d] (descending; entries >= k[b] undefined), V [batch][d][d] c128 (eigenvector q as row q),
- * k [batch].  path: 0 unblocked one-stage, 1 blocked one-stage, 2 two-stage (where it applies, else 1).
+ * k [batch].  path: 0 unblocked one-stage, 1 blocked one-stage, 2 two-stage (where it applies, else 1); + 4: the
+ * vectors of the smaller side of tau (PhaseLift's ACE_PROX_SIDE=1): when more than half of the eigenvalues exceed
+ * tau, V holds those at or below it (ascending) and k[b] = -(their count).
  * Synchronous; allocates its own device memory. */
 int ace_prox_eig_host(int batch, int d, int path, const double* A, const double* tau, double* lam, double* V,
                       int32_t* k);

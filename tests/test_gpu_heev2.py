@@ -22,6 +22,14 @@ def _herm(rng, d, batch, rank=None):
     return (A + np.conj(np.swapaxes(A, 1, 2))) / 2
 
 
+def _tau_at(a, f):
+    """A threshold halfway between two neighbouring eigenvalues (fraction f of the spectrum below it), so that the
+    kept count is not decided by rounding."""
+    w = np.linalg.eigvalsh(a)
+    i = min(max(int(f * len(w)), 1), len(w) - 1)
+    return 0.5 * (w[i - 1] + w[i])
+
+
 def _projector(lam, V, k, tau):
     Vk = V[:k]                       # rows = eigenvectors
     return Vk.T @ np.diag(lam[:k] - tau) @ Vk.conj()
@@ -50,7 +58,7 @@ def test_two_stage_matches_eigh(gpu, d):
     from ace_amd import prox_eig_host
     rng = np.random.default_rng(100 + d)
     A = _herm(rng, d, 3)
-    tau = np.array([np.quantile(np.linalg.eigvalsh(a), f) for a, f in zip(A, (0.4, 0.05, 0.9))])
+    tau = np.array([_tau_at(a, f) for a, f in zip(A, (0.4, 0.05, 0.9))])
     lam, V, k = prox_eig_host(A, tau, path=2)
     for b in range(3):
         _check(A[b], tau[b], lam[b], V[b], k[b])
@@ -95,3 +103,30 @@ def test_two_stage_batch_invariance(gpu):
     lam, V, k = prox_eig_host(A, tau, path=2)
     l1, V1, k1 = prox_eig_host(A[3:4], tau[3:4], path=2)
     assert k1[0] == k[3] and np.array_equal(l1[0, :k[3]], lam[3, :k[3]]) and np.array_equal(V1[0, :k[3]], V[3, :k[3]])
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_smaller_side(gpu, path):
+    """PhaseLift's default (path + 4): with more than half of the eigenvalues above tau the solver returns the
+    pairs at or below it, and X = (A - tau I) + sum_{lam <= tau} (tau - lam) v v^H is the same shrunk projector."""
+    from ace_amd import prox_eig_host
+    rng = np.random.default_rng(31)
+    d = 256
+    A = _herm(rng, d, 3)
+    tau = np.array([_tau_at(a, f) for a, f in zip(A, (0.2, 0.7, 0.45))])
+    lam, V, k = prox_eig_host(A, tau, path=path + 4)
+    for b in range(3):
+        w, U = np.linalg.eigh(A[b])
+        above = int((w > tau[b]).sum())
+        nrm = np.linalg.norm(A[b])
+        Xr = U[:, w > tau[b]] @ np.diag(w[w > tau[b]] - tau[b]) @ U[:, w > tau[b]].conj().T
+        if 2 * above > d:
+            kc = -k[b]
+            assert kc == d - above
+            Vk = V[b, :kc]
+            assert np.abs(lam[b, :kc] - w[:kc]).max() <= 1e-11 * nrm
+            X = A[b] - tau[b] * np.eye(d) + Vk.T @ np.diag(tau[b] - lam[b, :kc]) @ Vk.conj()
+        else:
+            assert k[b] == above
+            X = _projector(lam[b], V[b], k[b], tau[b])
+        assert np.linalg.norm(X - Xr) <= 1e-11 * nrm, (b, np.linalg.norm(X - Xr) / nrm)

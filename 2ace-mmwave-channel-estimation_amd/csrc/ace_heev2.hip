@@ -44,7 +44,10 @@ constexpr int S2_THREADS = 512, S2_NW = S2_THREADS / 64;
 // (s_j = i + 1 + 16 j); step j - 2 of sweep i + 1 touches rows [s_j - 31, s_j - 15), disjoint from it, and needs only
 // steps <= j - 1 of sweep i (their footprints meet at row s_j - 16), which ran a super-step earlier
 constexpr int S2_LAG = 2;
-constexpr int ABS = 33;          // LDS stride (complex) of a band column: offsets 0..31 (band 16 + bulge), 1 pad
+// LDS stride (complex) of a band column: offsets 0..31 (band 16 + bulge) and 2 pad, so that A[r][c] sits at
+// (ABS - 1) c + r == c + r (mod 16 complex = the 64 banks): the chase's row-wise and column-wise 16 x 16 block
+// accesses both spread over the banks (with 33, c + r became r: 16-way conflicts on the column-wise ones)
+constexpr int ABS = 34;
 
 // per-realisation extra scratch (doubles): T of the stage-1 panels [np][16][16], the panel's W [dp][16] and V,
 // the stage-2 reflectors (v[16], tau) of sweep i, step j at [ts][r][j] with the back-transform's time step
@@ -174,7 +177,10 @@ __device__ __forceinline__ void panel_qr(int d, int k, int r0, int dp, d2* C, d2
     const int L = dp - r0, tt = L >> 4, rr = t, r = r0 + rr;
     d2 P[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) P[c] = (rr < L && r < d && k + c < d) ? C[(long long)r * d + k + c] : czero();
+    for (int c = 0; c < 16; ++c) {   // (unconditional loads from clamped addresses, then masked: see ldC)
+        const d2 x = C[(long long)min(r, d - 1) * d + min(k + c, d - 1)];
+        P[c] = (rr < L && r < d && k + c < d) ? x : czero();
+    }
     d2* tbw = q.tb[w];
     // (one call per column with j a compile-time constant: the register array P is indexed by constants only)
     auto col_step = [&](auto jc) {
@@ -310,7 +316,12 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
     __shared__ QrLds q;
     __shared__ d2 sT[256];
     d2* slw = q.tb[w];   // the wave's X / M slot (its QR partials' space)
-    auto ldC = [&](int r, int c) -> d2 { return (r < d && c < d) ? C[(long long)r * d + c] : czero(); };
+    // (loads unconditional from a clamped address, then masked: no branch around a load, so that a tile's loads
+    // issue together instead of one wait each)
+    auto ldC = [&](int r, int c) -> d2 {
+        const d2 v = C[(long long)min(r, d - 1) * d + min(c, d - 1)];
+        return (r < d && c < d) ? v : czero();
+    };
     auto stC = [&](int r, int c, d2 v) {
         if (r < d && c < d) C[(long long)r * d + c] = v;
     };
@@ -329,53 +340,59 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         const d2* Vg = Vg2;
         panel_qr(d, 16 * p, r0, dp, C, Vg2, T1 + p * 256, sT, q);
         stamp(0);
-        // ---- X = A22 V T for the wave's block rows I
+        // ---- X = A22 V T for the wave's block rows I = w + 4 h, XG of them at once per block column J (the
+        // tiles' operand loads of one J in flight together: the phase is bound by memory round trips)
         // (X goes to Wg tile by tile, W is formed in place; M = V^H X accumulates as the tiles come)
+        auto lda = [&](int I, int J, int s) -> d2 {   // A22 tile (I, J) from the lower triangle (branch-free)
+            const int ri = r0 + 16 * I, rj = r0 + 16 * J, c = 4 * s + lr;
+            const bool below = J < I || (J == I && lc >= c);
+            d2 x = ldC(below ? ri + lc : rj + c, below ? rj + c : ri + lc);
+            x.y = below ? (J == I && lc == c ? 0.0 : x.y) : -x.y;
+            return x;
+        };
         Cacc Mp = cacc0();
-        for (int h = 0; h < S1_NH; ++h) {
-            const int I = w + S1_NW * h;
-            if (I >= tt) continue;
-            const int ri = r0 + 16 * I;
-            auto lda = [&](int J, int s) -> d2 {
-                const int rj = r0 + 16 * J, c = 4 * s + lr;
-                if (J < I) return ldC(ri + lc, rj + c);
-                if (J > I) return cconj(ldC(rj + c, ri + lc));
-                return lc > c ? ldC(ri + lc, ri + c) : (lc < c ? cconj(ldC(ri + c, ri + lc)) : make_double2(ldC(ri + c, ri + c).x, 0.0));
-            };
-            Cacc Y = cacc0();
-            d2 a[4], bv[4];
+        constexpr int XG = 2;   // block rows per pass (registers: XG accumulators and XG x 4 operands)
+        for (int h0 = 0; h0 < S1_NH; h0 += XG) {
+            if (w + S1_NW * h0 >= tt) break;
+            Cacc Y[XG];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                a[s] = lda(0, s);
-                bv[s] = Vg[(4 * s + lr) * 16 + lc];
-            }
+            for (int h = 0; h < XG; ++h) Y[h] = cacc0();
             for (int J = 0; J < tt; ++J) {
-                d2 an[4], bn[4];
-                const bool nx = J + 1 < tt;
+                d2 bv[4], a[XG][4];
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    an[s] = nx ? lda(J + 1, s) : czero();
-                    bn[s] = nx ? Vg[(16 * (J + 1) + 4 * s + lr) * 16 + lc] : czero();
+                for (int s = 0; s < 4; ++s) bv[s] = Vg[(16 * J + 4 * s + lr) * 16 + lc];
+#pragma unroll
+                for (int h = 0; h < XG; ++h) {
+                    const int I = w + S1_NW * (h0 + h);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const d2 x = lda(min(I, tt - 1), J, s);
+                        a[h][s] = I < tt ? x : czero();
+                    }
                 }
 #pragma unroll
-                for (int s = 0; s < 4; ++s) cmma(Y, a[s], bv[s]);
+                for (int h = 0; h < XG; ++h)
+                    if (w + S1_NW * (h0 + h) < tt) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    a[s] = an[s];
-                    bv[s] = bn[s];
-                }
+                        for (int s = 0; s < 4; ++s) cmma(Y[h], a[h][s], bv[s]);
+                    }
             }
 #pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4) slw[(lr + 4 * j4) * 16 + lc] = cget(Y, j4);
-            wave_sync();
-            Cacc Xh = cacc0();
+            for (int h = 0; h < XG; ++h) {
+                const int I = w + S1_NW * (h0 + h);
+                if (I >= tt) continue;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) cmma(Xh, slw[lc * 16 + 4 * s + lr], sT[(4 * s + lr) * 16 + lc]);
-            wave_sync();
+                for (int j4 = 0; j4 < 4; ++j4) slw[(lr + 4 * j4) * 17 + lc] = cget(Y[h], j4);   // (row stride 17:
+                wave_sync();                                                                      // the transposed read)
+                Cacc Xh = cacc0();
 #pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4) Wg[(16 * I + lr + 4 * j4) * 16 + lc] = cget(Xh, j4);
+                for (int s = 0; s < 4; ++s) cmma(Xh, slw[lc * 17 + 4 * s + lr], sT[(4 * s + lr) * 16 + lc]);
+                wave_sync();
 #pragma unroll
-            for (int s = 0; s < 4; ++s) cmma(Mp, cconj(Vg[(16 * I + 4 * s + lr) * 16 + lc]), cget(Xh, s));
+                for (int j4 = 0; j4 < 4; ++j4) Wg[(16 * I + lr + 4 * j4) * 16 + lc] = cget(Xh, j4);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) cmma(Mp, cconj(Vg[(16 * I + 4 * s + lr) * 16 + lc]), cget(Xh, s));
+            }
         }
         stamp(1);
         // ---- M = V^H X (partials per wave, summed in wave order), S = T^H M, W = X - V S / 2
@@ -406,38 +423,61 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         }
         __syncthreads();
         stamp(2);
-        // ---- A22 -= V W^H + W V^H on the lower tiles
-        auto upd = [&](int I, int J) {
-            const int ri = r0 + 16 * I, rj = r0 + 16 * J;
-            d2 vi[4], wi[4], wj[4], vj[4];
-            Cacc A;
-#pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4) {
-                const d2 x = ldC(ri + lr + 4 * j4, rj + lc);
-                A.r[j4] = x.x;
-                A.i[j4] = x.y;
-            }
+        // ---- A22 -= V W^H + W V^H on the lower tiles: wave w takes the block rows of snake order (I mod 8 = w or
+        // 7 - w: equal tile counts per wave), two rows at a time with both rows' tiles of one J loaded together
+        for (int pr = 0; pr < 2; ++pr) {
+            const int Ia = 8 * pr + w, Ib = 8 * pr + 7 - w;   // (Ia < Ib)
+            if (Ia >= tt) break;
+            const bool hb = Ib < tt;
+            d2 va[4], wa[4], vb2[4], wb2[4];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int c = 4 * s + lr;
-                vi[s] = Vg[(16 * I + lc) * 16 + c];
-                wi[s] = Wg[(16 * I + lc) * 16 + c];
-                wj[s] = Wg[(16 * J + lc) * 16 + c];
-                vj[s] = Vg[(16 * J + lc) * 16 + c];
+                va[s] = Vg[(16 * Ia + lc) * 16 + c];
+                wa[s] = Wg[(16 * Ia + lc) * 16 + c];
+                vb2[s] = Vg[(16 * min(Ib, tt - 1) + lc) * 16 + c];   // (unused unless hb)
+                wb2[s] = Wg[(16 * min(Ib, tt - 1) + lc) * 16 + c];
             }
+            const int Jn = hb ? Ib : Ia;
+            for (int J = 0; J <= Jn; ++J) {
+                const int rj = r0 + 16 * J;
+                const bool ta = J <= Ia;
+                d2 wj[4], vj[4];
+                Cacc A0, A1;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                cmma(A, cneg(vi[s]), cconj(wj[s]));
-                cmma(A, cneg(wi[s]), cconj(vj[s]));
+                for (int s = 0; s < 4; ++s) {
+                    const int c = 4 * s + lr;
+                    wj[s] = Wg[(16 * J + lc) * 16 + c];
+                    vj[s] = Vg[(16 * J + lc) * 16 + c];
+                }
+#pragma unroll
+                for (int j4 = 0; j4 < 4; ++j4) {
+                    const d2 x0 = ldC(r0 + 16 * Ia + lr + 4 * j4, rj + lc);   // (used if ta)
+                    const d2 x1 = ldC(r0 + 16 * Ib + lr + 4 * j4, rj + lc);   // (used if hb)
+                    A0.r[j4] = x0.x;
+                    A0.i[j4] = x0.y;
+                    A1.r[j4] = x1.x;
+                    A1.i[j4] = x1.y;
+                }
+                if (ta) {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        cmma(A0, cneg(va[s]), cconj(wj[s]));
+                        cmma(A0, cneg(wa[s]), cconj(vj[s]));
+                    }
+#pragma unroll
+                    for (int j4 = 0; j4 < 4; ++j4) stC(r0 + 16 * Ia + lr + 4 * j4, rj + lc, cget(A0, j4));
+                }
+                if (hb) {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        cmma(A1, cneg(vb2[s]), cconj(wj[s]));
+                        cmma(A1, cneg(wb2[s]), cconj(vj[s]));
+                    }
+#pragma unroll
+                    for (int j4 = 0; j4 < 4; ++j4) stC(r0 + 16 * Ib + lr + 4 * j4, rj + lc, cget(A1, j4));
+                }
             }
-#pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4) stC(ri + lr + 4 * j4, rj + lc, cget(A, j4));
-        };
-        const int nt = tt * (tt + 1) / 2;   // tiles I >= J
-        for (int e = w; e < nt; e += S1_NW) {
-            int I = 0;
-            while ((I + 1) * (I + 2) / 2 <= e) ++I;   // e = I (I + 1) / 2 + J, 0 <= J <= I
-            upd(I, e - I * (I + 1) / 2);
         }
         __syncthreads();
         stamp(3);
@@ -470,6 +510,16 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
         AB[c * ABS + o] = v;
     }
     __syncthreads();
+#ifdef ACE_H2_STAMPS
+    unsigned long long hs[4] = {0, 0, 0, 0}, hs_t = __builtin_amdgcn_s_memtime();
+    auto hstamp = [&](int ph) {
+        const unsigned long long n = __builtin_amdgcn_s_memtime();
+        hs[ph] += n - hs_t;
+        hs_t = n;
+    };
+#else
+    auto hstamp = [](int) {};
+#endif
     auto at = [&](int r, int c) -> d2& { return AB[c * ABS + (r - c)]; };   // r >= c
     auto herm = [&](int r, int c) -> d2 {
         if (r > c) return AB[c * ABS + (r - c)];
@@ -556,6 +606,7 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                     if (lq < len2 && cc < len) at(s0 + lq, r0 + cc) = csub(bk[u], cmul(y, cconj(vb[w][cc])));
                 }
                 wave_sync();
+                hstamp(0);
                 // the bulge's first column -> the new reflector, applied from the left to the block (lane: column
                 // lq, rows lm + 4 u)
                 d2 xc[4], bc[4];
@@ -597,13 +648,18 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                 r0 = s0;
                 len = len2;
                 wave_sync();
+                hstamp(1);
                 two_sided(r0, len, tau);
+                hstamp(2);
             }
         }
         lds_barrier();   // (the Q2 slots are global stores read only by bt2q2_kernel)
+        hstamp(3);
     }
 #ifdef ACE_H2_STAMPS
-    if (t == 0 && (b % 101) == 0) printf("hb2st b %d: %d super-steps\n", b, nss);
+    if (t == 0 && (b % 101) == 0)
+        printf("hb2st b %d: %d super-steps, wave 0 cycles: right %llu left %llu two-sided %llu barrier %llu\n", b, nss,
+               hs[0], hs[1], hs[2], hs[3]);
 #endif
     double* dd = base + hl.dd;
     double* ee = base + hl.ee;

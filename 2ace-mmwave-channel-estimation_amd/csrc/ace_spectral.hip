@@ -627,6 +627,93 @@ __device__ __forceinline__ void sturm_count2(const double* d, const double* e2, 
     c1 = n1;
 }
 
+// The eigenvector of an isolated eigenvalue lq (no other within kOrtol ||T||) by one twisted factorization
+// (Fernando; Parlett & Dhillon, the core of LAPACK dstemr's dlar1v, here on T - lq I itself):
+//   T - lq I = L+ D+ L+^T  (top down: D+_0 = d_0 - lq, L_i = e_i / D+_i, D+_{i+1} = d_{i+1} - lq - L_i e_i)
+//            = U- D- U-^T  (bottom up: D-_{n-1} = d_{n-1} - lq, U_i = e_i / D-_{i+1}, D-_i = d_i - lq - U_i e_i),
+// gamma_k = D+_k + D-_k - (d_k - lq), r = argmin |gamma_k|, z_r = 1, z_i = -L_i z_{i+1} (i < r),
+// z_{i+1} = -U_i z_i (i >= r), normalised.  It is the inverse-iteration step from the best unit start vector e_r
+// ((T - lq I) z = gamma_r e_r), in three passes over the row with two stored arrays instead of dgttrf's five and two
+// solves (the LU arrays are the path's HBM traffic).  Near-zero pivots are moved to +-tiny as in dlagts.  Returns
+// false (nothing written that the caller keeps) if the vector is not finite: the caller's inverse iteration then
+// runs.
+template <class At>
+__device__ bool twisted_vector(const double* d, const double* e, int mt, double lq, double tiny, double* zq, At at) {
+    auto guard = [&](double x) { return fabs(x) < tiny ? (x < 0.0 ? -tiny : tiny) : x; };
+    double Dp = guard(d[0] - lq);
+    for (int i = 0; i + 1 < mt; ++i) {   // top down: D+ (array 1), L (array 0)
+        const double Li = e[i] / Dp;
+        at(1, i) = Dp;
+        at(0, i) = Li;
+        Dp = guard(d[i + 1] - lq - Li * e[i]);
+    }
+    at(1, mt - 1) = Dp;
+    // bottom up: U (array 2), gamma against the stored D+ (loads issued TE_PF rows ahead of the chain)
+    double Dm = guard(d[mt - 1] - lq), best = fabs(Dp);
+    int r = mt - 1;
+    for (int i0 = mt - 2; i0 >= 0; i0 -= TE_PF) {
+        double dpv[TE_PF];
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) dpv[u] = at(1, max(i0 - u, 0));
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) {
+            const int i = i0 - u;
+            if (i < 0) break;
+            const double Ui = e[i] / Dm;
+            at(2, i) = Ui;
+            const double dl = d[i] - lq;
+            Dm = guard(dl - Ui * e[i]);
+            const double g = fabs(dpv[u] + Dm - dl);
+            if (g < best) {
+                best = g;
+                r = i;
+            }
+        }
+    }
+    // z outward from r (loads ahead of the chain), then normalised in place
+    double nrm = 1.0, z = 1.0;
+    zq[r] = 1.0;
+    for (int i0 = r - 1; i0 >= 0; i0 -= TE_PF) {
+        double lv[TE_PF];
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) lv[u] = at(0, max(i0 - u, 0));
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) {
+            const int i = i0 - u;
+            if (i < 0) break;
+            z = -lv[u] * z;
+            zq[i] = z;
+            nrm += z * z;
+        }
+    }
+    z = 1.0;
+    for (int i0 = r; i0 + 1 < mt; i0 += TE_PF) {
+        double uv[TE_PF];
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) uv[u] = at(2, min(i0 + u, mt - 2));
+#pragma unroll
+        for (int u = 0; u < TE_PF; ++u) {
+            const int i = i0 + u;
+            if (i + 1 >= mt) break;
+            z = -uv[u] * z;
+            zq[i + 1] = z;
+            nrm += z * z;
+        }
+    }
+    if (!(nrm < INFINITY)) return false;   // (overflow or NaN: the caller's inverse iteration)
+    const double inv = 1.0 / sqrt(nrm);
+    constexpr int TE_CP = 32;
+    for (int i0 = 0; i0 < mt; i0 += TE_CP) {
+        double tv[TE_CP];
+#pragma unroll
+        for (int u = 0; u < TE_CP; ++u) tv[u] = zq[min(i0 + u, mt - 1)];
+#pragma unroll
+        for (int u = 0; u < TE_CP; ++u)
+            if (i0 + u < mt) zq[i0 + u] = tv[u] * inv;
+    }
+    return true;
+}
+
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
@@ -645,7 +732,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (active && !active[b]) return;
 #ifdef ACE_H2_STAMPS
-    unsigned long long st_ph[4] = {0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_ph[4] = {0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime(), st_t0 = st_t;
     auto stamp = [&](int ph) {
         const unsigned long long n = __builtin_amdgcn_s_memrealtime();
         st_ph[ph] += n - st_t;
@@ -804,6 +891,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         const int ln = c % lay.lanes;
         auto at = [&](int arr, int i) -> double& { return lu[((long long)arr * mt + i) * lay.lanes + ln]; };
         const int q0 = (int)cl[c], q1 = (int)cl[c + 1];
+        if (q1 - q0 == 1 && twisted_vector(d, e, mt, lam[q0], tiny, Z + (long long)q0 * mt, at)) continue;
         for (int q = q0; q < q1; ++q) {
             const double lq = lam[q];
             // dgttrf on T - lq I with the running diagonal / superdiagonal entries carried in
@@ -940,6 +1028,15 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     if (t == 0 && (b % 101) == 0)
         printf("trieig b %d k %d ncl %d: grid %llu bisect %llu clus %llu invit %llu (x10ns)\n", b, k, ncl, st_ph[0],
                st_ph[1], st_ph[2], st_ph[3]);
+    __syncthreads();
+    if (t == 0) {   // slow work-groups: wall time and the largest cluster
+        const unsigned long long wall = __builtin_amdgcn_s_memrealtime() - st_t0;
+        if (wall > 180000) {
+            int mx = 0;
+            for (int c = 0; c < ncl; ++c) mx = max(mx, (int)cl[c + 1] - (int)cl[c]);
+            printf("trieig-slow b %d k %d ncl %d maxcl %d wall %llu bisect %llu\n", b, k, ncl, mx, wall, st_ph[1]);
+        }
+    }
 #endif
 }
 

@@ -9,7 +9,8 @@ oracle is the oracle's own envelope, as in test_gpu_parity.py::test_nuclear_mspa
 
     bound = max(1e-8, 100 * ||oracle(B) - oracle(B (1 + 1e-15))||)        (relative, phase aligned)
 
-per sampled realisation: tight (1e-8) where the reference is stable, as loose as the reference itself where it is
+(A2nuclear: the largest such distance over four perturbations of that size, B (1 +- 1e-15), B (1 + 3e-15),
+X0 (1 + 1e-15)) per sampled realisation: tight (1e-8) where the reference is stable, as loose as the reference itself where it is
 not.  The TFOCS objective 0.5 ||A(X) - b||^2 + lambda tr X (tfocs_AT.m:20-88, smooth_quad + prox_trace) of the final
 iterate is held to the same kind of bound: at 200 iterations it moves ~8e-4 relative under the 1e-15 perturbation
 in the oracle itself, so a fixed 1e-8 bar would fail the reference against itself (measured, r06).
@@ -72,13 +73,17 @@ def test_nuclear_config3_full_horizon_envelope(gpu):
     Ah, Bh, X0h = A.cpu().numpy(), B.cpu().numpy()[idx], X0.cpu().numpy()[idx]
     U = OC.make_U(Ah[0])[None]
     Xo, _, ito, _, _ = OC.infer_admm_r1_batch(Ah, U, Bh, X0h, 32, 32, variant=1, maxiter=200, fixed_iters=True)
-    Xp, _, _, _, _ = OC.infer_admm_r1_batch(Ah, U, Bh * (1 + 1e-15), X0h, 32, 32, variant=1, maxiter=200,
-                                           fixed_iters=True)
     assert (ito == 200).all()
+    # the envelope from several 1e-15-sized perturbations (one sample under-states it: on a chaotic realisation the
+    # oracle's own distance ranges over 5e-4 .. 1.3 between perturbations of the same size, measured)
+    noise = np.zeros(len(idx))
+    for Bq, Xq in ((Bh * (1 + 1e-15), X0h), (Bh * (1 - 1e-15), X0h), (Bh, X0h * (1 + 1e-15)),
+                   (Bh * (1 + 3e-15), X0h)):
+        Xp, _, _, _, _ = OC.infer_admm_r1_batch(Ah, U, Bq, Xq, 32, 32, variant=1, maxiter=200, fixed_iters=True)
+        noise = np.maximum(noise, [O.unit_phase_aligned_rel_err(Xp[k], Xo[k]) for k in range(len(idx))])
     tight = 0
     for k in range(len(idx)):
-        noise = O.unit_phase_aligned_rel_err(Xp[k], Xo[k])
-        bound = max(1e-8, 100 * noise)
+        bound = max(1e-8, 100 * noise[k])
         tight += bound == 1e-8
-        assert O.unit_phase_aligned_rel_err(X[k], Xo[k]) <= bound, (idx[k], noise)
+        assert O.unit_phase_aligned_rel_err(X[k], Xo[k]) <= bound, (idx[k], noise[k])
     print(f"A2nuclear 200 iterations: {tight} of {len(idx)} sampled realisations held to 1e-8")

@@ -526,14 +526,15 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
         if (r < c) return cconj(AB[r * ABS + (c - r)]);
         return make_double2(AB[c * ABS].x, 0.0);
     };
-    // D <- H^H D H on the diagonal block [r0, r0 + len) with v in vb[w] (zhetd2's x, w, rank-2 update);
-    // lane (row lq, columns lm + 4 u)
+    // D <- H^H D H on the diagonal block [r0, r0 + len) with v in vb[w] and the lane's entries v[lm + 4 u] in vr
+    // (zhetd2's x, w, rank-2 update); lane (row lq, columns lm + 4 u)
+    d2 vr[4];
     auto two_sided = [&](int r0, int len, d2 tau) {
         d2 xr = czero();
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int cc = lm + 4 * u;
-            if (lq < len && cc < len) xr = cadd(xr, cmul(herm(r0 + lq, r0 + cc), vb[w][cc]));
+            if (lq < len && cc < len) xr = cadd(xr, cmul(herm(r0 + lq, r0 + cc), vr[u]));
         }
         xr = cmul(tau, quad_sum(xr));
         const d2 vq = lq < len ? vb[w][lq] : czero();
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
             const int cc = lm + 4 * u;
             if (lq < len && cc <= lq) {
                 d2& a = at(r0 + lq, r0 + cc);
-                d2 x = csub(a, cadd(cmul(vq, cconj(wb[w][cc])), cmul(wr, cconj(vb[w][cc]))));
+                d2 x = csub(a, cadd(cmul(vq, cconj(wb[w][cc])), cmul(wr, cconj(vr[u]))));
                 if (cc == lq) x.y = 0.0;
                 a = x;
             }
@@ -586,6 +587,8 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                     if (lq == 0) slot(16) = tau;
                 }
                 wave_sync();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) vr[u] = vb[w][lm + 4 * u];
                 two_sided(r0, len, tau);
             } else {
                 const int s0 = r0 + len, len2 = min(16, d - s0);
@@ -597,13 +600,13 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                 for (int u = 0; u < 4; ++u) {
                     const int cc = lm + 4 * u;
                     bk[u] = (lq < len2 && cc < len) ? at(s0 + lq, r0 + cc) : czero();
-                    y = cadd(y, cmul(bk[u], vb[w][cc]));
+                    y = cadd(y, cmul(bk[u], vr[u]));   // (the previous reflector's entries, kept in registers)
                 }
                 y = cmul(tau, quad_sum(y));
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int cc = lm + 4 * u;
-                    if (lq < len2 && cc < len) at(s0 + lq, r0 + cc) = csub(bk[u], cmul(y, cconj(vb[w][cc])));
+                    if (lq < len2 && cc < len) at(s0 + lq, r0 + cc) = csub(bk[u], cmul(y, cconj(vr[u])));
                 }
                 wave_sync();
                 hstamp(0);
@@ -644,6 +647,8 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
                     }
                 }
                 if (lane == 0) slot(16) = R.tau;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) vr[u] = v2[u];   // (rows lm + 4 u: the layout two_sided reads)
                 tau = R.tau;
                 r0 = s0;
                 len = len2;

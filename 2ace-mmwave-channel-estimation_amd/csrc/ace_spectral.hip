@@ -714,6 +714,9 @@ __device__ bool twisted_vector(const double* d, const double* e, int mt, double 
     return true;
 }
 
+// dynamic LDS of trieig_kernel: d, e, e^2 and the eigenvalues (k <= mt), mt doubles each
+size_t trieig_lds(int mt) { return (size_t)mt * 32; }
+
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
@@ -745,6 +748,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
     double* d = smem;
     double* e = smem + mt;
     double* e2 = smem + 2 * mt;
+    double* slam = smem + 3 * mt;   // (the eigenvalues again, for the serial cluster scan)
     __shared__ double red[3 * 4];
     __shared__ int s_k, s_ncl;
     double* base = scratch + b * lay.stride;
@@ -847,17 +851,20 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
                     lo = x1;
                 }
             }
-            lam[q] = 0.5 * (lo + hi);
+            lam[q] = slam[q] = 0.5 * (lo + hi);
         }
         __syncthreads();
         stamp(1);
         if (t == 0) {
-            int nc = 0, mx = 0;
+            int nc = 0, mx = 0, cs = 0;   // (cs: the current cluster's first index, in a register)
             double sum = 0.0;
             for (int q = 0; q < k; ++q) {
-                if (q == 0 || fabs(lam[q - 1] - lam[q]) >= kOrtol * tn) cl[nc++] = q;
-                if (nc > 0) mx = max(mx, q + 1 - (int)cl[nc - 1]);
-                sum += lam[q] - tau;
+                if (q == 0 || fabs(slam[q - 1] - slam[q]) >= kOrtol * tn) {
+                    cl[nc++] = q;
+                    cs = q;
+                }
+                mx = max(mx, q + 1 - cs);
+                sum += slam[q] - tau;
             }
             if (side && mx > TE_SIDE_CL) {   // the eigenvalues above tau instead
                 s_side = 0;
@@ -1226,7 +1233,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
                            double* scratch, double* X, int* status, hipStream_t st, const PartRows* pr) {
     if (pr) mt = pr->m;   // the full A^H, B and K; test rows weighted zero
     const SpecLayout lay(n, r);
-    const size_t sm_h = hetrd_lds(n), sm_t = (size_t)n * 24;
+    const size_t sm_h = hetrd_lds(n), sm_t = trieig_lds(n);
     if (!hetrd_lds_ok(n)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() &&
                      lds_ok(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>), hetrd_blk_lds(n, HB_NB_SPEC));
@@ -1261,7 +1268,7 @@ int launch_spectral_primal(int mt, int n, int r, int batch, const double* K, con
 int launch_spectral(int mt, int r, int batch, const double* K, const double* Bt, double* scratch, double* W,
                     int* status, hipStream_t st, const PartRows* pr) {
     const SpecLayout lay(mt, r);
-    const size_t sm_h = hetrd_lds(mt), sm_t = (size_t)mt * 24;
+    const size_t sm_h = hetrd_lds(mt), sm_t = trieig_lds(mt);
     if (!hetrd_lds_ok(mt)) return ACE_ERR_UNSUPPORTED;
     const bool blk = spectral_blk() &&
                      lds_ok(reinterpret_cast<const void*>(&hetrd_blk_kernel<HB_NB_SPEC>), hetrd_blk_lds(mt, HB_NB_SPEC));
@@ -1419,7 +1426,7 @@ size_t heev_scratch_bytes(int d, int kmax, int batch) {
 void launch_trieig(int d, int kmax, int batch, const double* tau, double* scratch, int* status, const int* active,
                    hipStream_t st, int side_ok) {
     const SpecLayout lay(d, kmax);
-    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), (size_t)d * 24, st, d, tau, scratch, lay, status, 0, active,
+    hipLaunchKernelGGL(trieig_kernel, dim3(batch), dim3(256), trieig_lds(d), st, d, tau, scratch, lay, status, 0, active,
                        side_ok);
 }
 
@@ -1430,7 +1437,7 @@ int launch_heev(int d, int kmax, int batch, const double* tau, double* scratch, 
         return launch_heev2(d, kmax, batch, tau, scratch, V, status, active, st, side_ok);
     int blk = path != 0;
     const SpecLayout lay(d, kmax);
-    const size_t sm_h = hetrd_lds(d), sm_t = (size_t)d * 24;
+    const size_t sm_h = hetrd_lds(d), sm_t = trieig_lds(d);
     if (!hetrd_lds_ok(d)) return ACE_ERR_UNSUPPORTED;
     // the blocked reduction (hetrd_blk_kernel): blk = 1 (the caller reads ACE_HETRD_BLK once per solve)
     // (a check that records nothing: the unblocked reduction takes any d hetrd_lds_ok admits, so a blocked form

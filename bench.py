@@ -286,7 +286,7 @@ PMC_KERNEL["refine"] = PMC_KERNEL["unit"]   # the unit on the pipeline's X_max (
 PMC_KERNEL["pipeline"] = {"apply_AH": "i8ah_kernel<false, false>", "apply_A": "i8a_kernel",
                           "apply_K": "i8ah_kernel<true, false>", "apply_G": "zgemm3m_kernel<0, false",
                           "zstep": "zstep_kernel", "ystep": "ystep_r_kernel", "pre": "pre_kernel"}
-PMC_KERNEL["phaselift"] = {"zstep": "hetrd"}   # hetrd_blk_kernel (or hetrd_kernel with ACE_HETRD_BLK=0)
+PMC_KERNEL["phaselift"] = {"zstep": "he2hb_kernel"}   # the two-stage reduction's stage 1 (ace_heev2.hip)
 
 
 def _cpu_model():
@@ -889,17 +889,18 @@ def bench_phaselift(args, dev, rank, world):
              "apply_A": "A(z) GEMM", "ystep": "x update, backtracking", "final": "final eig + map"}
     if roof:
         roof["kernel"] = names.get(roof["kernel"], roof["kernel"])
-        if roof.get("traffic") and roof.get("traffic_kernel") == "hetrd":
-            # the traffic is the blocked tridiagonalisation's (PMC per launch of bsz matrices of order d): against
-            # its compulsory bytes (read C, write the reflectors) and against the one-stage reduction's floor,
-            # which reads the lower triangle of the trailing matrix once per column (d^3 / 6 entries) besides
+        if roof.get("traffic") and roof.get("traffic_kernel") == "he2hb_kernel":
+            # the traffic is stage 1 of the two-stage reduction (PMC per launch of bsz matrices of order d): against
+            # its compulsory bytes (read C, write the band and the reflectors: 2 d^2 complex) and against the
+            # blocked algorithm's own floor: per panel of 16, X = A V reads the trailing matrix (L^2 entries through
+            # its lower triangle) and the update reads and writes that lower triangle (L^2), sum 2 L^2 ~ d^3 / 24
             d = min(m, tx * tx)
             comp = bsz * 2 * 16 * d * d
-            lvl2 = bsz * 16 * (d ** 3 / 6 + 2 * d * d)
+            blk = bsz * 16 * d ** 3 / 24
             roof["traffic_algorithmic"] = comp
             roof["traffic_per_algorithmic"] = round(roof["traffic"] / comp, 3)
-            roof["traffic_level2_floor"] = round(lvl2)
-            roof["traffic_per_level2_floor"] = round(roof["traffic"] / lvl2, 3)
+            roof["traffic_blocked_floor"] = round(blk)
+            roof["traffic_per_blocked_floor"] = round(roof["traffic"] / blk, 3)
     line = {
         "metric": PL_METRIC, "value": round(world * bsz * args.steps / elapsed, 3), "unit": "recoveries/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

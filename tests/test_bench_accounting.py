@@ -134,7 +134,7 @@ def test_work_roofline_attaches_class_kernel_traffic(tmp_path, monkeypatch):
     b = _bench()
     prof = tmp_path / "profiles"
     prof.mkdir()
-    (prof / "r03_v9_phaselift_pmc_hbm.json").write_text(json.dumps({"hetrd_kernel": {"hbm_bytes": 5.0},
+    (prof / "r03_v9_phaselift_pmc_hbm.json").write_text(json.dumps({"he2hb_kernel": {"hbm_bytes": 5.0},
                                                                      "_meta": {"batch": 512}}))
     monkeypatch.setattr(b, "ROOT", tmp_path)
     kt = [0.0] * 10
@@ -142,7 +142,7 @@ def test_work_roofline_attaches_class_kernel_traffic(tmp_path, monkeypatch):
     kw, kb, ko = [0.0] * 10, [0.0] * 10, [0.0] * 10
     kt[8], kn[8], kw[8] = 100.0, 10, 1e12        # zstep class: the prox eig
     r, shares = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="phaselift", batch=512)
-    assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "hetrd"
+    assert r["kernel"] == "zstep" and r["traffic"] == 5 and r["traffic_kernel"] == "he2hb_kernel"
     r, _ = b.work_roofline(kt, kn, kw, kb, ko, "note", tag="pipeline", batch=512)
     assert r["traffic"] is None
 

@@ -43,7 +43,7 @@ CASES = [
     # the two-stage prox eigensolver (r06): every order it takes (32 <= d <= 256)
     ("he2hb", "ace_heev2.hip", [r"12he2hb_kernel"], [32, 40, 121, 200, 256]),
     ("hb2st", "ace_heev2.hip", [r"12hb2st_kernel"], [32, 40, 121, 200, 256]),
-    ("bt2", "ace_heev2.hip", [r"10bt2_kernel"], [32, 40, 121, 200, 256]),
+    ("bt2", "ace_heev2.hip", [r"12bt2q2_kernel", r"12bt2q1_kernel"], [32, 40, 121, 200, 256]),
 ]
 
 _REMARK = re.compile(r"remark: Function Name: (\S+)|remark:\s+LDS Size \[bytes/block\]: (\d+)")

@@ -53,7 +53,7 @@ constexpr int ABS = 34;
 // the stage-2 reflectors (v[16], tau) of sweep i, step j at [ts][r][j] with the back-transform's time step
 // ts = d - 2 - i + j (q2_index): the 16 step lanes of a time step read 16 consecutive entries per element r
 struct H2Lay {
-    long long T1, W, V, Q2, stride;
+    long long T1, W, V, VT, Q2, stride;
     int dp, np, jm;
 };
 H2Lay h2lay(int d) {
@@ -66,6 +66,7 @@ H2Lay h2lay(int d) {
     x.T1 = take(2LL * std::max(1, x.np) * 256);
     x.W = take(2LL * x.dp * 16);
     x.V = take(2LL * 2 * x.dp * 16);   // the stage-1 panel's V [2][dp][16] (double-buffered: look-ahead QR)
+    x.VT = take(2LL * std::max(1, x.np) * x.dp * 16);   // V_p T_p^H per panel [np][dp][16] (rows from the panel's r0)
     x.Q2 = take(2LL * (d + 14) * 17 * 16);
     x.stride = o;
     return x;
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
     d2* T1 = reinterpret_cast<d2*>(xb + xl.T1);
     d2* Wg = reinterpret_cast<d2*>(xb + xl.W);
     d2* Vg2 = reinterpret_cast<d2*>(xb + xl.V);
+    d2* VTg = reinterpret_cast<d2*>(xb + xl.VT);
     const int dp = xl.dp;
     __shared__ QrLds q;
     __shared__ d2 sT[256];
@@ -339,6 +341,18 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
         const int r0 = 16 * p + 16, tt = (dp - r0) >> 4;
         const d2* Vg = Vg2;
         panel_qr(d, 16 * p, r0, dp, C, Vg2, T1 + p * 256, sT, q);
+        {   // V T^H for the back-transform (Z -= V ((V T^H)^H Z): no per-work-group T product there), tile I of
+            // the panel's rows on wave I mod 4: D[i][c] = sum_k V[16 I + i][k] conj(T[c][k])
+            d2* VTp = VTg + (long long)p * dp * 16;
+            for (int I = w; I < tt; I += S1_NW) {
+                Cacc D = cacc0();
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    cmma(D, Vg[(16 * I + lc) * 16 + 4 * s + lr], cconj(sT[lc * 16 + 4 * s + lr]));
+#pragma unroll
+                for (int j4 = 0; j4 < 4; ++j4) VTp[(16 * I + lr + 4 * j4) * 16 + lc] = cget(D, j4);
+            }
+        }
         stamp(0);
         // ---- X = A22 V T for the wave's block rows I = w + 4 h, XG of them at once per block column J (the
         // tiles' operand loads of one J in flight together: the phase is bound by memory round trips)
@@ -521,10 +535,17 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
     auto hstamp = [](int) {};
 #endif
     auto at = [&](int r, int c) -> d2& { return AB[c * ABS + (r - c)]; };   // r >= c
-    auto herm = [&](int r, int c) -> d2 {
-        if (r > c) return AB[c * ABS + (r - c)];
-        if (r < c) return cconj(AB[r * ABS + (c - r)]);
-        return make_double2(AB[c * ABS].x, 0.0);
+    // a read at a clamped (always valid) address, masked afterwards: no branch around the LDS load, so that a
+    // step's reads issue together instead of one wait each
+    auto atm = [&](int r, int c, bool ok) -> d2 {
+        const d2 x = AB[min(c, d - 1) * ABS + min(max(r - c, 0), ABS - 1)];
+        return ok ? x : czero();
+    };
+    auto herm = [&](int r, int c) -> d2 {   // (one LDS read whatever the lane's side of the diagonal)
+        const int lo = min(r, c);
+        d2 a = AB[lo * ABS + abs(r - c)];
+        a.y = r > c ? a.y : (r < c ? -a.y : 0.0);
+        return a;
     };
     // D <- H^H D H on the diagonal block [r0, r0 + len) with v in vb[w] and the lane's entries v[lm + 4 u] in vr
     // (zhetd2's x, w, rank-2 update); lane (row lq, columns lm + 4 u)
@@ -534,10 +555,12 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int cc = lm + 4 * u;
-            if (lq < len && cc < len) xr = cadd(xr, cmul(herm(r0 + lq, r0 + cc), vr[u]));
+            const d2 hv = herm(min(r0 + lq, d - 1), min(r0 + cc, d - 1));
+            if (lq < len && cc < len) xr = cadd(xr, cmul(hv, vr[u]));
         }
         xr = cmul(tau, quad_sum(xr));
-        const d2 vq = lq < len ? vb[w][lq] : czero();
+        d2 vq = vb[w][lq];
+        if (lq >= len) vq = czero();
         d2 pr = (lm == 0 && lq < len) ? cmulc(xr, vq) : czero();
         pr.x = wave_sum_dpp(pr.x);
         pr.y = wave_sum_dpp(pr.y);
@@ -548,12 +571,10 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int cc = lm + 4 * u;
-            if (lq < len && cc <= lq) {
-                d2& a = at(r0 + lq, r0 + cc);
-                d2 x = csub(a, cadd(cmul(vq, cconj(wb[w][cc])), cmul(wr, cconj(vr[u]))));
-                if (cc == lq) x.y = 0.0;
-                a = x;
-            }
+            const d2 av = atm(r0 + lq, r0 + cc, true);   // (unconditional reads, conditional store)
+            d2 x = csub(av, cadd(cmul(vq, cconj(wb[w][cc])), cmul(wr, cconj(vr[u]))));
+            if (cc == lq) x.y = 0.0;
+            if (lq < len && cc <= lq) at(r0 + lq, r0 + cc) = x;
         }
         wave_sync();
     };
@@ -599,7 +620,7 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int cc = lm + 4 * u;
-                    bk[u] = (lq < len2 && cc < len) ? at(s0 + lq, r0 + cc) : czero();
+                    bk[u] = atm(s0 + lq, r0 + cc, lq < len2 && cc < len);
                     y = cadd(y, cmul(bk[u], vr[u]));   // (the previous reflector's entries, kept in registers)
                 }
                 y = cmul(tau, quad_sum(y));
@@ -617,9 +638,9 @@ __global__ __launch_bounds__(S2_THREADS) void hb2st_kernel(int d, double* scratc
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int rr = lm + 4 * u;
-                    xc[u] = rr < len2 ? at(s0 + rr, r0) : czero();
+                    xc[u] = atm(s0 + rr, r0, rr < len2);
                     if (rr >= 1) s += cabs2(xc[u]);
-                    bc[u] = (rr < len2 && lq < len) ? at(s0 + rr, r0 + lq) : czero();
+                    bc[u] = atm(s0 + rr, r0 + lq, rr < len2 && lq < len);
                 }
                 s += bfly16<1>(s);
                 s += bfly16<2>(s);
@@ -809,8 +830,8 @@ __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int 
 }
 
 // Q1 = prod_p (I - V_p T_p V_p^H), the last panel first, on 32 vectors per work-group held in registers in the f64
-// MFMA layout (wave w: row tiles w and w + 8, both 16-vector column tiles); W1 = V_p^H Z is summed over the waves in
-// wave order through LDS.  A panel's V operands (both layouts) are loaded for the next panel while the current one
+// MFMA layout (wave w: row tiles w and w + 8, both 16-vector column tiles); W2 = (V_p T_p^H)^H Z (he2hb stored
+// V_p T_p^H) is summed over the waves in wave order through LDS, then Z -= V_p W2.  A panel's V operands (both layouts) are loaded for the next panel while the current one
 // computes.
 constexpr int Q1_THREADS = 512, Q1_NW = 8, Q1_NV = 32;
 __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int batch, int nc, const double* scratch,
@@ -827,7 +848,7 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
     const int dp = xl.dp, nti = dp >> 4;
     __shared__ d2 sl[Q1_NW][2][256];
     const d2* Cm = reinterpret_cast<const d2*>(base + hl.C);
-    const d2* T1 = reinterpret_cast<const d2*>(xs + (long long)b * xl.stride + xl.T1);
+    const d2* VT = reinterpret_cast<const d2*>(xs + (long long)b * xl.stride + xl.VT);
     d2* Vo = reinterpret_cast<d2*>(Vout) + (long long)b * kmax * d;
     Cacc Z[2][2];
 #pragma unroll
@@ -860,7 +881,7 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
             const bool live = p >= 0 && I >= p + 1 && I < nti;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                if (a) va[h][s] = live ? cconj(vget(p, 16 * I + 4 * s + lr, lc)) : czero();
+                if (a) va[h][s] = live ? cconj(VT[((long long)p * dp + 16 * (I - p - 1) + 4 * s + lr) * 16 + lc]) : czero();
                 if (bb) vb[h][s] = live ? vget(p, 16 * I + lc, 4 * s + lr) : czero();
             }
         }
@@ -877,25 +898,24 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
 #pragma unroll
                 for (int cv = 0; cv < 2; ++cv) cmma(W1[cv], va[h][s], cget(Z[h][cv], s));
         }
-        d2 tw[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) tw[s] = T1[p * 256 + lc * 16 + 4 * s + lr];
 #pragma unroll
         for (int cv = 0; cv < 2; ++cv)
 #pragma unroll
             for (int j4 = 0; j4 < 4; ++j4) sl[w][cv][(lr + 4 * j4) * 16 + lc] = cget(W1[cv], j4);
         lds_barrier();
-        Cacc W2[2] = {cacc0(), cacc0()};
+        // W2 = (V T^H)^H Z = T V^H Z, summed over the waves in wave order (row 4 s + lr of W2 in register s); two
+        // waves' partials per round (all 64 loads at once would not fit the registers)
+        d2 w2[2][4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int kk = 4 * s + lr;
+        for (int cv = 0; cv < 2; ++cv)
 #pragma unroll
-            for (int cv = 0; cv < 2; ++cv) {
-                d2 m = czero();
+            for (int s = 0; s < 4; ++s) w2[cv][s] = czero();
+#pragma unroll 2
+        for (int ww = 0; ww < Q1_NW; ++ww) {
 #pragma unroll
-                for (int ww = 0; ww < Q1_NW; ++ww) m = cadd(m, sl[ww][cv][kk * 16 + lc]);
-                cmma(W2[cv], tw[s], m);
-            }
+            for (int cv = 0; cv < 2; ++cv)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) w2[cv][s] = cadd(w2[cv][s], sl[ww][cv][(4 * s + lr) * 16 + lc]);
         }
         load_v(p - 1, true, false);   // (the next panel's W1 operands: this panel's are used)
 #pragma unroll
@@ -906,7 +926,7 @@ __global__ __launch_bounds__(Q1_THREADS) void bt2q1_kernel(int d, int kmax, int 
             for (int cv = 0; cv < 2; ++cv) {
                 Cacc U = cacc0();
 #pragma unroll
-                for (int s = 0; s < 4; ++s) cmma(U, vb[h][s], cget(W2[cv], s));
+                for (int s = 0; s < 4; ++s) cmma(U, vb[h][s], w2[cv][s]);
                 Z[h][cv].r -= U.r;
                 Z[h][cv].i -= U.i;
             }

@@ -281,9 +281,11 @@ size_t heev2_request_bytes(int d, int which);   // ... of he2hb_kernel (0), hb2s
 //   C[b][i] = epi( sum_k op(L)[i][k] * V[b][k] )   (complex)
 // mode 0: C = acc, 1: C = E - acc, 2: C = E + acc.  conj_l: use conj(L).
 // Batched over `nz` independent problems with strides (complex elements).
+// klim (optional): per z-slice bound on the summation index, read from klim[z * klim_stride] (a double, e.g. the
+// eigensolver's kept count): operand entries at or beyond it must be zero; their K blocks are skipped
 void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
                   const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
-                  long long strideC, int nz, hipStream_t st);
+                  long long strideC, int nz, hipStream_t st, const double* klim = nullptr, long long klim_stride = 0);
 
 // Batched GEMV with a private LHS per realisation: C[b] = epi(L_b V[b]) (rows) or
 // C[b] = epi(L_b^H V[b]) (cols).  L_b = L + b*strideL (complex M x K row-major).

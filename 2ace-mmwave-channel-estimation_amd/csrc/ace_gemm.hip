@@ -218,7 +218,8 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
                                                          const double* __restrict__ E, int ldc, long long strideC,
                                                          int tilesI, int tilesJ, const double* __restrict__ V2,
                                                          const double* __restrict__ E2, const RealState* __restrict__ rs,
-                                                         YsArgs ys = YsArgs{}) {
+                                                         YsArgs ys = YsArgs{}, const double* __restrict__ klim = nullptr,
+                                                         long long klim_stride = 0) {
     constexpr int BJ = CF::BJ, BC = CF::BC, BKC = CF::BKC, NT = CF::NT, TJ = CF::TJ, TC = CF::TC;
     constexpr int VST = CF::VST, LST = CF::LST, PV = CF::PV, PL = CF::PL;
     __shared__ d2 Vs[2][BJ * VST];
@@ -241,6 +242,9 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wj = w / CF::WI, wi = w % CF::WI;
+    // klim (optional): per z-slice bound on the summation index (entries at or beyond it are zero in both operands,
+    // e.g. PhaseLift's assembly over the kept eigenpairs): the K blocks past it are skipped
+    if (klim) K = min(K, max(0, (int)klim[(long long)z * klim_stride]));
     const int ksteps = (K + BKC - 1) / BKC;
 
     d2 vreg[PV], lreg[PL];
@@ -430,13 +434,14 @@ __global__ __launch_bounds__(CF::NT) void zgemm3m_kernel(int M, int K, int nb, c
 template <class CF>
 void launch_zgemm3m_cfg(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
                         const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
-                        long long strideC, int nz, hipStream_t st) {
+                        long long strideC, int nz, hipStream_t st, const double* klim = nullptr,
+                        long long klim_stride = 0) {
     const int tilesI = (M + CF::BC - 1) / CF::BC;
     const int tilesJ = (nb + CF::BJ - 1) / CF::BJ;
     dim3 grid(tilesI * tilesJ, 1, nz), block(CF::NT);
 #define ACE_GEMM_LAUNCH(MD, CJ)                                                                                    \
     hipLaunchKernelGGL((zgemm3m_kernel<MD, CJ, CF>), grid, block, 0, st, M, K, nb, L, ldl, strideL, V, ldv, strideV, \
-                       C, E, ldc, strideC, tilesI, tilesJ, nullptr, nullptr, nullptr)
+                       C, E, ldc, strideC, tilesI, tilesJ, nullptr, nullptr, nullptr, YsArgs{}, klim, klim_stride)
     if (conj_l) {
         if (mode == 0) ACE_GEMM_LAUNCH(0, true);
         else if (mode == 1) ACE_GEMM_LAUNCH(1, true);
@@ -474,7 +479,7 @@ void launch_zgemm_cfg(int mode, bool conj_l, int M, int K, int nb, const double*
 
 void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, int ldl, long long strideL,
                   const double* V, int ldv, long long strideV, double* C, const double* E, int ldc,
-                  long long strideC, int nz, hipStream_t st) {
+                  long long strideC, int nz, hipStream_t st, const double* klim, long long klim_stride) {
     // 3M kernel (measured on MI355X, tools/probe_gemm.hip, unit shapes: apply_A 196 -> 135 us, apply_AH
     // 194 -> 135 us, G/K 52.6 -> 38.4 us against the 4M GemmDefault).  8 waves per work-group; the
     // 64 x 32 output tile when the 64 x 64 one would leave fewer than 512 work-groups.
@@ -482,9 +487,11 @@ void launch_zgemm(int mode, bool conj_l, int M, int K, int nb, const double* L, 
     using Small = Gemm3mCfg<64, 32, 16, 4, 2>;
     const long long big_blocks = (long long)((M + 63) / 64) * ((nb + 63) / 64) * nz;
     if (big_blocks >= 256 && M >= 64)
-        launch_zgemm3m_cfg<Big>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
+        launch_zgemm3m_cfg<Big>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st,
+                                klim, klim_stride);
     else
-        launch_zgemm3m_cfg<Small>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st);
+        launch_zgemm3m_cfg<Small>(mode, conj_l, M, K, nb, L, ldl, strideL, V, ldv, strideV, C, E, ldc, strideC, nz, st,
+                                  klim, klim_stride);
 }
 
 // g = G T with the Y-step in the epilogue (r = 1, shared G).  ys.part: [nb][ceil(m/64)][5].

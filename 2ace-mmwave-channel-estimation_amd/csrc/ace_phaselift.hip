@@ -255,9 +255,10 @@ __global__ __launch_bounds__(256) void pl_assemble_kernel(PlArgs a) {
     // VT[i][q] = V[q][i] (q < k, else 0) and P[i][q] = VT[i][q] (lam_q - tau), by 32 x 32 tiles through LDS: V read
     // along its rows (the element-wise form read V[q][i] down a column), the same values
     __shared__ d2 tv[32][33];
-    const int nt = (d + 31) / 32, cc = t & 31, r0 = t >> 5;
+    // (column tiles past the kept count are all zero and not written: the assembly GEMM sums over q < k only)
+    const int nt = (d + 31) / 32, ntq = (k + 31) / 32, cc = t & 31, r0 = t >> 5;
     for (int I = 0; I < nt; ++I)
-        for (int Q = 0; Q < nt; ++Q) {
+        for (int Q = 0; Q < ntq; ++Q) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int rr = r0 + 8 * u, q = 32 * Q + rr, i = 32 * I + cc;

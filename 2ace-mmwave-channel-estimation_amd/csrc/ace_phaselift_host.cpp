@@ -198,8 +198,9 @@ int solve_batch(const ace_phaselift_cfg* cfg, int batch, int m, int n, const dou
             }
             {
                 ProfScope ps(ACE_K_APPLY_G, st, 8.0 * dd3 * act);   // z = V diag(s) V^H
+                // (summation over the kept pairs only: P's and VT's columns q >= k are zero, misc[0] = k)
                 launch_zgemm(0, true, d, d, d, a.VT, d, (long long)d * d, a.P, d, (long long)d * d, a.Znew, nullptr, d,
-                             (long long)d * d, batch, st);
+                             (long long)d * d, batch, st, a.scratch + a.hl.misc, a.hl.stride);
                 launch_pl_take_z(a, st);
             }
             { ProfScope ps(ACE_K_APPLY_A, st, 8.0 * dd2m * act); applyA(a.z, a.Az); }

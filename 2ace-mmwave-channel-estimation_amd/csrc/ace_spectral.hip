@@ -717,6 +717,38 @@ __device__ bool twisted_vector(const double* d, const double* e, int mt, double 
 // dynamic LDS of trieig_kernel: d, e, e^2 and the eigenvalues (k <= mt), mt doubles each
 size_t trieig_lds(int mt) { return (size_t)mt * 32; }
 
+// A small cluster whose eigenvalues are still apart by TE_TW_GAP ||T|| or more: each vector by the twisted
+// factorization, then orthogonalised against the cluster's earlier ones (modified Gram-Schmidt).  A vector's error is
+// a rotation inside the cluster of angle ~ eps ||T|| / gap, which moves the residual and the prox's projector
+// sum (lam - tau) v v^H only by ~ eps ||T|| (the rotation times the eigenvalue difference).  Closer eigenvalues (or a
+// non-finite vector) return false: the caller's inverse iteration with distinct start vectors runs.
+constexpr int TE_TW_CL = 4;
+constexpr double TE_TW_GAP = 1e-9;
+template <class At>
+__device__ bool twisted_cluster(const double* d, const double* e, int mt, const double* slam, int q0, int q1, double tn,
+                                double tiny, double* Z, At at) {
+    for (int q = q0 + 1; q < q1; ++q)
+        if (fabs(slam[q - 1] - slam[q]) < TE_TW_GAP * tn) return false;
+    for (int q = q0; q < q1; ++q) {
+        double* zq = Z + (long long)q * mt;
+        if (!twisted_vector(d, e, mt, slam[q], tiny, zq, at)) return false;
+        for (int p = q0; p < q; ++p) {
+            const double* zp = Z + (long long)p * mt;
+            double sp = 0.0;
+            for (int i = 0; i < mt; ++i) sp += zp[i] * zq[i];
+            for (int i = 0; i < mt; ++i) zq[i] -= sp * zp[i];
+        }
+        if (q > q0) {
+            double nrm = 0.0;
+            for (int i = 0; i < mt; ++i) nrm += zq[i] * zq[i];
+            if (!(nrm > 0.0 && nrm < INFINITY)) return false;
+            const double inv = 1.0 / sqrt(nrm);
+            for (int i = 0; i < mt; ++i) zq[i] *= inv;
+        }
+    }
+    return true;
+}
+
 // Eigenpairs of the tridiagonal (d, e) (one work-group per realisation): the kmax largest
 // (tau == nullptr) or all eigenvalues above tau[b] (prox_trace, at most kmax), descending.
 // Bisection by Sturm counts to full precision; inverse iteration with the partial-pivoting
@@ -899,6 +931,7 @@ __global__ __launch_bounds__(256) void trieig_kernel(int mt, const double* tau_p
         auto at = [&](int arr, int i) -> double& { return lu[((long long)arr * mt + i) * lay.lanes + ln]; };
         const int q0 = (int)cl[c], q1 = (int)cl[c + 1];
         if (q1 - q0 == 1 && twisted_vector(d, e, mt, lam[q0], tiny, Z + (long long)q0 * mt, at)) continue;
+        if (q1 - q0 <= TE_TW_CL && twisted_cluster(d, e, mt, slam, q0, q1, tn, tiny, Z, at)) continue;
         for (int q = q0; q < q1; ++q) {
             const double lq = lam[q];
             // dgttrf on T - lq I with the running diagonal / superdiagonal entries carried in

@@ -170,11 +170,21 @@ struct VMax {
 
 // wave64 sum with DPP inside the 16-lane rows, one swizzle across the rows of each half, one exchange between the
 // halves (VALU latency for 4 of the 6 steps); another association than wave_sum, every lane gets the same value
+// x + x[lane ^ 16] and x + x[lane ^ 32] by gfx950's row / half-wave swaps (VALU, no LDS round trip): with both
+// operands x, the swap returns the even- and the odd-row (lower- and upper-half) values in every lane, whose sum is
+// the pair's sum in the same order in both lanes of a pair
+__device__ __forceinline__ double xor16_sum(double v) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double xor32_sum(double v) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
 __device__ __forceinline__ double wave_sum_dpp(double v) {
-    v = bsum16(v);
-    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x401F), hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x401F);
-    v += __hiloint2double(hi, lo);
-    return v + __shfl_xor(v, 32, 64);
+    return xor32_sum(xor16_sum(bsum16(v)));
 }
 // block_sum with wave_sum_dpp
 template <int NV>

@@ -140,6 +140,11 @@ __device__ __forceinline__ double row_shr1(double x) {   // lane l <- lane l - 1
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x111, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+__device__ __forceinline__ double ror8(double x) {   // lane l <- lane l ^ 8 (DPP row_ror:8 inside the 16-lane row)
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x128, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x128, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ d2 quad_sum(d2 v) {   // over the 4 lanes of a quad (DPP, identical in every lane)
     v.x += bfly16<1>(v.x);
     v.y += bfly16<1>(v.y);
@@ -211,11 +216,10 @@ __device__ __forceinline__ void panel_qr(int d, int k, int r0, int dp, d2* C, d2
                 d2 a = czero();
 #pragma unroll
                 for (int l = 0; l < 8; ++l) a = cadd(a, tbw[(8 * part + l) * TBS + c8]);
-#pragma unroll
-                for (int o = 8; o < 64; o <<= 1) {
-                    a.x += __shfl_xor(a.x, o, 64);
-                    a.y += __shfl_xor(a.y, o, 64);
-                }
+                a.x += ror8(a.x);   // (the 8 parts: lanes ^ 8, ^ 16, ^ 32)
+                a.y += ror8(a.y);
+                a.x = xor32_sum(xor16_sum(a.x));
+                a.y = xor32_sum(xor16_sum(a.y));
                 if (part == 0) q.wpart[w][8 * hf + c8] = a;
                 wave_sync();
             }

@@ -677,8 +677,8 @@ __global__ __launch_bounds__(PNT) void pgk_kernel(PgkArgs a) {
             if (K == I) {   // end of the tile row: sum the four column quarters
                 racc.x += __shfl_xor(racc.x, 16, 64);
                 racc.y += __shfl_xor(racc.y, 16, 64);
-                racc.x += __shfl_xor(racc.x, 32, 64);
-                racc.y += __shfl_xor(racc.y, 32, 64);
+                racc.x = xor32_sum(racc.x);
+                racc.y = xor32_sum(racc.y);
                 if (q == 0) grow[16 * I + r16] = racc;
             }
         };

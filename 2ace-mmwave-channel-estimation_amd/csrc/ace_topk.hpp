@@ -28,11 +28,13 @@ constexpr int TK_MAX = 16;   // largest profile rank taken this way (32-antenna 
 constexpr int TK_LD = 65;    // LDS stride (doubles) of the per-eigenvalue vectors (spreads the banks)
 constexpr int TK_ONE = 512, TK_ZERO = 513;   // constant slots after the compact reflectors (<= 465 entries)
 // sum over each 32-lane half: DPP within the 16-lane rows, then one swizzle across the two rows
-__device__ __forceinline__ double hsum32(double v) {
-    v = bsum16(v);
-    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), 0x401F);
-    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), 0x401F);
-    return v + __hiloint2double(hi, lo);
+__device__ __forceinline__ double hsum32(double v) {   // (the row pair on a permlane16 swap: VALU, no LDS)
+    return xor16_sum(bsum16(v));
+}
+// lane src's value in every lane (src uniform: v_readlane, no LDS round trip)
+__device__ __forceinline__ double readlane_d(double x, int src) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), src),
+                            __builtin_amdgcn_readlane(__double2loint(x), src));
 }
 template <class Sync>
 __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd, double* ee, double* e2, int n, int K,
@@ -75,7 +77,7 @@ __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd
         }
         sync();
         const d2 x = (i > k && i < n) ? conj_d2(rowb[i]) : zero;   // A[i][k]
-        const double ar = __shfl(x.x, k + 1, 64), ai = __shfl(x.y, k + 1, 64);
+        const double ar = readlane_d(x.x, k + 1), ai = readlane_d(x.y, k + 1);
         const double xn2 = hsum32(i > k + 1 ? cabs2(x) : 0.0);
         d2 tau = zero, sc = zero;
         double beta = ar;
@@ -103,8 +105,8 @@ __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd
             d2 pa = zero;
 #pragma unroll
             for (int t = 0; t < 16; ++t) pa = cadd(pa, cmul(a[t], vsh[c0 + t]));
-            pa.x += __shfl_xor(pa.x, 32, 64);
-            pa.y += __shfl_xor(pa.y, 32, 64);
+            pa.x = xor32_sum(pa.x);
+            pa.y = xor32_sum(pa.y);
             const d2 p = i > k ? cmul(tau, pa) : zero;
             const double pvr = hsum32(p.x * v.x + p.y * v.y), pvi = hsum32(p.x * v.y - p.y * v.x);
             const d2 al = cscale(cmul(tau, make_double2(pvr, pvi)), -0.5);
@@ -265,7 +267,7 @@ __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd
         double dot = 0.0;
 #pragma unroll
         for (int t = 0; t < 16; ++t) dot += cj[c0 + t] * q[t];
-        dot += __shfl_xor(dot, 32, 64);
+        dot = xor32_sum(dot);
         const double td = tq * dot;
 #pragma unroll
         for (int t = 0; t < 16; ++t) q[t] -= cj[c0 + t] * td;
@@ -284,7 +286,7 @@ __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd
             const double rv = (dd[r] - tht) * q[t] + (r > 0 ? ee[r] * qm : 0.0) + (r + 1 < n ? ee[r + 1] * qp : 0.0);
             r2 += r < n ? rv * rv : 0.0;
         }
-        r2 += __shfl_xor(r2, 32, 64);
+        r2 = xor32_sum(r2);
         const double lim = 0x1p-44 * scale;
         if (__any(i < K && !(r2 <= lim * lim))) return false;
     }
@@ -300,8 +302,8 @@ __device__ __forceinline__ bool topk_tri(d2* T0, d2* vsh, double* tk, double* dd
         d2 dot = zero;
 #pragma unroll
         for (int t = 0; t < 16; ++t) dot = cadd(dot, cmulc(VB[vidx(c0 + t)], qc[t]));
-        dot.x += __shfl_xor(dot.x, 32, 64);
-        dot.y += __shfl_xor(dot.y, 32, 64);
+        dot.x = xor32_sum(dot.x);
+        dot.y = xor32_sum(dot.y);
         const d2 td = cmul(tau, dot);
 #pragma unroll
         for (int t = 0; t < 16; ++t) qc[t] = csub(qc[t], cmul(VB[vidx(c0 + t)], td));

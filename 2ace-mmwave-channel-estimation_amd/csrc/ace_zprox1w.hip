@@ -250,8 +250,8 @@ __device__ __forceinline__ bool r1_top(const d2* H, d2* Vb, double* tri, int tx,
             wr += hv.x * v.x - hv.y * v.y;
             wi += hv.x * v.y + hv.y * v.x;
         }
-        wr += __shfl_xor(wr, 32, 64);
-        wi += __shfl_xor(wi, 32, 64);
+        wr = xor32_sum(wr);
+        wi = xor32_sum(wi);
         const double alpha = half_sum(q.x * wr + q.y * wi);   // Re q^H w
         wr -= alpha * q.x + bk * qprev.x;
         wi -= alpha * q.y + bk * qprev.y;

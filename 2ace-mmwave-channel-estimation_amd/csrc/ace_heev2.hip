@@ -6,20 +6,21 @@
 // model of the same index conventions):
 //
 //   he2hb_kernel  stage 1, dense -> band of width 16 (LAPACK zhetrd_he2hb, lower): per panel of 16 columns the
-//                 panel below the band is QR-factored (zgeqr2 in registers, 8 waves), T = zlarft, and the
-//                 trailing matrix takes Q^H A Q as  X = A V T,  W = X - V (T^H V^H X) / 2,  A -= V W^H + W V^H,
-//                 all 16 x 16 complex tiles on v_mfma_f64_16x16x4_f64 (4 real products per complex one); the
-//                 trailing matrix is read twice and written once per panel (d^3 / 48 entries per pass)
+//                 panel below the band is QR-factored (zgeqr2, one panel row per thread in registers, 4 waves),
+//                 T = zlarft, V T^H kept for the back-transform, and the trailing matrix takes Q^H A Q as
+//                 X = A V T,  W = X - V (T^H V^H X) / 2,  A -= V W^H + W V^H, all 16 x 16 complex tiles on
+//                 v_mfma_f64_16x16x4_f64 (4 real products per complex one); the trailing matrix is read twice and
+//                 written once per panel (d^3 / 48 entries per pass); two matrices per CU
 //   hb2st_kernel  stage 2, band -> real symmetric tridiagonal by bulge chasing (Householder reflectors of length
 //                 <= 16; each chase step right-applies the previous reflector to the block below it, annihilates
 //                 the first column of the bulge and applies the new reflector to the next diagonal block), the
 //                 band in LDS; sweep i runs on wave i mod 8, 2 steps behind sweep i - 1, so that 8 sweeps are in
 //                 flight on disjoint footprints (the same arithmetic as one sweep after the other)
 //   trieig_kernel (ace_spectral.hip) the eigenpairs of the tridiagonal above tau
-//   bt2q2_kernel  back-transform through the stage-2 reflectors: 64 eigenvectors per work-group, each in the
+//   bt2q2_kernel  back-transform through the stage-2 reflectors: 32 eigenvectors per work-group, each in the
 //                 registers of 16 lanes, reflectors applied in a lag-pipelined order that needs no barrier
-//   bt2q1_kernel  back-transform through the stage-1 blocks Z -= V (T (V^H Z)) on the matrix cores, 16 vectors per
-//                 work-group in registers
+//   bt2q1_kernel  back-transform through the stage-1 blocks Z -= V ((V T^H)^H Z) on the matrix cores, 32 vectors
+//                 per work-group in registers
 //
 // Matrices whose order is not a multiple of 16 are handled as if zero-padded to dp = 16 ceil(d / 16): the padded
 // rows and columns stay exactly zero through stage 1 (masked loads and stores), stage 2 and the tridiagonal run on
@@ -36,7 +37,7 @@ namespace ace {
 namespace {
 
 constexpr int H2_MAXD = 256;
-// stage 1: 4 waves per matrix, two matrices per CU (LDS 77 KB, <= 256 VGPRs each): one matrix's serial panel QR
+// stage 1: 4 waves per matrix, two matrices per CU (LDS 47 KB, <= 256 VGPRs each): one matrix's serial panel QR
 // overlaps the other's MFMA phases; wave w owns the trailing matrix's block rows w + 4 h (h < S1_NH)
 constexpr int S1_THREADS = 256, S1_NW = S1_THREADS / 64, S1_NH = (H2_MAXD / 16 + S1_NW - 1) / S1_NW;
 constexpr int S2_THREADS = 512, S2_NW = S2_THREADS / 64;
@@ -49,7 +50,8 @@ constexpr int S2_LAG = 2;
 // accesses both spread over the banks (with 33, c + r became r: 16-way conflicts on the column-wise ones)
 constexpr int ABS = 34;
 
-// per-realisation extra scratch (doubles): T of the stage-1 panels [np][16][16], the panel's W [dp][16] and V,
+// per-realisation extra scratch (doubles): T of the stage-1 panels [np][16][16], the panel's W [dp][16] and V, V T^H
+// of every panel,
 // the stage-2 reflectors (v[16], tau) of sweep i, step j at [ts][r][j] with the back-transform's time step
 // ts = d - 2 - i + j (q2_index): the 16 step lanes of a time step read 16 consecutive entries per element r
 struct H2Lay {
@@ -65,7 +67,7 @@ H2Lay h2lay(int d) {
     auto take = [&](long long nd) { long long p = o; o += (nd + 31) & ~31LL; return p; };
     x.T1 = take(2LL * std::max(1, x.np) * 256);
     x.W = take(2LL * x.dp * 16);
-    x.V = take(2LL * 2 * x.dp * 16);   // the stage-1 panel's V [2][dp][16] (double-buffered: look-ahead QR)
+    x.V = take(2LL * x.dp * 16);   // the stage-1 panel's V [dp][16]
     x.VT = take(2LL * std::max(1, x.np) * x.dp * 16);   // V_p T_p^H per panel [np][dp][16] (rows from the panel's r0)
     x.Q2 = take(2LL * (d + 14) * 17 * 16);
     x.stride = o;

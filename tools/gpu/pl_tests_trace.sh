@@ -1,6 +1,8 @@
+# The eigensolver / PhaseLift / spectral / pipeline GPU tests, then a kernel trace of the 200-iteration PhaseLift
+# bench step with per-kernel totals (development loop of the prox eigensolver, r06).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/h2m; mkdir -p $O
+O=gpurun_out/pl_trace; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_heev2.py tests/test_gpu_phaselift.py tests/test_gpu_spectral.py tests/test_gpu_pipeline.py -x -q --timeout 300 --timeout-method thread > $O/t1.log 2>&1; rc=$?
 tail -3 $O/t1.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $O/t1.log | head -20; exit 1; }
@@ -8,7 +10,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/pl -o run --output-form
 grep -h '"metric"' $O/pl.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('phaselift', d['value'], d['ms_per_step'])"
 python3 - <<'PY'
 import csv, collections
-rows = list(csv.DictReader(open('gpurun_out/h2m/pl/run_kernel_trace.csv')))
+rows = list(csv.DictReader(open('gpurun_out/pl_trace/pl/run_kernel_trace.csv')))
 by = collections.defaultdict(list)
 for r in rows:
     by[r['Kernel_Name'][:40]].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)
@@ -17,7 +19,7 @@ for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1]))[:7]:
 PY
 rm -rf $O/pl
 python3 - <<'PY'
-L = open('gpurun_out/h2m/stamps.log').read().splitlines()
+L = open('gpurun_out/pl_trace/stamps.log').read().splitlines()
 rows = [l for l in L if l.startswith('trieig')]
 print('trieig', len(rows))
 for l in rows[:3] + rows[len(rows)//2:len(rows)//2+3] + rows[-3:]:

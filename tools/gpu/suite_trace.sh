@@ -1,6 +1,7 @@
+# The full GPU suite, a PhaseLift kernel trace and a short unit bench (r06).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/h2p; mkdir -p $O
+O=gpurun_out/suite_trace; mkdir -p $O
 timeout -k 10 1500 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests > $O/t1.log 2>&1; rc=$?
 tail -3 $O/t1.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $O/t1.log | head -20; exit 1; }
@@ -8,7 +9,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/pl -o run --output-form
 grep -h '"metric"' $O/pl.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('phaselift', d['value'], d['ms_per_step'])"
 python3 - <<'PY'
 import csv, collections
-rows = list(csv.DictReader(open('gpurun_out/h2p/pl/run_kernel_trace.csv')))
+rows = list(csv.DictReader(open('gpurun_out/suite_trace/pl/run_kernel_trace.csv')))
 by = collections.defaultdict(list)
 for r in rows:
     by[r['Kernel_Name'][:40]].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)

@@ -377,25 +377,38 @@ __global__ __launch_bounds__(S1_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
             Cacc Y[XG];
 #pragma unroll
             for (int h = 0; h < XG; ++h) Y[h] = cacc0();
-            for (int J = 0; J < tt; ++J) {
-                d2 bv[4], a[XG][4];
+            // operands of block column J + 1 loaded while J multiplies (the last round re-loads J: clamped index,
+            // no conditional load)
+            d2 bv[4], a[XG][4];
+            auto load_j = [&](int J, d2 (&bo)[4], d2 (&ao)[XG][4]) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) bv[s] = Vg[(16 * J + 4 * s + lr) * 16 + lc];
+                for (int s = 0; s < 4; ++s) bo[s] = Vg[(16 * J + 4 * s + lr) * 16 + lc];
 #pragma unroll
                 for (int h = 0; h < XG; ++h) {
                     const int I = w + S1_NW * (h0 + h);
 #pragma unroll
                     for (int s = 0; s < 4; ++s) {
                         const d2 x = lda(min(I, tt - 1), J, s);
-                        a[h][s] = I < tt ? x : czero();
+                        ao[h][s] = I < tt ? x : czero();
                     }
                 }
+            };
+            load_j(0, bv, a);
+            for (int J = 0; J < tt; ++J) {
+                d2 bn[4], an[XG][4];
+                load_j(min(J + 1, tt - 1), bn, an);
 #pragma unroll
                 for (int h = 0; h < XG; ++h)
                     if (w + S1_NW * (h0 + h) < tt) {
 #pragma unroll
                         for (int s = 0; s < 4; ++s) cmma(Y[h], a[h][s], bv[s]);
                     }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) bv[s] = bn[s];
+#pragma unroll
+                for (int h = 0; h < XG; ++h)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) a[h][s] = an[h][s];
             }
 #pragma unroll
             for (int h = 0; h < XG; ++h) {

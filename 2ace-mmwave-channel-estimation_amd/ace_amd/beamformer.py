@@ -48,17 +48,30 @@ class BeamResult:
     beam_idx: object  # [batch][2] int32 (tx_idx, rx_idx)
     rss: object       # [batch] float64 (dB of the winning pair)
     status: object    # [batch] uint32 (ACE_ST_BF_*)
-    vh_r: object = None  # [batch][n][n] complex128 Vh of svd(H)   (optional)
-    vh_t: object = None  # [batch][n][n] complex128 Vh of svd(H^T) (optional)
+    vh_r: object = None  # [batch][rx][rx] complex128 Vh of svd(H)   (optional)
+    vh_t: object = None  # [batch][tx][tx] complex128 Vh of svd(H^T) (optional)
 
 
 def _codes_str(c):
     return "".join(chr(48 + int(x)) for x in c)
 
 
+def _offset_len(offset, tx, rx):
+    """Length of the per-realisation offset row.  The reference multiplies wr (rx entries) and wt (tx
+    entries) by the same ``exp(-1j * offset)`` (codebook_library.py:122, :129), so the row must broadcast
+    against both, as numpy requires: a constant, or max(tx, rx) entries when tx == rx."""
+    shp = np.shape(offset)
+    L = shp[-1] if len(shp) else 1
+    if L != 1 and (L != rx or L != tx):
+        raise ValueError(f"operands could not be broadcast together: offset of length {L} against "
+                         f"wr ({rx},) and wt ({tx},)")
+    return L
+
+
 def svd_beamformer_host(H, offset=None, want_vh=False) -> BeamResult:
-    """Batch of svd_beamformer(_compensation) on host arrays.  H [batch][tx][rx] complex;
-    offset None or [batch][rx] / [rx] radians."""
+    """Batch of svd_beamformer(_compensation) on host arrays.  H [batch][tx][rx] complex (1..32
+    antennas each side, tx != rx allowed); offset None, or radians per realisation ([batch][L] / [L] /
+    scalar) with L = rx = tx or L = 1 (the C-ABI row is max(tx, rx) entries)."""
     H = np.ascontiguousarray(np.asarray(H, dtype=np.complex128))
     if H.ndim == 2:
         H = H[None]
@@ -67,13 +80,16 @@ def svd_beamformer_host(H, offset=None, want_vh=False) -> BeamResult:
     batch, tx, rx = H.shape
     off = None
     if offset is not None:
-        off = np.ascontiguousarray(np.broadcast_to(np.asarray(offset, dtype=np.float64), (batch, rx)))
+        L = _offset_len(offset, tx, rx)
+        o = np.asarray(offset, dtype=np.float64).reshape(-1, L)
+        off = np.ascontiguousarray(np.broadcast_to(o, (batch, L)))
+        off = np.ascontiguousarray(np.broadcast_to(off, (batch, max(tx, rx))))
     wr = np.empty((batch, rx), np.uint8)
     wt = np.empty((batch, tx), np.uint8)
     idx = np.empty((batch, 2), np.int32)
     rss = np.empty(batch, np.float64)
     st = np.empty(batch, np.uint32)
-    vr = np.empty((batch, tx, tx), np.complex128) if want_vh else None
+    vr = np.empty((batch, rx, rx), np.complex128) if want_vh else None
     vt = np.empty((batch, tx, tx), np.complex128) if want_vh else None
     f64 = lambda a: None if a is None else a.view(np.float64).ctypes.data_as(_dp)  # noqa: E731
     check(LIB.ace_svd_beamformer_host(batch, tx, rx, f64(H), None if off is None else off.ctypes.data_as(_dp),
@@ -84,7 +100,8 @@ def svd_beamformer_host(H, offset=None, want_vh=False) -> BeamResult:
 
 
 def svd_beamformer_batch(H, offset=None, *, want_vh=False, stream=None) -> BeamResult:
-    """Batch on device tensors: H [batch][tx][rx] complex128, offset None or [batch][rx] f64."""
+    """Batch on device tensors: H [batch][tx][rx] complex128, offset None or [batch][L] / [L] f64 (L as
+    in svd_beamformer_host)."""
     import torch
     if not H.is_cuda:
         raise ValueError("svd_beamformer_batch needs device tensors")
@@ -92,13 +109,15 @@ def svd_beamformer_batch(H, offset=None, *, want_vh=False, stream=None) -> BeamR
     batch, tx, rx = H.shape
     dev = H.device
     if offset is not None:
-        offset = offset.to(device=dev, dtype=torch.float64).expand(batch, rx).contiguous()
+        L = _offset_len(offset, tx, rx)
+        offset = offset.to(device=dev, dtype=torch.float64).reshape(-1, L).expand(batch, L)
+        offset = offset.expand(batch, max(tx, rx)).contiguous()
     out = BeamResult(torch.empty((batch, rx), dtype=torch.uint8, device=dev),
                      torch.empty((batch, tx), dtype=torch.uint8, device=dev),
                      torch.empty((batch, 2), dtype=torch.int32, device=dev),
                      torch.empty(batch, dtype=torch.float64, device=dev),
                      torch.empty(batch, dtype=torch.int32, device=dev),
-                     torch.empty((batch, tx, tx), dtype=torch.complex128, device=dev) if want_vh else None,
+                     torch.empty((batch, rx, rx), dtype=torch.complex128, device=dev) if want_vh else None,
                      torch.empty((batch, tx, tx), dtype=torch.complex128, device=dev) if want_vh else None)
     if stream is None:
         stream = torch.cuda.current_stream(dev)
@@ -139,9 +158,10 @@ def codebook_beams(H_est, H_directional, num_tx_ant, num_rx_ant,
     Hs = np.concatenate([H_est, H_dir]).reshape(-1, num_tx_ant, num_rx_ant)
     if len(Hs) == 0:
         return [], []
-    off = np.zeros((len(Hs), num_rx_ant))
+    comp = np.asarray(compensation, dtype=np.float64) * (np.pi / 2)
+    off = np.zeros((len(Hs), _offset_len(comp, num_tx_ant, num_rx_ant) if len(H_est) else 1))
     if len(H_est):
-        off[0] = np.asarray(compensation, dtype=np.float64) * (np.pi / 2)
+        off[0] = comp
     res = svd_beamformer_host(Hs, off)
     if np.any(res.status & ACE_ST_BF_NONFINITE):
         raise LinAlgError("SVD did not converge")

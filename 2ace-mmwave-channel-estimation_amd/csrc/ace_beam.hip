@@ -15,8 +15,10 @@
 //   search     T = H wr (exact +-1/+-j multipliers), M = wt^T T, argmax over lanes
 //
 // For n <= 25 this is zgesdd's path (dbdsdc -> dlasdq -> dbdsqr).  For 26..32 numpy's
-// zgesdd uses divide and conquer, whose real singular-vector signs can differ: the status
-// bit ACE_ST_BF_DC marks those realisations (the beam is the same up to a global sign).
+// zgesdd uses divide and conquer (dlasd0: two dlasdq leaves and one dlasd1 merge), whose real
+// singular vectors equal dbdsqr's up to sign; the merge's sign convention is applied after
+// dbdsqr (gesdd_vh).  The status bit ACE_ST_BF_DC marks those realisations: a vector the merge
+// deflated (the null space of a rank-deficient H) can still differ from numpy's.
 #include "ace_common.hpp"
 #include "ace_host.hpp"
 
@@ -170,30 +172,29 @@ struct BfShared {  // per-wave LDS carve (one realisation per block)
     double* d;   // [BF_NMAX] bidiagonal
     double* e;   // [BF_NMAX]
     d2* taup;    // [BF_NMAX]
-    signed char* qr;  // [n][n] quantised phases of Vh(H)   (around(angle/(pi/2)), -2..2)
-    signed char* qt;  // [n][n] quantised phases of Vh(H^T)
+    d2* Q;       // [N][ld] zgelq2's H(1) ... H(m) (tx != rx only)
+    signed char* qr;  // [rx][rx] quantised phases of Vh(H)   (around(angle/(pi/2)), -2..2)
+    signed char* qt;  // [tx][tx] quantised phases of Vh(H^T)
 };
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // block == one wavefront
 
-// Vh of zgesdd(M) for the n x n matrix loaded in sh.A; result in sh.X.  Returns false when
-// dbdsqr exhausted its iteration budget.
-__device__ bool gesdd_vh(const BfShared& sh, int n, int ld, int lane) {
+// zgebd2 for m >= n (upper bidiagonal d [n], e [n - 1]) of the m x n matrix in sh.A: the column reflectors'
+// tails stay below the diagonal, G(i) (i < n - 1) acts on columns i + 1 .. n - 1 with its tail in A[i][i + 2 ..]
+__device__ void zgebd2_upper(const BfShared& sh, int m, int n, int ld, int lane) {
     d2* A = sh.A;
-    d2* X = sh.X;
     double* dd = sh.d;
     double* ee = sh.e;
-    // ---------------- zgebd2 (m == n: upper bidiagonal)
     for (int i = 0; i < n; ++i) {
         // column reflector H(i) annihilating A(i+1:n, i)
         double part = 0.0;
-        if (lane > i && lane < n) part = cabs2(A[lane * ld + i]);
+        if (lane > i && lane < m) part = cabs2(A[lane * ld + i]);
         const double xnorm = sqrt(wave_sum(part));
         double beta;
         d2 tauq, scal;
         zlarfg(A[i * ld + i], xnorm, beta, tauq, scal);
         wsync();
-        if (lane > i && lane < n) A[lane * ld + i] = cmul(A[lane * ld + i], scal);
+        if (lane > i && lane < m) A[lane * ld + i] = cmul(A[lane * ld + i], scal);
         dd[i] = beta;
         wsync();
         if (i < n - 1) {
@@ -201,10 +202,10 @@ __device__ bool gesdd_vh(const BfShared& sh, int n, int ld, int lane) {
             if (lane > i && lane < n) {
                 const int c = lane;
                 d2 w = A[i * ld + c];
-                for (int r = i + 1; r < n; ++r) w = cadd(w, cmulc(A[r * ld + i], A[r * ld + c]));
+                for (int r = i + 1; r < m; ++r) w = cadd(w, cmulc(A[r * ld + i], A[r * ld + c]));
                 const d2 tw = cmul(cconj(tauq), w);
                 A[i * ld + c] = csub(A[i * ld + c], tw);
-                for (int r = i + 1; r < n; ++r) A[r * ld + c] = csub(A[r * ld + c], cmul(A[r * ld + i], tw));
+                for (int r = i + 1; r < m; ++r) A[r * ld + c] = csub(A[r * ld + c], cmul(A[r * ld + i], tw));
             }
             wsync();
             // row reflector G(i) annihilating A(i, i+2:n) (on the conjugated row)
@@ -219,8 +220,8 @@ __device__ bool gesdd_vh(const BfShared& sh, int n, int ld, int lane) {
             ee[i] = beta2;
             sh.taup[i] = taup;
             wsync();
-            // A(i+1:n, i+1:n) := A G(i), G = I - taup v v^H; lane = row
-            if (lane > i && lane < n) {
+            // A(i+1:m, i+1:n) := A G(i), G = I - taup v v^H; lane = row
+            if (lane > i && lane < m) {
                 const int r = lane;
                 d2 w = A[r * ld + i + 1];
                 for (int c = i + 2; c < n; ++c) w = cadd(w, cmul(A[r * ld + c], A[i * ld + c]));
@@ -231,15 +232,28 @@ __device__ bool gesdd_vh(const BfShared& sh, int n, int ld, int lane) {
             wsync();
         }
     }
+}
+
+// Right singular vectors of the real upper bidiagonal (sh.d, sh.e) of order n into VT = sh.X [nc][nc] (nc >= n:
+// rows and columns >= n stay the identity's), zgesdd's sign convention included.  Returns false when dbdsqr
+// exhausted its iteration budget.
+__device__ bool bd_vt(const BfShared& sh, int n, int nc, int ld, int lane) {
+    d2* X = sh.X;
+    double* dd = sh.d;
+    double* ee = sh.e;
     // ---------------- VT := I (real parts of X)
-    if (lane < n)
-        for (int r = 0; r < n; ++r) X[r * ld + lane] = make_double2(r == lane ? 1.0 : 0.0, 0.0);
+    if (lane < nc)
+        for (int r = 0; r < nc; ++r) X[r * ld + lane] = make_double2(r == lane ? 1.0 : 0.0, 0.0);
     wsync();
     bool ok = true;
+    // divide and conquer (n > 25): the bidiagonal's row n / 2 (dlasdt's root, dlasd0's merge row) before dbdsqr
+    // overwrites it
+    const int mid = n / 2;
+    const double dmid = n > BF_SMLSIZ ? dd[mid] : 0.0, emid = n > BF_SMLSIZ ? ee[mid] : 0.0;
     if (n > 1) {
         // ---------------- dbdsqr (ncvt = n, relative accuracy); 1-based m/ll as in LAPACK
         const double tol = bd_tol();
-        const bool col = lane < n;
+        const bool col = lane < nc;
         auto rot = [&](int i, double c, double s) {  // drot on VT rows i, i+1 (0-based)
             if (col) {
                 const double x = X[i * ld + lane].x, y = X[(i + 1) * ld + lane].x;
@@ -432,20 +446,256 @@ __device__ bool gesdd_vh(const BfShared& sh, int n, int ld, int lane) {
             }
         }
         wsync();
-        // ---------------- Vh = VT * P^H = VT G(n-1)^H ... G(1)^H; lane = row
-        if (lane < n) {
+        if (n > BF_SMLSIZ && lane < n) {
+            // zgesdd's dbdsdc (n > SMLSIZ = 25) -> dlasd0: one merge at row mid of the leaves [0, mid) (dlasdq on
+            // mid x (mid + 1)) and (mid, n) (dlasdq on the rest), dlasd1 -> dlasd3 builds every non-deflated left
+            // vector with its merge-row component -1 / ||.|| (dlasd3: U(1, i) = -1, the first deflated coordinate being
+            // that row).  The vectors equal dbdsqr's up to sign, so row i of VT flips where u_i(mid) =
+            // (d_mid v_i(mid) + e_mid v_i(mid + 1)) / s_i > 0.  Deflated vectors (z_j below 64 eps: a subproblem
+            // vector with no merge-row component, e.g. the null space of an exactly rank-deficient H) keep the sign
+            // of the leaf's own dbdsqr, which is not reproduced (nor is the basis of a degenerate null space): those
+            // are what ACE_ST_BF_DC still flags
             const int r = lane;
-            for (int i = n - 2; i >= 0; --i) {
-                const d2 ctp = cconj(sh.taup[i]);
-                d2 w = X[r * ld + i + 1];
-                for (int c = i + 2; c < n; ++c) w = cadd(w, cmul(X[r * ld + c], A[i * ld + c]));
-                const d2 tw = cmul(ctp, w);
-                X[r * ld + i + 1] = csub(X[r * ld + i + 1], tw);
-                for (int c = i + 2; c < n; ++c) X[r * ld + c] = csub(X[r * ld + c], cmul(tw, cconj(A[i * ld + c])));
-            }
+            const double um = dmid * X[r * ld + mid].x + emid * X[r * ld + mid + 1].x;
+            if (um > 0.0)
+                for (int c = 0; c < n; ++c) X[r * ld + c].x = -X[r * ld + c].x;
         }
         wsync();
     }
+    return ok;
+}
+
+// Vh := VT P^H = VT G(k-1)^H ... G(0)^H on VT = sh.X [nc][nc]; G(i) acts on columns c0 = i + off .. nc - 1 with
+// the leading 1 at c0 and its tail in A[i][c0 + 1 ..] (off = 1: zgebd2 upper, 0: lower); lane = row
+__device__ void apply_ph(const BfShared& sh, int nc, int k, int off, int ld, int lane) {
+    const d2* A = sh.A;
+    d2* X = sh.X;
+    if (lane < nc) {
+        const int r = lane;
+        for (int i = k - 1; i >= 0; --i) {
+            const int c0 = i + off;
+            const d2 ctp = cconj(sh.taup[i]);
+            d2 w = X[r * ld + c0];
+            for (int c = c0 + 1; c < nc; ++c) w = cadd(w, cmul(X[r * ld + c], A[i * ld + c]));
+            const d2 tw = cmul(ctp, w);
+            X[r * ld + c0] = csub(X[r * ld + c0], tw);
+            for (int c = c0 + 1; c < nc; ++c) X[r * ld + c] = csub(X[r * ld + c], cmul(tw, cconj(A[i * ld + c])));
+        }
+    }
+    wsync();
+}
+
+// zgebd2 for m < n (lower bidiagonal d [m], e [m - 1]): G(i) on the conjugated row A(i, i:n) (columns i .. n - 1,
+// tail in A[i][i + 1 ..]), then H(i) annihilating A(i + 2:m, i)
+__device__ void zgebd2_lower(const BfShared& sh, int m, int n, int ld, int lane) {
+    d2* A = sh.A;
+    double* dd = sh.d;
+    double* ee = sh.e;
+    for (int i = 0; i < m; ++i) {
+        double p2 = 0.0;
+        if (lane > i && lane < n) p2 = cabs2(A[i * ld + lane]);
+        const double xn2 = sqrt(wave_sum(p2));
+        double beta;
+        d2 taup, scal;
+        zlarfg(cconj(A[i * ld + i]), xn2, beta, taup, scal);
+        wsync();
+        if (lane > i && lane < n) A[i * ld + lane] = cmul(cconj(A[i * ld + lane]), scal);  // v tail
+        dd[i] = beta;
+        sh.taup[i] = taup;
+        wsync();
+        if (i == m - 1) break;
+        // A(i+1:m, i:n) := A G(i); lane = row
+        if (lane > i && lane < m) {
+            const int r = lane;
+            d2 w = A[r * ld + i];
+            for (int c = i + 1; c < n; ++c) w = cadd(w, cmul(A[r * ld + c], A[i * ld + c]));
+            const d2 tw = cmul(taup, w);
+            A[r * ld + i] = csub(A[r * ld + i], tw);
+            for (int c = i + 1; c < n; ++c) A[r * ld + c] = csub(A[r * ld + c], cmul(tw, cconj(A[i * ld + c])));
+        }
+        wsync();
+        // H(i) annihilating A(i+2:m, i)
+        double part = 0.0;
+        if (lane > i + 1 && lane < m) part = cabs2(A[lane * ld + i]);
+        const double xnorm = sqrt(wave_sum(part));
+        double beta2;
+        d2 tauq, scal2;
+        zlarfg(A[(i + 1) * ld + i], xnorm, beta2, tauq, scal2);
+        wsync();
+        if (lane > i + 1 && lane < m) A[lane * ld + i] = cmul(A[lane * ld + i], scal2);
+        ee[i] = beta2;
+        wsync();
+        // A(i+1:m, i+1:n) := H(i)^H A; lane = column
+        if (lane > i && lane < n) {
+            const int c = lane;
+            d2 w = A[(i + 1) * ld + c];
+            for (int r = i + 2; r < m; ++r) w = cadd(w, cmulc(A[r * ld + i], A[r * ld + c]));
+            const d2 tw = cmul(cconj(tauq), w);
+            A[(i + 1) * ld + c] = csub(A[(i + 1) * ld + c], tw);
+            for (int r = i + 2; r < m; ++r) A[r * ld + c] = csub(A[r * ld + c], cmul(A[r * ld + i], tw));
+        }
+        wsync();
+    }
+}
+
+// zgeqr2 (m > n): R in A[0:n][0:n], zero below the diagonal
+__device__ void zgeqr2_r(const BfShared& sh, int m, int n, int ld, int lane) {
+    d2* A = sh.A;
+    for (int i = 0; i < n; ++i) {
+        double part = 0.0;
+        if (lane > i && lane < m) part = cabs2(A[lane * ld + i]);
+        const double xnorm = sqrt(wave_sum(part));
+        double beta;
+        d2 tau, scal;
+        zlarfg(A[i * ld + i], xnorm, beta, tau, scal);
+        wsync();
+        if (lane > i && lane < m) A[lane * ld + i] = cmul(A[lane * ld + i], scal);
+        wsync();
+        if (lane > i && lane < n) {  // A(i:m, i+1:n) := H(i)^H A; lane = column
+            const int c = lane;
+            d2 w = A[i * ld + c];
+            for (int r = i + 1; r < m; ++r) w = cadd(w, cmulc(A[r * ld + i], A[r * ld + c]));
+            const d2 tw = cmul(cconj(tau), w);
+            A[i * ld + c] = csub(A[i * ld + c], tw);
+            for (int r = i + 1; r < m; ++r) A[r * ld + c] = csub(A[r * ld + c], cmul(A[r * ld + i], tw));
+        }
+        wsync();
+        if (lane == 0) A[i * ld + i] = make_double2(beta, 0.0);
+        wsync();
+    }
+    if (lane < n)
+        for (int r = lane + 1; r < n; ++r) A[r * ld + lane] = make_double2(0.0, 0.0);
+    wsync();
+}
+
+// zgelq2 (m < n): L in A[0:m][0:m] (zero above the diagonal), sh.Q [n][n] := H(1) H(2) ... H(m), so that
+// zunglq's Q = sh.Q^H (A = L Q[0:m])
+__device__ void zgelq2_lq(const BfShared& sh, int m, int n, int ld, int lane) {
+    d2* A = sh.A;
+    d2* Qh = sh.Q;
+    if (lane < n)
+        for (int r = 0; r < n; ++r) Qh[r * ld + lane] = make_double2(r == lane ? 1.0 : 0.0, 0.0);
+    for (int i = 0; i < m; ++i) {
+        double p2 = 0.0;
+        if (lane > i && lane < n) p2 = cabs2(A[i * ld + lane]);
+        const double xn2 = sqrt(wave_sum(p2));
+        double beta;
+        d2 tau, scal;
+        zlarfg(cconj(A[i * ld + i]), xn2, beta, tau, scal);
+        wsync();
+        if (lane > i && lane < n) A[i * ld + lane] = cmul(cconj(A[i * ld + lane]), scal);  // v tail
+        wsync();
+        // A(i+1:m, i:n) := A H(i) and Qh(:, i:n) := Qh H(i); lane = row
+        if (lane > i && lane < m) {
+            const int r = lane;
+            d2 w = A[r * ld + i];
+            for (int c = i + 1; c < n; ++c) w = cadd(w, cmul(A[r * ld + c], A[i * ld + c]));
+            const d2 tw = cmul(tau, w);
+            A[r * ld + i] = csub(A[r * ld + i], tw);
+            for (int c = i + 1; c < n; ++c) A[r * ld + c] = csub(A[r * ld + c], cmul(tw, cconj(A[i * ld + c])));
+        }
+        if (lane < n) {
+            const int r = lane;
+            d2 w = Qh[r * ld + i];
+            for (int c = i + 1; c < n; ++c) w = cadd(w, cmul(Qh[r * ld + c], A[i * ld + c]));
+            const d2 tw = cmul(tau, w);
+            Qh[r * ld + i] = csub(Qh[r * ld + i], tw);
+            for (int c = i + 1; c < n; ++c) Qh[r * ld + c] = csub(Qh[r * ld + c], cmul(tw, cconj(A[i * ld + c])));
+        }
+        wsync();
+        if (lane == 0) A[i * ld + i] = make_double2(beta, 0.0);
+        wsync();
+    }
+    if (lane < m)
+        for (int c = lane + 1; c < m; ++c) A[lane * ld + c] = make_double2(0.0, 0.0);
+    wsync();
+}
+
+// Vh of zgesdd(JOBZ='A') for the square n x n matrix in sh.A, into sh.X
+__device__ bool gesdd_vh_square(const BfShared& sh, int n, int ld, int lane) {
+    zgebd2_upper(sh, n, n, ld, lane);
+    if (n == 1) {
+        if (lane == 0) sh.X[0] = make_double2(1.0, 0.0);  // dbdsdc n == 1: VT = 1
+        wsync();
+        return true;
+    }
+    const bool ok = bd_vt(sh, n, n, ld, lane);
+    apply_ph(sh, n, n - 1, 1, ld, lane);
+    return ok;
+}
+
+// Vh [n][n] of zgesdd(JOBZ='A') for the m x n matrix in sh.A, into sh.X (m, n <= 32), following zgesdd's
+// path choice (MNTHR1 = INT(MINMN * 17 / 9)): QR first for m >= MNTHR1 (paths 1-4), LQ first for n >= MNTHR1
+// (paths 1t-4t), the matrix itself otherwise (paths 5/6, 5t/6t: upper / lower bidiagonal)
+__device__ bool gesdd_vh(const BfShared& sh, int m, int n, int ld, int lane) {
+    if (n == 1) {
+        if (lane == 0) sh.X[0] = make_double2(1.0, 0.0);
+        wsync();
+        return true;
+    }
+    if (m == n) return gesdd_vh_square(sh, n, ld, lane);
+    const int mnthr1 = (int)(min(m, n) * 17.0 / 9.0);
+    if (m > n && m >= mnthr1) {
+        zgeqr2_r(sh, m, n, ld, lane);
+        return gesdd_vh_square(sh, n, ld, lane);
+    }
+    if (n > m && n >= mnthr1) {
+        zgelq2_lq(sh, m, n, ld, lane);
+        const bool ok = gesdd_vh_square(sh, m, ld, lane);
+        // VT = [Vh_L Q[0:m]; Q[m:n]], Q = Qh^H; built in A, then copied to X; lane = column
+        d2* A = sh.A;
+        d2* X = sh.X;
+        const d2* Qh = sh.Q;
+        if (lane < n) {
+            const int c = lane;
+            for (int r = 0; r < m; ++r) {
+                d2 acc = make_double2(0.0, 0.0);
+                for (int k = 0; k < m; ++k) acc = cadd(acc, cmul(X[r * ld + k], cconj(Qh[c * ld + k])));
+                A[r * ld + c] = acc;
+            }
+            for (int r = m; r < n; ++r) A[r * ld + c] = cconj(Qh[c * ld + r]);
+        }
+        wsync();
+        if (lane < n)
+            for (int r = 0; r < n; ++r) X[r * ld + lane] = A[r * ld + lane];
+        wsync();
+        return ok;
+    }
+    if (m > n) {
+        zgebd2_upper(sh, m, n, ld, lane);
+        const bool ok = bd_vt(sh, n, n, ld, lane);
+        apply_ph(sh, n, n - 1, 1, ld, lane);
+        return ok;
+    }
+    zgebd2_lower(sh, m, n, ld, lane);
+    bool ok = true;
+    if (m == 1) {
+        if (lane < n)
+            for (int r = 0; r < n; ++r) sh.X[r * ld + lane] = make_double2(r == lane ? 1.0 : 0.0, 0.0);
+        wsync();
+    } else {
+        // dbdsdc('L'): rotate to upper bidiagonal on the left (the right vectors are unchanged); every lane runs
+        // the scalar recurrence, lane 0 stores it
+        double* dd = sh.d;
+        double* ee = sh.e;
+        double di = dd[0];
+        for (int i = 0; i < m - 1; ++i) {
+            double cs, sn, r;
+            dlartg(di, ee[i], cs, sn, r);
+            const double dn = dd[i + 1];
+            wsync();
+            if (lane == 0) {
+                dd[i] = r;
+                ee[i] = sn * dn;
+            }
+            di = cs * dn;
+        }
+        wsync();
+        if (lane == 0) dd[m - 1] = di;
+        wsync();
+        ok = bd_vt(sh, m, n, ld, lane);
+    }
+    apply_ph(sh, n, m, 0, ld, lane);
     return ok;
 }
 
@@ -485,33 +735,35 @@ __device__ __forceinline__ unsigned char code_of(int q, bool has_off, double off
     return (unsigned char)c;
 }
 
-__global__ __launch_bounds__(64) void beamformer_kernel(int n, const d2* __restrict__ H, const double* __restrict__ offset,
+__global__ __launch_bounds__(64) void beamformer_kernel(int tx, int rx, const d2* __restrict__ H,
+                                                        const double* __restrict__ offset,
                                                         unsigned char* __restrict__ wr_code,
                                                         unsigned char* __restrict__ wt_code, int32_t* __restrict__ beam_idx,
                                                         double* __restrict__ rss_out, uint32_t* __restrict__ status,
                                                         d2* __restrict__ vh_r, d2* __restrict__ vh_t) {
     extern __shared__ __align__(16) unsigned char bf_lds[];
     const int lane = threadIdx.x;
-    const int ld = n + 1;
+    const int N = max(tx, rx), ld = N + 1;
     const size_t b = blockIdx.x;
-    const int nn = n * n;
+    const int nh = tx * rx;
     BfShared sh;
     sh.A = (d2*)bf_lds;
-    sh.X = sh.A + n * ld;
-    sh.taup = sh.X + n * ld;
+    sh.X = sh.A + N * ld;
+    sh.Q = sh.X + N * ld;
+    sh.taup = sh.Q + (tx != rx ? N * ld : 0);
     sh.d = (double*)(sh.taup + BF_NMAX);
     sh.e = sh.d + BF_NMAX;
     sh.qr = (signed char*)(sh.e + BF_NMAX);
-    sh.qt = sh.qr + nn;
-    const d2* Hb = H + b * nn;
+    sh.qt = sh.qr + rx * rx;
+    const d2* Hb = H + b * nh;
 
     // non-finite input: numpy's zgesdd fails (LinAlgError "SVD did not converge")
     bool bad = false;
-    for (int k = lane; k < nn; k += 64) {
+    for (int k = lane; k < nh; k += 64) {
         const d2 h = Hb[k];
         bad |= !isfinite(h.x) || !isfinite(h.y);
     }
-    uint32_t st = (n > BF_SMLSIZ) ? ACE_ST_BF_DC : 0u;
+    uint32_t st = (min(tx, rx) > BF_SMLSIZ) ? ACE_ST_BF_DC : 0u;
     if (__any(bad)) {
         if (lane == 0) {
             status[b] = st | ACE_ST_BF_NONFINITE;
@@ -519,51 +771,55 @@ __global__ __launch_bounds__(64) void beamformer_kernel(int n, const d2* __restr
             beam_idx[2 * b + 1] = -1;
             rss_out[b] = __builtin_nan("");
         }
-        for (int k = lane; k < n; k += 64) wr_code[b * n + k] = wt_code[b * n + k] = 0;
+        for (int k = lane; k < rx; k += 64) wr_code[b * rx + k] = 0;
+        for (int k = lane; k < tx; k += 64) wt_code[b * tx + k] = 0;
         return;
     }
     bool ok = true;
     for (int pass = 0; pass < 2; ++pass) {
-        // pass 0: zgesdd(H) -> wr; pass 1: zgesdd(H^T) -> wt   (codebook_library.py:59-60)
-        for (int k = lane; k < nn; k += 64) {
-            const int r = k / n, c = k - r * n;
-            sh.A[r * ld + c] = pass == 0 ? Hb[k] : Hb[c * n + r];
+        // pass 0: zgesdd(H) [tx][rx] -> Vh [rx][rx] -> wr; pass 1: zgesdd(H^T) [rx][tx] -> [tx][tx] -> wt
+        // (codebook_library.py:59-60)
+        const int m = pass == 0 ? tx : rx, n = pass == 0 ? rx : tx;
+        for (int k = lane; k < nh; k += 64) {
+            const int r = k / rx, c = k - r * rx;   // H[r][c]
+            if (pass == 0) sh.A[r * ld + c] = Hb[k];
+            else sh.A[c * ld + r] = Hb[k];
         }
         wsync();
-        ok &= gesdd_vh(sh, n, ld, lane);
+        ok &= gesdd_vh(sh, m, n, ld, lane);
         signed char* q = pass == 0 ? sh.qr : sh.qt;
         d2* vh_out = pass == 0 ? vh_r : vh_t;
-        for (int k = lane; k < nn; k += 64) {
+        for (int k = lane; k < n * n; k += 64) {
             const int r = k / n, c = k - r * n;
-            const d2 v = (n == 1) ? make_double2(1.0, 0.0) : sh.X[r * ld + c];
+            const d2 v = sh.X[r * ld + c];
             q[k] = quant(v);
-            if (vh_out) vh_out[b * nn + k] = v;
+            if (vh_out) vh_out[b * n * n + k] = v;
         }
         wsync();
     }
     if (!ok) st |= ACE_ST_BF_NOCONV;
     // ---------------- received-power search (codebook_library.py:67-77)
-    // wr_quant[b', j] = j^(-qr[j][b']), wt_quant[a, i] = j^(-qt[i][a])
+    // wr_quant[b', j] = j^(-qr[j][b']) (b', j < rx), wt_quant[a, i] = j^(-qt[i][a]) (a, i < tx)
     d2* Hs = sh.A;
     d2* T = sh.X;
-    for (int k = lane; k < nn; k += 64) {
-        const int r = k / n, c = k - r * n;
+    for (int k = lane; k < nh; k += 64) {
+        const int r = k / rx, c = k - r * rx;
         Hs[r * ld + c] = Hb[k];
     }
     wsync();
-    for (int k = lane; k < nn; k += 64) {  // T[a][j] = sum_b H[a][b] wr[b][j]
-        const int a = k / n, j = k - a * n;
+    for (int k = lane; k < nh; k += 64) {  // T[a][j] = sum_b H[a][b] wr[b][j]
+        const int a = k / rx, j = k - a * rx;
         d2 acc = make_double2(0.0, 0.0);
-        for (int bb = 0; bb < n; ++bb) acc = cadd(acc, rotk(Hs[a * ld + bb], -sh.qr[j * n + bb]));
+        for (int bb = 0; bb < rx; ++bb) acc = cadd(acc, rotk(Hs[a * ld + bb], -sh.qr[j * rx + bb]));
         T[a * ld + j] = acc;
     }
     wsync();
     double best = -__builtin_inf();
     int bidx = 0x7fffffff;
-    for (int k = lane; k < nn; k += 64) {  // M[i][j] = sum_a wt[a][i] T[a][j]
-        const int i = k / n, j = k - i * n;
+    for (int k = lane; k < nh; k += 64) {  // M[i][j] = sum_a wt[a][i] T[a][j], i-major (i < tx, j < rx)
+        const int i = k / rx, j = k - i * rx;
         d2 acc = make_double2(0.0, 0.0);
-        for (int a = 0; a < n; ++a) acc = cadd(acc, rotk(T[a * ld + j], -sh.qt[i * n + a]));
+        for (int a = 0; a < tx; ++a) acc = cadd(acc, rotk(T[a * ld + j], -sh.qt[i * tx + a]));
         const double amp = hypot(acc.x, acc.y);
         const double rss = 10.0 * log10(amp * amp * 1000.0);
         if (bf_better(rss, k, best, bidx)) { best = rss; bidx = k; }
@@ -573,13 +829,14 @@ __global__ __launch_bounds__(64) void beamformer_kernel(int n, const d2* __restr
         const int oi = __shfl_xor(bidx, o, 64);
         if (bf_better(ob, oi, best, bidx)) { best = ob; bidx = oi; }
     }
-    const int tx_idx = bidx / n, rx_idx = bidx - tx_idx * n;
+    const int tx_idx = bidx / rx, rx_idx = bidx - tx_idx * rx;
+    // offset [batch][N]: entry k compensates element k of both codes (numpy broadcasting of the reference's
+    // `* np.exp(-1j * offset)`, :122-127; tx != rx admits only a constant offset there)
     const bool has_off = offset != nullptr;
-    for (int k = lane; k < n; k += 64) {
-        const double off = has_off ? offset[b * n + k] : 0.0;
-        wr_code[b * n + k] = code_of(sh.qr[rx_idx * n + k], has_off, off);
-        wt_code[b * n + k] = code_of(sh.qt[tx_idx * n + k], has_off, off);
-    }
+    for (int k = lane; k < rx; k += 64)
+        wr_code[b * rx + k] = code_of(sh.qr[rx_idx * rx + k], has_off, has_off ? offset[b * N + k] : 0.0);
+    for (int k = lane; k < tx; k += 64)
+        wt_code[b * tx + k] = code_of(sh.qt[tx_idx * tx + k], has_off, has_off ? offset[b * N + k] : 0.0);
     if (lane == 0) {
         beam_idx[2 * b] = tx_idx;
         beam_idx[2 * b + 1] = rx_idx;
@@ -588,9 +845,10 @@ __global__ __launch_bounds__(64) void beamformer_kernel(int n, const d2* __restr
     }
 }
 
-size_t bf_lds_bytes(int n) {
-    return (size_t)2 * n * (n + 1) * sizeof(d2) + BF_NMAX * sizeof(d2) + 2 * BF_NMAX * sizeof(double) +
-           (size_t)2 * n * n;
+size_t bf_lds_bytes(int tx, int rx) {
+    const size_t N = std::max(tx, rx);
+    return (size_t)(tx != rx ? 3 : 2) * N * (N + 1) * sizeof(d2) + BF_NMAX * sizeof(d2) +
+           2 * BF_NMAX * sizeof(double) + (size_t)tx * tx + (size_t)rx * rx;
 }
 
 }  // namespace
@@ -603,13 +861,13 @@ extern "C" int ace_svd_beamformer_batch(int batch, int tx, int rx, const double*
                                         uint32_t* status, double* vh_r, double* vh_t, void* stream) {
     g_err.clear();
     if (batch < 0) return fail(ACE_ERR_ARG, "svd_beamformer: batch %d < 0", batch);
-    if (tx != rx) return fail(ACE_ERR_UNSUPPORTED, "svd_beamformer: tx (%d) != rx (%d) — square arrays only", tx, rx);
-    if (tx < 1 || tx > BF_NMAX) return fail(ACE_ERR_UNSUPPORTED, "svd_beamformer: %d antennas outside 1..%d", tx, BF_NMAX);
+    if (tx < 1 || tx > BF_NMAX || rx < 1 || rx > BF_NMAX)
+        return fail(ACE_ERR_UNSUPPORTED, "svd_beamformer: %d x %d antennas outside 1..%d", tx, rx, BF_NMAX);
     if (batch == 0) return ACE_OK;
     if (!H || !wr_code || !wt_code || !beam_idx || !rss || !status)
         return fail(ACE_ERR_ARG, "svd_beamformer: null output/input pointer");
-    const size_t lds = bf_lds_bytes(tx);
-    hipLaunchKernelGGL(beamformer_kernel, dim3(batch), dim3(64), lds, (hipStream_t)stream, tx, (const d2*)H, offset,
+    const size_t lds = bf_lds_bytes(tx, rx);
+    hipLaunchKernelGGL(beamformer_kernel, dim3(batch), dim3(64), lds, (hipStream_t)stream, tx, rx, (const d2*)H, offset,
                        wr_code, wt_code, beam_idx, rss, status, (d2*)vh_r, (d2*)vh_t);
     ACE_HIP(hipGetLastError());
     return ACE_OK;
@@ -619,11 +877,12 @@ extern "C" int ace_svd_beamformer_host(int batch, int tx, int rx, const double* 
                                        uint8_t* wr_code, uint8_t* wt_code, int32_t* beam_idx, double* rss,
                                        uint32_t* status, double* vh_r, double* vh_t) {
     g_err.clear();
-    if (batch < 0 || tx != rx || tx < 1 || tx > BF_NMAX)
+    if (batch < 0 || tx < 1 || tx > BF_NMAX || rx < 1 || rx > BF_NMAX)
         return ace_svd_beamformer_batch(batch, tx, rx, H, offset, wr_code, wt_code, beam_idx, rss, status, vh_r,
                                         vh_t, nullptr);
     if (batch == 0) return ACE_OK;
-    const size_t n = tx, nH = 16 * (size_t)batch * n * n, nc = (size_t)batch * n;
+    const size_t B = batch, N = std::max(tx, rx), nH = 16 * B * tx * rx, nvr = 16 * B * rx * rx,
+                 nvt = 16 * B * tx * tx, noff = 8 * B * N, ncr = B * rx, nct = B * tx;
     std::vector<void*> bufs;
     auto cleanup = [&]() {
         for (void* q : bufs) (void)hipFree(q);
@@ -636,14 +895,14 @@ extern "C" int ace_svd_beamformer_host(int batch, int tx, int rx, const double* 
     };
     void *dH, *doff = nullptr, *dwr, *dwt, *didx, *drss, *dst, *dvr = nullptr, *dvt = nullptr;
     hipError_t e;
-    if ((e = dalloc(nH, &dH)) || (offset && (e = dalloc(8 * nc, &doff))) || (e = dalloc(nc, &dwr)) ||
-        (e = dalloc(nc, &dwt)) || (e = dalloc(8 * (size_t)batch, &didx)) || (e = dalloc(8 * (size_t)batch, &drss)) ||
-        (e = dalloc(4 * (size_t)batch, &dst)) || (vh_r && (e = dalloc(nH, &dvr))) || (vh_t && (e = dalloc(nH, &dvt)))) {
+    if ((e = dalloc(nH, &dH)) || (offset && (e = dalloc(noff, &doff))) || (e = dalloc(ncr, &dwr)) ||
+        (e = dalloc(nct, &dwt)) || (e = dalloc(8 * B, &didx)) || (e = dalloc(8 * B, &drss)) ||
+        (e = dalloc(4 * B, &dst)) || (vh_r && (e = dalloc(nvr, &dvr))) || (vh_t && (e = dalloc(nvt, &dvt)))) {
         cleanup();
         return fail(ACE_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
     }
     if ((e = hipMemcpy(dH, H, nH, hipMemcpyHostToDevice)) ||
-        (offset && (e = hipMemcpy(doff, offset, 8 * nc, hipMemcpyHostToDevice)))) {
+        (offset && (e = hipMemcpy(doff, offset, noff, hipMemcpyHostToDevice)))) {
         cleanup();
         return fail(ACE_ERR_HIP, "hipMemcpy: %s", hipGetErrorString(e));
     }
@@ -651,13 +910,13 @@ extern "C" int ace_svd_beamformer_host(int batch, int tx, int rx, const double* 
                                       (uint8_t*)dwt, (int32_t*)didx, (double*)drss, (uint32_t*)dst, (double*)dvr,
                                       (double*)dvt, nullptr);
     if (rc == ACE_OK) {
-        if ((e = hipDeviceSynchronize()) || (e = hipMemcpy(wr_code, dwr, nc, hipMemcpyDeviceToHost)) ||
-            (e = hipMemcpy(wt_code, dwt, nc, hipMemcpyDeviceToHost)) ||
-            (e = hipMemcpy(beam_idx, didx, 8 * (size_t)batch, hipMemcpyDeviceToHost)) ||
-            (e = hipMemcpy(rss, drss, 8 * (size_t)batch, hipMemcpyDeviceToHost)) ||
-            (e = hipMemcpy(status, dst, 4 * (size_t)batch, hipMemcpyDeviceToHost)) ||
-            (vh_r && (e = hipMemcpy(vh_r, dvr, nH, hipMemcpyDeviceToHost))) ||
-            (vh_t && (e = hipMemcpy(vh_t, dvt, nH, hipMemcpyDeviceToHost))))
+        if ((e = hipDeviceSynchronize()) || (e = hipMemcpy(wr_code, dwr, ncr, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(wt_code, dwt, nct, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(beam_idx, didx, 8 * B, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(rss, drss, 8 * B, hipMemcpyDeviceToHost)) ||
+            (e = hipMemcpy(status, dst, 4 * B, hipMemcpyDeviceToHost)) ||
+            (vh_r && (e = hipMemcpy(vh_r, dvr, nvr, hipMemcpyDeviceToHost))) ||
+            (vh_t && (e = hipMemcpy(vh_t, dvt, nvt, hipMemcpyDeviceToHost))))
             rc = fail(ACE_ERR_HIP, "svd_beamformer: %s", hipGetErrorString(e));
     }
     const std::string keep = g_err;

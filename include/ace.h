@@ -290,16 +290,19 @@ int ace_driver_randperm(uint64_t seed, uint64_t stream, int P, int k, int32_t* o
  *   wr_out, wt_out = svd_beamformer(H)                       main/codebook_library.py:57-96
  *   wr_out, wt_out = svd_beamformer_compensation(H, offset)  main/codebook_library.py:98-138
  *   reached from codebook_generator (:192-213), H = reshape(H_est[i,:], [tx, rx]) (:197).
- * H: [batch][tx][rx] c128 row-major (DEVICE for _batch).  offset: [batch][rx] radians
- * (compensation * pi/2) or NULL for svd_beamformer.  Outputs: wr_code [batch][rx] and
- * wt_code [batch][tx] (2-bit phase codes 0..3 = the characters of the reference's strings),
- * beam_idx [batch][2] = (tx_idx, rx_idx) of the argmax pair, rss [batch] = its
- * 10*log10(|wt^T H wr|^2 * 1000), status [batch] (ACE_ST_BF_*).  vh_r / vh_t (optional,
- * may be NULL): [batch][n][n] c128 Vh of svd(H) and svd(H^T) in numpy's (zgesdd's) phase
- * convention.  Square arrays only (tx == rx <= 32, as main.py:454 calls it). */
+ * H: [batch][tx][rx] c128 row-major (DEVICE for _batch), 1 <= tx, rx <= 32 (main.py:454 calls
+ * it square; any shape np.shape(H) gives is taken, with zgesdd's QR / LQ / direct paths).
+ * offset: [batch][max(tx, rx)] radians (compensation * pi/2; entry k compensates element k of
+ * both codes, i.e. numpy's broadcasting — tx != rx admits only a constant row there) or NULL
+ * for svd_beamformer.  Outputs: wr_code [batch][rx] and wt_code [batch][tx] (2-bit phase codes
+ * 0..3 = the characters of the reference's strings), beam_idx [batch][2] = (tx_idx, rx_idx) of
+ * the argmax pair, rss [batch] = its 10*log10(|wt^T H wr|^2 * 1000), status [batch]
+ * (ACE_ST_BF_*).  vh_r [batch][rx][rx] / vh_t [batch][tx][tx] (optional, may be NULL): c128 Vh
+ * of svd(H) and svd(H^T) in numpy's (zgesdd's) phase and sign convention. */
 #define ACE_ST_BF_NONFINITE 16u /* H has NaN/Inf: numpy raises LinAlgError; codes zeroed, beam_idx -1 */
 #define ACE_ST_BF_NOCONV 32u    /* dbdsqr iteration budget exhausted (numpy would raise) */
-#define ACE_ST_BF_DC 64u        /* n > 25: numpy's zgesdd uses divide and conquer; beams match up to sign */
+#define ACE_ST_BF_DC 64u        /* min(tx, rx) > 25: zgesdd's divide and conquer, its merge's signs applied;
+                                   a vector the merge deflates (rank-deficient H) may still differ */
 int ace_svd_beamformer_batch(int batch, int tx, int rx, const double* H, const double* offset,
                              uint8_t* wr_code, uint8_t* wt_code, int32_t* beam_idx, double* rss,
                              uint32_t* status, double* vh_r, double* vh_t, void* stream);

@@ -22,8 +22,9 @@ reproduces zgesdd's convention.  For square n <= 25 (ilaenv SMLSIZ) zgesdd's pat
 ``dlartg`` sign convention: c >= 0, r carries the sign of f).  ``test_beamformer_oracle``
 checks it against ``numpy.linalg.svd`` itself, which pins the convention the HIP kernel
 implements.  For 26 <= n <= 32 zgesdd switches to divide and conquer (dlasd0), whose real
-singular-vector signs differ; the phases from zgebd2 are the same, so beams agree up to a
-per-beam sign = code offset 0 or 2 (a physically identical beam).
+singular vectors are dbdsqr's up to sign; ``dc_merge_signs`` restates the merge's sign
+convention (dlasd1 / dlasd3), exact except on vectors the merge deflates (the null space of a
+rank-deficient H), where beams agree up to a per-beam sign = code offset 0 or 2.
 
 ``svd_beamformer`` itself uses ``numpy.linalg.svd`` exactly as the reference does.
 """
@@ -480,16 +481,170 @@ def zgebd2_upper(A):
     return d, e, refl
 
 
+SMLSIZ = 25   # ilaenv(9, 'DBDSDC'): dbdsdc's divide-and-conquer threshold
+
+
+def dc_merge_signs(d, e, vtb):
+    """zgesdd's divide-and-conquer sign convention for 26 <= n <= 32, applied to dbdsqr's VT.
+
+    dbdsdc('U', 'I') with n > SMLSIZ calls dlasd0, whose dlasdt tree for n <= 2 (SMLSIZ + 1)
+    is one root at row mid = n // 2 (0-based) over the leaves [0, mid) (dlasdq, sqre = 1) and
+    (mid, n) (dlasdq, sqre = 0).  dlasd1 merges them: dlasd2 puts the merge row's unit vector
+    first in the deflated basis and dlasd3 sets every non-deflated secular vector's first
+    component to -1 before normalising (``U(1, I) = NEGONE``), so the merged left vector u_i
+    has u_i(mid) < 0.  The singular vectors themselves equal dbdsqr's up to sign (distinct
+    singular values), hence: flip VT row i where u_i(mid) = (d_mid v_i(mid) + e_mid
+    v_i(mid + 1)) / s_i > 0.  A vector dlasd2 deflated (|z_j| <= 64 eps * scale) keeps its
+    leaf's dbdsqr sign instead, which this does not model (only the null space of a rank-
+    deficient matrix was seen to deflate; test_beamformer_oracle measures it)."""
+    n = len(d)
+    mid = n // 2
+    um = d[mid] * vtb[:, mid] + e[mid] * vtb[:, mid + 1]
+    return vtb * np.where(um > 0.0, -1.0, 1.0)[:, None]
+
+
 def gesdd_vh(A, stats=None):
-    """Vh of zgesdd(JOBZ='A') for a square A with n <= 25 (see module docstring)."""
+    """Vh of zgesdd(JOBZ='A') for a square A with n <= 32 (see module docstring; n > 25 takes
+    the divide-and-conquer sign convention of ``dc_merge_signs``)."""
     A = np.asarray(A, dtype=np.complex128)
     n = A.shape[0]
     d, e, refl = zgebd2_upper(A)
     if n == 1:                               # dbdsdc n == 1: VT = 1, the sign goes to U
         return np.ones((1, 1), np.complex128)
-    _, vtb = dbdsqr_vt(d, e, stats)
+    _, vtb = dbdsqr_vt(d.copy(), e.copy(), stats)
+    if n > SMLSIZ:
+        vtb = dc_merge_signs(d, e, vtb)
     X = vtb.astype(np.complex128)
     for (c0, vv, taup) in reversed(refl):   # X := X G(i)^H, i = n-1 .. 1
+        sub = X[:, c0:]
+        w = sub @ vv
+        X[:, c0:] = sub - np.conj(taup) * np.outer(w, vv.conj())
+    return X
+
+
+# ------------------------------------------- rectangular arrays (tx != rx): zgesdd's paths
+def gesdd_paths(m, n):
+    """zgesdd's path choice for an m x n input (zgesdd.f: MNTHR1 = INT(MINMN * 17 / 9),
+    MNTHR2 = INT(MINMN * 5 / 3)): 'qr' (paths 1-4, M >= MNTHR1: QR first), 'lq' (paths 1t-4t,
+    N >= MNTHR1: LQ first) or 'direct' (paths 5/6 and 5t/6t: zgebrd on the input itself;
+    5 and 6 differ only in how P^H is formed, not in the result)."""
+    minmn = min(m, n)
+    mnthr1 = int(minmn * 17.0 / 9.0)
+    if m >= n and m >= mnthr1 and m > n:
+        return "qr"
+    if n > m and n >= mnthr1:
+        return "lq"
+    return "direct"
+
+
+def zgeqr2_r(A):
+    """R of LAPACK zgeqr2 (Householder QR, zlarfg conventions) of an m x n, m >= n input."""
+    A = np.array(A, dtype=np.complex128)
+    m, n = A.shape
+    for i in range(n):
+        beta, tau, v = zlarfg(A[i, i], A[i + 1:, i])
+        A[i, i] = beta
+        A[i + 1:, i] = 0.0
+        if i < n - 1:
+            vq = np.concatenate([[1.0 + 0j], v])
+            C = A[i:, i + 1:]
+            A[i:, i + 1:] = C - np.conj(tau) * np.outer(vq, vq.conj() @ C)   # H(i)^H C
+    return np.triu(A[:n, :n])
+
+
+def zgelq2_lq(A):
+    """LAPACK zgelq2 of an m x n, m < n input: (L [m][m] lower, Q [n][n]) with A = L Q[:m],
+    Q = H(m)^H ... H(1)^H (zunglq with k = m reflectors, all n rows)."""
+    A = np.array(A, dtype=np.complex128)
+    m, n = A.shape
+    Qh = np.eye(n, dtype=np.complex128)           # H(1) H(2) ... H(m)
+    for i in range(m):
+        row = np.conj(A[i, i:])                    # zlacgv
+        beta, tau, v = zlarfg(row[0], row[1:])
+        vv = np.concatenate([[1.0 + 0j], v])
+        if i < m - 1:
+            C = A[i + 1:, i:]
+            A[i + 1:, i:] = C - tau * np.outer(C @ vv, vv.conj())             # C H(i)
+        A[i, i] = beta
+        A[i, i + 1:] = 0.0
+        sub = Qh[:, i:]
+        Qh[:, i:] = sub - tau * np.outer(sub @ vv, vv.conj())
+    return np.tril(A[:, :m]), Qh.conj().T
+
+
+def zgebd2_lower(A):
+    """LAPACK zgebd2 for m < n: A = Q B P^H, B real lower bidiagonal (d [m], e [m - 1]).
+    Returns (d, e, [(c0, v, taup)]) with G(i) = I - taup v v^H acting on columns c0 = i .. n."""
+    A = np.array(A, dtype=np.complex128)
+    m, n = A.shape
+    d = np.zeros(m)
+    e = np.zeros(max(m - 1, 0))
+    refl = []
+    for i in range(m):
+        row = np.conj(A[i, i:])                    # zlacgv
+        beta, taup, vp = zlarfg(row[0], row[1:])
+        d[i] = beta.real
+        vv = np.concatenate([[1.0 + 0j], vp])
+        refl.append((i, vv, taup))
+        if i < m - 1:
+            C = A[i + 1:, i:]
+            A[i + 1:, i:] = C - taup * np.outer(C @ vv, vv.conj())           # C G(i)
+            beta2, tauq, vq = zlarfg(A[i + 1, i], A[i + 2:, i])
+            e[i] = beta2.real
+            vc = np.concatenate([[1.0 + 0j], vq])
+            C2 = A[i + 1:, i + 1:]
+            A[i + 1:, i + 1:] = C2 - np.conj(tauq) * np.outer(vc, vc.conj() @ C2)   # H(i)^H C
+    return d, e, refl
+
+
+def lower_to_upper(d, e):
+    """dbdsdc('L'): Givens rotations on the left turn the lower bidiagonal into an upper one with
+    the same right singular vectors (dbdsdc.f, IUPLO = 2: DLARTG, E(I) = SN D(I+1), D(I+1) = CS D(I+1))."""
+    d = [float(x) for x in d]
+    e = [float(x) for x in e]
+    for i in range(len(d) - 1):
+        cs, sn, r = dlartg(d[i], e[i])
+        d[i] = r
+        e[i] = sn * d[i + 1]
+        d[i + 1] = cs * d[i + 1]
+    return np.array(d), np.array(e)
+
+
+def gesdd_vh_rect(A, stats=None):
+    """Vh [n][n] of zgesdd(JOBZ='A') for any m x n input with m, n <= 32 (square: gesdd_vh)."""
+    A = np.asarray(A, dtype=np.complex128)
+    m, n = A.shape
+    if m == n:
+        return gesdd_vh(A, stats)
+    if n == 1:                                   # dbdsdc n == 1: VT = 1
+        return np.ones((1, 1), np.complex128)
+    path = gesdd_paths(m, n)
+    if path == "qr":                             # zgeqrf, zgebrd on R (n x n)
+        return gesdd_vh(zgeqr2_r(A), stats)
+    if path == "lq":                             # zgelqf, zgebrd on L (m x m), VT = [Vh_L Q[:m]; Q[m:]]
+        L, Q = zgelq2_lq(A)
+        X = np.empty((n, n), np.complex128)
+        X[:m] = (np.ones((1, 1)) if m == 1 else gesdd_vh(L, stats)) @ Q[:m]
+        X[m:] = Q[m:]
+        return X
+    if m > n:                                    # direct, tall: upper bidiagonal n x n
+        d, e, refl = zgebd2_upper(A)
+        _, vtb = dbdsqr_vt(d.copy(), e.copy(), stats)
+        if n > SMLSIZ:
+            vtb = dc_merge_signs(d, e, vtb)
+        X = vtb.astype(np.complex128)
+    else:                                        # direct, wide: lower bidiagonal m x m, VT = [VT_b 0; 0 I] P^H
+        d, e, refl = zgebd2_lower(A)
+        if m == 1:
+            vtb = np.ones((1, 1))
+        else:
+            du, eu = lower_to_upper(d, e)
+            _, vtb = dbdsqr_vt(du.copy(), eu.copy(), stats)
+            if m > SMLSIZ:
+                vtb = dc_merge_signs(du, eu, vtb)
+        X = np.eye(n, dtype=np.complex128)
+        X[:m, :m] = vtb
+    for (c0, vv, taup) in reversed(refl):        # X := X G(i)^H, last reflector first
         sub = X[:, c0:]
         w = sub @ vv
         X[:, c0:] = sub - np.conj(taup) * np.outer(w, vv.conj())

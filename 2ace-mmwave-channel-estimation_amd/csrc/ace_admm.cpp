@@ -805,7 +805,8 @@ int admm_run(const LinOps& L, const AdmmParams& p, const AdmmState& w, int batch
     za.optX = w.optX;
     za.optY = w.optY;
     za.done_count = w.done;
-    za.np = rank_profile(p.tx, p.rx, m, n, p.rank_one ? 0 : p.use_rank_one, za.rl, za.fl);
+    za.np = rank_profile(p.prof_tx ? p.prof_tx : p.tx, p.rx, m, p.prof_n ? p.prof_n : n,
+                         p.rank_one ? 0 : p.use_rank_one, za.rl, za.fl);
     za.rank_one = p.rank_one;
     za.tol_rel = p.tol_rel;
     za.tol_abs = p.tol_abs;

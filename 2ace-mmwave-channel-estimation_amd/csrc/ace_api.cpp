@@ -20,8 +20,8 @@ int validate(const ace_admm_cfg* c, int batch, int m, int n, int tx, int rx) {
     if (tx * rx != n) return fail(ACE_ERR_ARG, "n (%d) != tx*rx (%d*%d)", n, tx, rx);
     if (c->variant != ACE_VARIANT_A2ONLY && c->variant != ACE_VARIANT_NUCLEAR)
         return fail(ACE_ERR_ARG, "unknown variant %d", c->variant);
-    if (c->variant == ACE_VARIANT_A2ONLY && (tx < 2 || tx > 32 || (tx & 1) || rx > 32))
-        return fail(ACE_ERR_UNSUPPORTED, "A2only Z-prox needs even tx in [2,32] and rx <= 32 (got %d, %d)", tx, rx);
+    if (c->variant == ACE_VARIANT_A2ONLY && (tx < 1 || tx > 32 || ((tx & 1) && tx > 31) || rx > 32))
+        return fail(ACE_ERR_UNSUPPORTED, "A2only Z-prox needs tx in [1,32] and rx <= 32 (got %d, %d)", tx, rx);
     if (n > 4096 || m > 4096) return fail(ACE_ERR_UNSUPPORTED, "m, n must be <= 4096 (got %d, %d)", m, n);
     if (c->maxiter < 1) return fail(ACE_ERR_ARG, "maxiter must be >= 1");
     if (!(c->mu0 > 0) || !(c->rho > 0)) return fail(ACE_ERR_ARG, "mu0 and rho must be > 0");
@@ -231,6 +231,63 @@ size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n)
     return cv.off + 256;
 }
 
+}  // extern "C"
+
+namespace {
+int solve_core(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, int prof_tx, int prof_n,
+               const double* A, const double* B, const double* X0, double* Xo, double* Yo, int32_t* iters,
+               uint32_t* status, double* mu_out, void* workspace, size_t workspace_bytes, hipStream_t st);
+
+// A2only with an odd tx.  The reference reshapes z to tx x rx for any tx (inferLowRankV4_multi.m:426); the
+// Z-prox's parallel Jacobi pairs rows, so the problem is solved as the (tx + 1) x rx one whose extra row is
+// zero: A's columns tx + (tx + 1) j are zero, hence that row of X (= (I + A^H A)^{-1}(A^H T + Z - N / mu)), of
+// E = X + N / mu, Z and N stays exactly zero (E E^H gets an exact zero eigenpair whose U^H E row is zero), and
+// every other entry follows the tx x rx problem's arithmetic.  The rank profile keeps the original tx and n
+// (:437-464).  The padded A, X0, X and workspace are this call's own allocations, released after the solve's
+// stream drains (so this shape returns synchronously).
+int solve_odd_tx(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
+                 const double* B, const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
+                 double* mu_out, hipStream_t st) {
+    const int txp = tx + 1, np = txp * rx, r = cols(cfg), R = cfg->scale_by_row ? r : 1;
+    const size_t arows = (size_t)(cfg->a_shared ? 1 : batch) * m * rx, xrows = (size_t)batch * r * rx,
+                 orows = (size_t)batch * R * rx, ws = ace_admm_workspace_size(cfg, batch, m, np) + 4096;
+    void *dA = nullptr, *dX0 = nullptr, *dX = nullptr, *dW = nullptr;
+    hipError_t e = hipMalloc(&dA, arows * txp * 16);
+    if (e == hipSuccess) e = hipMalloc(&dX0, xrows * txp * 16);
+    if (e == hipSuccess) e = hipMalloc(&dX, orows * txp * 16);
+    if (e == hipSuccess) e = hipMalloc(&dW, ws);
+    auto release = [&]() {   // (the solve's work on st must finish before its buffers go)
+        (void)hipStreamSynchronize(st);
+        for (void* q : {dA, dX0, dX, dW})
+            if (q) (void)hipFree(q);
+    };
+    // [rows][tx] runs of complex entries -> [rows][tx + 1] with a zero last entry
+    if (e == hipSuccess) e = hipMemsetAsync(dA, 0, arows * txp * 16, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dX0, 0, xrows * txp * 16, st);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(dA, (size_t)txp * 16, A, (size_t)tx * 16, (size_t)tx * 16, arows, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(dX0, (size_t)txp * 16, X0, (size_t)tx * 16, (size_t)tx * 16, xrows, hipMemcpyDeviceToDevice,
+                             st);
+    if (e != hipSuccess) {
+        release();
+        return fail(ACE_ERR_HIP, "odd-tx padding: %s", hipGetErrorString(e));
+    }
+    int rc = solve_core(cfg, batch, m, np, txp, rx, tx, n, (const double*)dA, B, (const double*)dX0, (double*)dX, Yo,
+                        iters, status, mu_out, dW, ws, st);
+    if (rc == ACE_OK &&
+        (e = hipMemcpy2DAsync(Xo, (size_t)tx * 16, dX, (size_t)txp * 16, (size_t)tx * 16, orows, hipMemcpyDeviceToDevice,
+                              st)) != hipSuccess)
+        rc = fail(ACE_ERR_HIP, "odd-tx unpadding: %s", hipGetErrorString(e));
+    const std::string keep = g_err;
+    release();
+    g_err = keep;
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
 int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
                          const double* B, const double* X0, double* Xo, double* Yo, int32_t* iters, uint32_t* status,
                          double* mu_out, void* workspace, size_t workspace_bytes, void* stream) {
@@ -239,6 +296,18 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     if (rc) return rc;
     if (!A || !B || !X0 || !Xo || !Yo || !workspace) return fail(ACE_ERR_ARG, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
+    if (cfg->variant == ACE_VARIANT_A2ONLY && (tx & 1))
+        return solve_odd_tx(cfg, batch, m, n, tx, rx, A, B, X0, Xo, Yo, iters, status, mu_out, st);
+    return solve_core(cfg, batch, m, n, tx, rx, 0, 0, A, B, X0, Xo, Yo, iters, status, mu_out, workspace,
+                      workspace_bytes, st);
+}
+
+}  // extern "C"
+
+namespace {
+int solve_core(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, int prof_tx, int prof_n,
+               const double* A, const double* B, const double* X0, double* Xo, double* Yo, int32_t* iters,
+               uint32_t* status, double* mu_out, void* workspace, size_t workspace_bytes, hipStream_t st) {
     const size_t need = ace_admm_workspace_size(cfg, batch, m, n);
     if (need > workspace_bytes)
         return fail(ACE_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
@@ -264,10 +333,15 @@ int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int t
     p.tol_abs = cfg->tol_abs;
     p.tx = tx;
     p.rx = rx;
+    p.prof_tx = prof_tx;
+    p.prof_n = prof_n;
     p.use_rank_one = cfg->use_rank_one;
     p.rank_one = cfg->rank_one;
     return admm_run(L, p, w, batch, B, X0, Xo, Yo, iters, status, mu_out, st);
 }
+}  // namespace
+
+extern "C" {
 
 int ace_admm_solve_host(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx, const double* A,
                         const double* B, const double* X0, double* X, double* Y, int32_t* iters, uint32_t* status,

@@ -213,6 +213,8 @@ struct AdmmParams {
     int variant, r, row_mode, maxiter, fixed_iters, eig_warm;
     double mu0, rho, tol_rel, tol_abs;
     int tx, rx;
+    int prof_tx, prof_n;               // the rank profile's tx and n when they differ from the layout's (odd tx,
+                                       // solved zero-padded to tx + 1 rows: ace_api.cpp); 0: tx, n
     int use_rank_one;                  // batch-wide flag (ignored where rank_one is given)
     const unsigned char* rank_one;     // per-realisation use_rank_one (device, may be null)
     // per-realisation train partitions (r > 1 stages only): L is the full A's operators, the state is in

@@ -121,10 +121,11 @@ size_t ace_admm_workspace_size(const ace_admm_cfg* cfg, int batch, int m, int n)
  *   iters  [batch] int32 out (may be NULL)    iterations run
  *   status [batch] uint32 out (may be NULL)   ACE_ST_* bits
  *   mu     [batch] f64 out (may be NULL)      final penalty mu
- * Constraints: n == tx*rx, tx <= 32, rx <= 32 (tx, rx in {4,8,16,32} in the reference),
- * m >= 1, 1 <= r <= 32 (r > 1: shared A only).  Returns once all kernels are enqueued; in
- * convergence mode (fixed_iters == 0) the host polls a device flag every few iterations and so
- * synchronises `stream` periodically. */
+ * Constraints: n == tx*rx, tx <= 32, rx <= 32 (tx, rx in {4,8,16,32} in the reference; A2only
+ * with an odd tx <= 31 is solved as the zero-padded (tx + 1) x rx problem in buffers of its own,
+ * `workspace` unused, and returns synchronously), m >= 1, 1 <= r <= 32 (r > 1: shared A only).
+ * Returns once all kernels are enqueued; in convergence mode (fixed_iters == 0) the host polls a
+ * device flag every few iterations and so synchronises `stream` periodically. */
 int ace_admm_solve_batch(const ace_admm_cfg* cfg, int batch, int m, int n, int tx, int rx,
                          const double* A, const double* B, const double* X0,
                          double* X, double* Y, int32_t* iters, uint32_t* status, double* mu,

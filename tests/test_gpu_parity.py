@@ -177,9 +177,36 @@ def test_error_paths(gpu):
     A, B, X0, _ = _problem(1, 1, 16, 4)
     with pytest.raises(AceError):
         infer_admm_host(A, B, X0, 4, 5)            # n != tx*rx
-    A3, B3, X03, _ = _problem(1, 1, 16, 3)
-    with pytest.raises(AceError):
-        infer_admm_host(A3, B3, X03, 3, 3)         # odd tx unsupported for the Jacobi Z-prox
+    with pytest.raises(AceError):                  # tx = 33: beyond the Z-prox's 32 rows (33 + 1 padded)
+        infer_admm_host(np.ones((1, 16, 66), np.complex128), np.ones((1, 16)), np.zeros((1, 66), np.complex128),
+                        33, 2)
+
+
+@pytest.mark.parametrize("tx,rx,m", [(3, 3, 32), (5, 4, 64), (15, 16, 256), (31, 8, 256), (1, 8, 32)])
+def test_a2only_odd_tx(gpu, tx, rx, m):
+    """Odd tx (inferLowRankV4_multi.m:426 reshapes z to tx x rx for any tx): solved as the zero-padded
+    (tx + 1) x rx problem (ace_api.cpp solve_odd_tx), against the C oracle on the tx x rx problem itself:
+    convergence mode (X, Y, iteration counts, converged flags) and 200 fixed iterations, shared and
+    per-realisation A.  Bound: TOL, or 100x the oracle's own move under a 1e-15 perturbation of B where
+    the reference is ill-conditioned (measured: at tx = 1, per-realisation A, one realisation's Y moves 1e-4
+    in the oracle itself -- Y's phase at an entry where AX + M/mu is nearly zero)."""
+    from ace_amd import infer_admm_host, synth
+    for a_shared in (True, False):
+        A, B, X0, _ = synth.problem(31 + tx, 0, 4, m, tx, rx, a_shared=a_shared)
+        U = np.stack([OC.make_U(a) for a in A])
+        res = infer_admm_host(A, B, X0, tx, rx, variant="A2only")
+        Xo, Yo, ito, cvo, _ = OC.infer_admm_r1_batch(A, U, B, X0, tx, rx, variant=0)
+        Xp, Yp, _, _, _ = OC.infer_admm_r1_batch(A, U, B * (1 + 1e-15), X0, tx, rx, variant=0)
+        bx = np.maximum(TOL, 100 * _errs(Xp, Xo))
+        by = np.maximum(TOL, 100 * _errs(Yp, Yo))
+        assert (_errs(res.X, Xo) <= bx).all(), (a_shared, _errs(res.X, Xo), bx)
+        assert (_errs(res.Y, Yo) <= by).all(), (a_shared, _errs(res.Y, Yo), by)
+        assert np.array_equal(res.iters, ito), (res.iters, ito)
+        assert np.array_equal(res.converged, cvo)
+    res = infer_admm_host(A, B, X0, tx, rx, variant="A2only", maxiter=200, fixed_iters=True)
+    Xo, _, ito, _, _ = OC.infer_admm_r1_batch(A, U, B, X0, tx, rx, variant=0, maxiter=200, fixed_iters=True)
+    assert (res.iters == 200).all() and (ito == 200).all()
+    assert _errs(res.X, Xo).max() <= TOL
 
 
 @pytest.mark.parametrize("fixed", [True, False])

@@ -627,7 +627,9 @@ __device__ bool gesdd_vh_square(const BfShared& sh, int n, int ld, int lane) {
 // Vh [n][n] of zgesdd(JOBZ='A') for the m x n matrix in sh.A, into sh.X (m, n <= 32), following zgesdd's
 // path choice (MNTHR1 = INT(MINMN * 17 / 9)): QR first for m >= MNTHR1 (paths 1-4), LQ first for n >= MNTHR1
 // (paths 1t-4t), the matrix itself otherwise (paths 5/6, 5t/6t: upper / lower bidiagonal)
+template <bool RECT>
 __device__ bool gesdd_vh(const BfShared& sh, int m, int n, int ld, int lane) {
+    if constexpr (!RECT) return gesdd_vh_square(sh, n, ld, lane);   // (tx == rx: the square path alone)
     if (n == 1) {
         if (lane == 0) sh.X[0] = make_double2(1.0, 0.0);
         wsync();
@@ -735,6 +737,8 @@ __device__ __forceinline__ unsigned char code_of(int q, bool has_off, double off
     return (unsigned char)c;
 }
 
+// RECT = false: tx == rx (the square path only, which keeps the kernel at four waves per SIMD)
+template <bool RECT>
 __global__ __launch_bounds__(64) void beamformer_kernel(int tx, int rx, const d2* __restrict__ H,
                                                         const double* __restrict__ offset,
                                                         unsigned char* __restrict__ wr_code,
@@ -786,7 +790,7 @@ __global__ __launch_bounds__(64) void beamformer_kernel(int tx, int rx, const d2
             else sh.A[c * ld + r] = Hb[k];
         }
         wsync();
-        ok &= gesdd_vh(sh, m, n, ld, lane);
+        ok &= gesdd_vh<RECT>(sh, m, n, ld, lane);
         signed char* q = pass == 0 ? sh.qr : sh.qt;
         d2* vh_out = pass == 0 ? vh_r : vh_t;
         for (int k = lane; k < n * n; k += 64) {
@@ -867,7 +871,8 @@ extern "C" int ace_svd_beamformer_batch(int batch, int tx, int rx, const double*
     if (!H || !wr_code || !wt_code || !beam_idx || !rss || !status)
         return fail(ACE_ERR_ARG, "svd_beamformer: null output/input pointer");
     const size_t lds = bf_lds_bytes(tx, rx);
-    hipLaunchKernelGGL(beamformer_kernel, dim3(batch), dim3(64), lds, (hipStream_t)stream, tx, rx, (const d2*)H, offset,
+    hipLaunchKernelGGL(tx == rx ? beamformer_kernel<false> : beamformer_kernel<true>, dim3(batch), dim3(64), lds,
+                       (hipStream_t)stream, tx, rx, (const d2*)H, offset,
                        wr_code, wt_code, beam_idx, rss, status, (d2*)vh_r, (d2*)vh_t);
     ACE_HIP(hipGetLastError());
     return ACE_OK;

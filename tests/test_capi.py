@@ -59,7 +59,7 @@ def test_workspace_size():
 
 @pytest.mark.parametrize("kw,tx,rx,msg", [
     ({}, 4, 5, "tx*rx"),
-    ({}, 3, 3, "even tx"),
+    ({}, 33, 1, "tx in [1,32]"),   # (odd tx <= 31 is padded to tx + 1 rows; 33 would need 34)
     ({"variant": 7}, 4, 4, "unknown variant"),
     ({"maxiter": 0}, 4, 4, "maxiter"),
     ({"mu0": 0.0}, 4, 4, "mu0"),
@@ -70,7 +70,7 @@ def test_validation_errors(kw, tx, rx, msg):
     """Validation runs before any HIP call; NULL buffers make a missed check fail safely."""
     import ace_amd
     c = ace_amd.default_cfg(**kw)
-    n = 16 if tx * rx != 9 else 9
+    n = 16 if msg == "tx*rx" else tx * rx
     rc = ace_amd.LIB.ace_admm_solve_batch(C.byref(c), 1, 4, n, tx, rx, None, None, None, None, None, None, None,
                                           None, None, 0, None)
     assert rc in (ace_amd._lib.ACE_ERR_ARG, ace_amd._lib.ACE_ERR_UNSUPPORTED)

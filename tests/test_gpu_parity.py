@@ -182,6 +182,21 @@ def test_error_paths(gpu):
                         33, 2)
 
 
+def test_a2only_odd_tx_device_path(gpu):
+    """The device entry (torch tensors, torch's stream, a caller workspace it does not need) at an odd tx:
+    the same X as the host entry, bit for bit."""
+    import torch
+    from ace_amd import infer_admm_batch, infer_admm_host, synth
+    A, B, X0, _ = synth.problem(77, 0, 64, 256, 15, 16)
+    ref = infer_admm_host(A, B, X0, 15, 16, variant="A2only", maxiter=200, fixed_iters=True)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        dev = infer_admm_batch(torch.from_numpy(A).cuda(), torch.from_numpy(B).cuda(), torch.from_numpy(X0).cuda(),
+                               15, 16, variant="A2only", maxiter=200, fixed_iters=True)
+    s.synchronize()
+    np.testing.assert_array_equal(dev.X.cpu().numpy(), ref.X)
+
+
 @pytest.mark.parametrize("tx,rx,m", [(3, 3, 32), (5, 4, 64), (15, 16, 256), (31, 8, 256), (1, 8, 32)])
 def test_a2only_odd_tx(gpu, tx, rx, m):
     """Odd tx (inferLowRankV4_multi.m:426 reshapes z to tx x rx for any tx): solved as the zero-padded

@@ -732,9 +732,9 @@ __device__ __forceinline__ void bt_decode(int g, int nc, int& b, int& c) {
 // row_shr:1 inside the 16-lane row), lane 0's the next untouched row of z, and the bottom row becomes the gap.  The
 // window index rotates through the registers (the time loop is unrolled by 16).  A lane writes its rows out after
 // its last reflector (sweep 0): they are final then (every later reflector of the schedule lies below them).
-// The work-group's 8 waves (32 vectors) share the reflectors, staged in LDS 8 time steps at a time (the layout
-// q2_index makes a time step's reflectors contiguous), double-buffered, one barrier per 8 time steps.
-constexpr int Q2_THREADS = 512, Q2_NV = Q2_THREADS / 16, Q2_BLK = 8;   // (214 VGPRs: 2 waves per SIMD)
+// The work-group's 8 waves (32 vectors) share the reflectors, staged in LDS 16 time steps at a time (the layout
+// q2_index makes a time step's reflectors contiguous), double-buffered, one barrier pair per 16 time steps.
+constexpr int Q2_THREADS = 512, Q2_NV = Q2_THREADS / 16, Q2_BLK = 16;   // (252 VGPRs: 2 waves per SIMD; LDS 136 KB)
 constexpr int Q2_BLKE = Q2_BLK * 17 * 16;   // staged entries (complex) per block of time steps
 __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int batch, int nc, const double* scratch,
                                                            HeevLayout hl, const double* xs, H2Lay xl, double* Vout,
@@ -787,10 +787,10 @@ __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int 
     auto run_block = [&](int blk, auto moff_c) {
         constexpr int MOFF = decltype(moff_c)::value;
         const d2* vb = vs[blk & 1];
-        if (MOFF == 0) {   // the next 16 untouched rows of z, d - 2 - t0 - j, one per lane of the group (loaded a
-                           // 16-step block ahead)
+        if (MOFF % 16 == 0) {   // the next 16 untouched rows of z, d - 2 - t0 - j, one per lane of the group (loaded
+                                // a 16-step period ahead)
             zin = zin_next;
-            const int zr = d - 2 - (blk + 2) * Q2_BLK - j;
+            const int zr = d - 2 - (blk + 16 / Q2_BLK) * Q2_BLK - j;
             zin_next = (has_vec && zr >= 0) ? zv[zr] : 0.0;
         }
 #pragma unroll
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(Q2_THREADS) void bt2q2_kernel(int d, int kmax, int 
                 }
             }
             // shift: the new top row from lane j - 1's gap (lane 0: z), the bottom row becomes the gap
-            const double nz = __shfl(zin, (lane & 48) | mm, 64);
+            const double nz = __shfl(zin, (lane & 48) | (mm & 15), 64);
             d2 top = make_double2(row_shr1(gap.x), row_shr1(gap.y));
             if (j == 0) top = make_double2(nz, 0.0);
             gap = win[(15 - mm) & 15];
